@@ -1,0 +1,98 @@
+/* cpuref -- CPU restatement of winmad/Winmad-s-raytracer-v1.0's BDPT / PT hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle: tests/, the smoke()
+ * check in __graft_entry__.py and bench.py's cpu_baseline leg load it.  The
+ * shipped renderer (winmad-s-raytracer-v1.0_amd/) never links or calls it.
+ *
+ * Pinned against the reference itself: oracle/_ref/refdrv (the reference's own
+ * translation units, see oracle/Makefile) generated tests/golden/ fixtures; the
+ * `-m "not gpu"` tests check this file against those fixtures bit for bit.
+ *
+ * Arithmetic mirrors the reference statement by statement (float, left-to-right,
+ * no FMA contraction: build with -ffp-contract=off), so MT-serial mode replays the
+ * reference's film exactly.  Counter mode swaps the single MT19937 stream for the
+ * per-subpath counter RNG the HIP path uses (DESIGN.md "Counter RNG").
+ */
+#ifndef WINMAD_CPUREF_H
+#define WINMAD_CPUREF_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cr_scene cr_scene;
+
+enum { CR_RNG_MT = 0, CR_RNG_COUNTER = 1 };
+
+typedef struct {
+    int64_t closest_rays;  /* Scene::intersect traversals            */
+    int64_t shadow_rays;   /* Scene::occluded traversals             */
+    int64_t inner_visits;  /* KD inner nodes visited (all traversals) */
+    int64_t leaf_visits;
+    int64_t prim_refs;     /* leaf primitive references read          */
+    int64_t tri_tests;     /* Triangle::hit calls inside traverse()   */
+    int64_t sph_tests;
+    double seconds;
+} cr_stats;
+
+/* Load a .scene (scene.cpp:259-467) and build the KD tree (scene.cpp:469-489).
+ * Returns NULL on error (message via cr_last_error). */
+cr_scene* cr_scene_load(const char* path);
+void cr_scene_free(cr_scene* s);
+const char* cr_last_error(void);
+
+int cr_scene_nobjs(const cr_scene* s);
+int cr_scene_nlights(const cr_scene* s);
+/* Text dump in the same format as `refdrv scene` (oracle/ref_driver.cpp). */
+int cr_scene_dump(const cr_scene* s, const char* out_path);
+
+/* Per ray (9 floats: origin, unnormalised dir, occlusion target):
+ * Scene::intersect(Ray(o,d)) and Scene::occluded(o,d,target).
+ * out_i[3*k] = prim (-1 miss), out_i[3*k+1] = inside, out_i[3*k+2] = matId,
+ * out_f[7*k] = t, p(3), n(3), occ[k] = occluded.  Stats accumulate. */
+void cr_trace(const cr_scene* s, const float* rays9, int64_t n, int32_t* out_i,
+              float* out_f, uint8_t* occ, cr_stats* st);
+
+/* BDPT (bidirPathTracing.cpp:5-665).  film: H*W*3 floats, film[x][y] layout of
+ * ImageFilm (pre-transpose), ACCUMULATED (not scaled by 1/iterations).
+ * Iterations [iter_begin, iter_begin + iterations).  Paths restricted to
+ * [path_begin, path_end) (full frame: 0, W*H) -- used only to time a bounded
+ * CPU sample.  control_length 3 = reference; <= 0 disables the length filter. */
+int cr_render_bdpt(const cr_scene* s, int W, int H, int iter_begin, int iterations,
+                   uint32_t seed, int rng_mode, int control_length, int64_t path_begin,
+                   int64_t path_end, float* film, cr_stats* st);
+
+/* PT (pathIntegrator.cpp:29-148 + surfaceIntegrator.cpp:14-46); film scaled by 1/spp. */
+int cr_render_pt(const cr_scene* s, int W, int H, int spp, int max_depth, uint32_t seed,
+                 int rng_mode, int64_t pix_begin, int64_t pix_end, float* film, cr_stats* st);
+
+/* Counter RNG (shared spec with the HIP path). */
+uint64_t cr_stream_key(uint32_t seed, uint32_t iteration, uint32_t subpath, uint32_t path);
+uint32_t cr_stream_u32(uint64_t key, uint32_t index);
+
+/* MT19937 (rng.cpp) -- first n outputs for a seed. */
+void cr_mt_outputs(uint32_t seed, int n, uint32_t* out);
+
+/* Known-answer hooks for the component fixtures (tests/golden/kat_*). */
+void cr_kat_sampler(const float* u, float power, float* out /* 3 cosh + pdf, 3 pcosh + pdf + pdf2 */);
+void cr_kat_triangle(const float* u, const float* p012, float* out3);
+void cr_kat_frame(const float* z, float* out9);
+float cr_kat_fresnel(float cosi, float idx);
+void cr_kat_strat(const float* u, int k, int tot, float* out3);
+/* BSDF(wi, inter{n, matId}) then f / pdf / sample: returns valid flag.
+ * out: isDelta, cosWi, contProb, fresnel, 4 probs, f(3), cosWo, dirPdf, revPdf,
+ *      pdf(dir), pdf(rev), type, sample(3), wo(3), spdf, scos   (26 floats) */
+int cr_kat_bsdf(const cr_scene* s, int matId, const float* n, const float* wi,
+                const float* wo, const float* r3, float* out);
+/* out: illuminance(3) dirToLight(3) dist dpdf epdf cal | emit(3) pos(3) dir(3) emp dpa cal
+ *      | radiance(3) dpa epdf   (30 floats) */
+void cr_kat_light(const cr_scene* s, int li, const float* pos, const float* r3,
+                  const float* dr, const float* pr, const float* rd, float* out);
+/* out: ray origin(3) dir(3), raster(3), check */
+void cr_kat_camera(const cr_scene* s, float x, float y, const float* w, float* out10);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

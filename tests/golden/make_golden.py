@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/ from the reference itself.
+
+Test infrastructure: runs oracle/_ref/refdrv -- the reference's own translation
+units compiled from /root/reference by `make -C oracle ref` -- and stores its
+outputs as fixtures.  Only data is written here (inputs and expected outputs);
+no reference source text.  Needs /root/reference (this container only); the GPU
+box uses the committed fixtures.
+
+    python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "winmad-s-raytracer-v1.0_amd"))
+from winmad_rt import scenes  # noqa: E402
+
+REFDRV = os.path.join(REPO, "oracle", "_ref", "refdrv")
+
+
+def refdrv(*args, cwd):
+    env = dict(os.environ, REFDRV_CWD=cwd)
+    return subprocess.run([REFDRV, *map(str, args)], check=True, capture_output=True,
+                          text=True, env=env).stdout
+
+
+def sha(text):
+    return hashlib.sha256(text.encode()).hexdigest()
+
+
+def ray_corpus(scene_dump, n, seed):
+    """Half camera-like rays from the camera position through random raster
+    points of the scene's own camera, half random rays inside the root box;
+    occlusion targets are random points (half of them on the first hit of a
+    pilot ray are not needed: occlusion is checked both ways by mixing near and
+    far targets)."""
+    rng = np.random.default_rng(seed)
+    lines = scene_dump.splitlines()
+    cam = [float.fromhex(t) for t in next(l for l in lines if l.startswith("camera")).split()[1:]]
+    kd = [float.fromhex(t) for t in next(l for l in lines if l.startswith("kd ")).split()[2:]]
+    lo, hi = np.array(kd[:3]), np.array(kd[3:6])
+    pos = np.array(cam[:3])
+    out = np.zeros((n, 9), np.float32)
+    h = n // 2
+    tgt = lo + (hi - lo) * rng.random((h, 3))
+    out[:h, 0:3] = pos
+    out[:h, 3:6] = tgt - pos
+    out[:h, 6:9] = lo + (hi - lo) * rng.random((h, 3))
+    o = lo + (hi - lo) * rng.random((n - h, 3))
+    d = rng.normal(size=(n - h, 3))
+    out[h:, 0:3] = o
+    out[h:, 3:6] = d
+    out[h:, 6:9] = o + d * rng.random((n - h, 1)) * np.linalg.norm(hi - lo)
+    return out
+
+
+def main():
+    if not os.path.exists(REFDRV):
+        sys.exit("build the reference driver first: make -C oracle ref")
+    tmp = tempfile.mkdtemp(prefix="wr_golden_")
+    meta = {}
+    # MT19937 streams (rng.cpp)
+    for seed in (5489, 12345):
+        txt = refdrv("mt", seed, 2000, cwd=tmp)
+        with open(os.path.join(HERE, f"mt_{seed}.txt"), "w") as f:
+            f.write(txt)
+    cases = {
+        "torus64": (scenes.torus_scene(64, 64), scenes.params_text(64, 64)),
+        "torus256": (scenes.torus_scene(256, 256), scenes.params_text(256, 256)),
+        "cbox64x48": (scenes.cbox_scene(64, 48), scenes.params_text(64, 48, 7, 16)),
+    }
+    for name, (sc, pa) in cases.items():
+        sp = scenes.write(os.path.join(tmp, name + ".scene"), sc)
+        pp = scenes.write(os.path.join(tmp, name + ".para"), pa)
+        dump = refdrv("scene", sp, pp, cwd=tmp)
+        lines = dump.splitlines()
+        meta[name] = {
+            "scene_sha256": sha(dump),
+            "nobjs": int(lines[0].split()[1]),
+            "inner": sum(1 for l in lines if l.startswith("I ")),
+            "leaves": sum(1 for l in lines if l.startswith("L ")),
+            "refs": sum(int(l.split()[1]) for l in lines if l.startswith("L ")),
+            "depmax": int(next(l for l in lines if l.startswith("kd ")).split()[1]),
+        }
+        if name == "torus256":
+            continue
+        corpus = ray_corpus(dump, 2048 if name == "torus64" else 1024, 99)
+        cp = os.path.join(HERE, f"rays_{name}.f32")
+        corpus.tofile(cp)
+        # second pass: every other hitting ray gets its own hit point as the
+        # occlusion target, so both outcomes of the position-equality test
+        # (scene.cpp:65) are covered
+        for k, line in enumerate(refdrv("rays", sp, pp, cp, cwd=tmp).splitlines()):
+            tok = line.split()
+            if tok[0] != "-1" and k % 2 == 0:
+                corpus[k, 6:9] = [float.fromhex(t) for t in tok[2:5]]
+        corpus.tofile(cp)
+        with open(os.path.join(HERE, f"rays_{name}.txt"), "w") as f:
+            f.write(refdrv("rays", sp, pp, cp, cwd=tmp))
+        with open(os.path.join(HERE, f"kat_{name}.txt"), "w") as f:
+            f.write(refdrv("kat", sp, pp, 128, 777, cwd=tmp))
+    # films (pre-transpose, accumulated), MT-serial
+    for name, it, seed in (("torus64", 1, 5489), ("torus64", 4, 5489), ("torus64", 2, 7)):
+        sp, pp = os.path.join(tmp, name + ".scene"), os.path.join(tmp, name + ".para")
+        out = os.path.join(HERE, f"bdpt_{name}_i{it}_s{seed}.f32")
+        refdrv("bdpt", sp, pp, it, seed, out, cwd=tmp)
+    sp, pp = os.path.join(tmp, "torus256.scene"), os.path.join(tmp, "torus256.para")
+    tmpf = os.path.join(tmp, "b256.f32")
+    refdrv("bdpt", sp, pp, 4, 5489, tmpf, cwd=tmp)
+    film = np.fromfile(tmpf, np.float32).reshape(256, 256, 3)
+    meta["bdpt_torus256_i4_s5489"] = {
+        "mean": film.mean(axis=(0, 1)).tolist(),
+        "rms": float(np.sqrt((film.astype(np.float64) ** 2).mean())),
+        "block32_mean": film.reshape(8, 32, 8, 32, 3).mean(axis=(1, 3)).tolist(),
+        "sha256": hashlib.sha256(film.tobytes()).hexdigest(),
+    }
+    sp, pp = os.path.join(tmp, "cbox64x48.scene"), os.path.join(tmp, "cbox64x48.para")
+    refdrv("pt", sp, pp, 5489, os.path.join(HERE, "pt_cbox64x48_spp16_s5489.f32"), cwd=tmp)
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print(json.dumps({k: v for k, v in meta.items() if "block32_mean" not in v}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
