@@ -1,0 +1,156 @@
+/* winmad_rt.h -- C ABI of the MI355X-native BDPT / PT hot path.
+ *
+ * Drop-in boundary for winmad/Winmad-s-raytracer-v1.0 (paths below are relative
+ * to /root/reference/Winmad-s-raytracer-v1.0/src).  The reference has no FFI;
+ * its seam is the C++ class SurfaceIntegrator (surfaceIntegrator/surfaceIntegrator.h:14-34)
+ * with Scene::intersect / Scene::occluded below it.  Each entry point names the
+ * reference interface it replaces.  INTEGRATION.md shows the C++ / ctypes
+ * bindings a maintainer adds on the reference side.
+ *
+ * Conventions (all functions):
+ *   - return 0 on success, a negative WR_E* code on failure; never throw;
+ *     the message of the last failure on this thread is wr_last_error();
+ *   - plain pointers and sizes only; the caller owns every input / output buffer;
+ *   - a wr_context is used by one host thread at a time; it owns one HIP stream on
+ *     one device.  Multi-GPU = one process (one context) per GPU; see DESIGN.md.
+ */
+#ifndef WINMAD_RT_H
+#define WINMAD_RT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WR_API_VERSION 1
+
+enum {
+  WR_OK = 0,
+  WR_E_ARG = -1,      /* bad argument                                  */
+  WR_E_IO = -2,       /* scene / obj file unreadable or malformed      */
+  WR_E_HIP = -3,      /* HIP runtime error (no device, OOM, launch)    */
+  WR_E_SCENE = -4,    /* scene lacks what the call needs (lights, ...) */
+  WR_E_NODEVICE = -5  /* the HIP extension found no gfx950 device       */
+};
+
+typedef struct wr_scene wr_scene;     /* host-side loaded scene + KD tree */
+typedef struct wr_context wr_context; /* scene resident in HBM + stream  */
+
+/* Ray (geometry/ray.h:6-32).  `d` is used as given: callers normalise it as
+ * the Ray constructor does (ray.h:14-21).  The reference always has tmin = 0,
+ * tmax = INF (1e7). */
+typedef struct {
+  float o[3];
+  float d[3];
+  float tmin, tmax;
+} wr_ray; /* 32 bytes */
+
+/* Intersection (geometry/intersection.h:6-19) + index of the winning primitive
+ * in the reference's `Scene::objs` order (-1 = miss). */
+typedef struct {
+  float t;
+  float p[3];
+  float n[3];
+  int32_t prim;
+  int32_t inside;
+  int32_t mat_id;
+} wr_hit; /* 40 bytes */
+
+typedef struct {
+  int32_t nprims, ntriangles, nspheres, nlights, nmaterials;
+  int32_t kd_depth_max;   /* depMax = int(1.2 ln N + 2) (KDtreeAccel.cpp:16) */
+  int32_t kd_inner, kd_leaves;
+  int64_t kd_refs;
+  int32_t kd_max_stack;   /* traversal stack depth bound                    */
+  int32_t missing_files;  /* .obj files the reference would silently skip   */
+  float camera_xres, camera_yres;
+  int64_t device_bytes;   /* bytes this scene occupies in HBM               */
+} wr_scene_info;
+
+/* BidirPathTracing knobs (bidirPathTracing.cpp:5-21). */
+typedef struct {
+  int32_t width, height;     /* Parameters WIDTH / HEIGHT; the film is height x width x 3   */
+  int32_t iterations;        /* samples per pixel = iterations (hard-coded 1 in the reference) */
+  int32_t iter_begin;        /* global index of the first iteration (RNG key; sharding)     */
+  int32_t control_length;    /* 3 = reference filter; <= 0 accumulates every path length     */
+  int32_t max_path_length;   /* 10 in the reference                                          */
+  uint32_t seed;
+  int32_t faithful;          /* 1: trace every ray the reference traces (default);
+                                0: skip shadow rays whose contribution is filtered out       */
+  int32_t time_kernels;      /* 1: HIP events around every launch -> wr_stats.kernel_ms      */
+  int32_t count_work;        /* 1: per-traversal node / ref counters -> wr_stats              */
+} wr_bdpt_params;
+
+/* PathIntegrator knobs (pathIntegrator.cpp:3-15, parameters.para). */
+typedef struct {
+  int32_t width, height;
+  int32_t spp;               /* SAMPLES_PER_PIXEL: the stratification grid (surfaceIntegrator.cpp:26-32) */
+  int32_t max_depth;         /* MAX_TRACING_DEPTH                                          */
+  int32_t sample_begin;      /* first sample index k rendered (RNG key; sharding)          */
+  int32_t sample_count;      /* samples rendered by this call (<= 0: spp - sample_begin)   */
+  uint32_t seed;
+  int32_t time_kernels;
+  int32_t count_work;
+} wr_path_params;
+
+enum { WR_K_TRACE = 0, WR_K_SHADE = 1, WR_K_RESOLVE = 2, WR_K_GEN = 3, WR_K_OTHER = 4, WR_K_NUM = 8 };
+
+typedef struct {
+  int64_t closest_rays;      /* Scene::intersect traversals                 */
+  int64_t shadow_rays;       /* Scene::occluded traversals                  */
+  int64_t inner_visits;      /* count_work only                             */
+  int64_t leaf_visits;
+  int64_t prim_refs;         /* = triangle / sphere tests                   */
+  double seconds;            /* host wall time of the call (stream synced)  */
+  double kernel_ms[WR_K_NUM];      /* time_kernels only: summed launch durations */
+  int64_t kernel_launches[WR_K_NUM];
+} wr_stats;
+
+/* ---- scene (Scene::init, scene/scene.cpp:469-489 + loadScene :259-467) ---- */
+int wr_scene_load(const char* scene_path, wr_scene** out);
+int wr_scene_info_get(const wr_scene* scene, wr_scene_info* out);
+/* Text dump in the format of oracle/ref_driver.cpp `scene` (parity tests). */
+int wr_scene_dump(const wr_scene* scene, const char* out_path);
+void wr_scene_free(wr_scene* scene);
+
+/* ---- device context ---- */
+int wr_device_count(void);
+int wr_create(const wr_scene* scene, int hip_device, wr_context** out);
+void wr_destroy(wr_context* ctx);
+
+/* ---- traversal ---- */
+/* Scene::intersect (scene/scene.cpp:21-43) -> KDtreeAccel::traverse
+ * (scene/KDtreeAccel.cpp:309-388).  Host arrays of n rays / hits. */
+int wr_trace_closest(wr_context* ctx, const wr_ray* rays, int64_t n, wr_hit* hits);
+/* Scene::occluded (scene/scene.cpp:55-81): a closest-hit traversal of
+ * Ray(o, d) (d re-normalised as the Ray constructor does) whose answer is
+ * "not occluded" iff it misses or its hit point equals targets[3k..3k+2]
+ * within EPS per component. */
+int wr_occluded(wr_context* ctx, const wr_ray* rays, const float* targets, int64_t n, uint8_t* occluded);
+
+/* ---- integrators ---- */
+/* BidirPathTracing::render (surfaceIntegrator/bidirPathTracing.cpp:23-27,
+ * runIteration :53-265).  film: height*width*3 floats in ImageFilm layout
+ * film[x_raster][y_raster] (pre-transpose), accumulated (+=), NOT scaled by
+ * 1/iterations.  film_on_device != 0: `film` is a device pointer on the
+ * context's device. */
+int wr_render_bdpt(wr_context* ctx, const wr_bdpt_params* p, float* film, int film_on_device, wr_stats* stats);
+/* SurfaceIntegrator::render (surfaceIntegrator.cpp:14-46) + PathIntegrator::raytracing
+ * (pathIntegrator.cpp:29-148).  film[height][width][3] accumulates the per-sample
+ * radiance SUM (the reference's final film->scale(1/spp) is left to the caller). */
+int wr_render_path(wr_context* ctx, const wr_path_params* p, float* film, int film_on_device, wr_stats* stats);
+
+/* ---- output (ImageFilm::outputImage, scene/film.cpp:39-64; BDPT transpose
+ * bidirPathTracing.cpp:29-46) ---- scale -> clamp [0,1] -> pow(1/gamma) ->
+ * (uchar)(x*255.0); binary PPM (RGB).  transpose != 0 swaps [i][j] <-> [j][i]
+ * first (square films only, as the reference). */
+int wr_film_write_ppm(const float* film, int height, int width, float scale, float gamma, int transpose,
+                      const char* path);
+
+const char* wr_last_error(void);
+int wr_api_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WINMAD_RT_H */

@@ -1,0 +1,95 @@
+#include "integrators.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+
+namespace winmad {
+namespace {
+void ok(int rc) {
+  if (rc != WR_OK) throw std::runtime_error(std::string("winmad_rt: ") + wr_last_error());
+}
+}  // namespace
+
+void Parameters::load_parameters(const char* filename) {
+  FILE* fp = std::fopen(filename, "r");
+  if (!fp) throw std::runtime_error(std::string("cannot open parameter file ") + filename);
+  int* slots[8] = {&MAX_TRACING_DEPTH, &SAMPLES_PER_PIXEL, &SAMPLES_OF_LIGHT, &SAMPLES_OF_HEMISPHERE,
+                   &WIDTH, &HEIGHT, &PHONG_POWER_INDEX, &POINT_LIGHT_NUM};
+  char tok[1024];
+  int k = 0;
+  while (k < 8 && std::fscanf(fp, "%1023s", tok) == 1) {
+    if (tok[0] == '#') continue;  // read_int (parameters.cpp:9-20)
+    *slots[k++] = std::atoi(tok);
+  }
+  for (; k < 8; ++k) *slots[k] = -1;  // read_int returns -1 at EOF
+  std::fclose(fp);
+}
+
+SurfaceIntegrator::~SurfaceIntegrator() {
+  if (ctx_) wr_destroy(ctx_);
+  if (scene_) wr_scene_free(scene_);
+}
+
+void SurfaceIntegrator::load(const char* filename) {
+  ok(wr_scene_load(filename, &scene_));
+  ok(wr_create(scene_, device, &ctx_));
+  film.assign(static_cast<size_t>(height) * width * 3, 0.f);
+}
+
+void BidirPathTracing::init(const char* filename, Parameters& para) {
+  samplesPerPixel = para.SAMPLES_PER_PIXEL;  // stored, unused by BDPT (:11)
+  height = para.HEIGHT;
+  width = para.WIDTH;
+  load(filename);
+}
+
+void BidirPathTracing::render() {
+  wr_bdpt_params p{};
+  p.width = width;
+  p.height = height;
+  p.iterations = iterations;
+  p.iter_begin = 0;
+  p.control_length = controlLength;
+  p.max_path_length = maxPathLength;
+  p.seed = seed;
+  p.faithful = 1;
+  ok(wr_render_bdpt(ctx_, &p, film.data(), 0, &stats));
+}
+
+void BidirPathTracing::outputImage(const char* filename) {
+  // The reference transposes in place assuming height == width (:31-44);
+  // only square films are transposed here (non-square reference output is corrupt).
+  ok(wr_film_write_ppm(film.data(), height, width, 1.f / iterations, 2.2f, height == width, filename));
+}
+
+void PathIntegrator::init(const char* filename, Parameters& para) {
+  maxTracingDepth = para.MAX_TRACING_DEPTH;
+  samplesPerPixel = para.SAMPLES_PER_PIXEL;
+  samplesOfLight = para.SAMPLES_OF_LIGHT;
+  samplesOfHemisphere = para.SAMPLES_OF_HEMISPHERE;
+  height = para.HEIGHT;
+  width = para.WIDTH;
+  load(filename);
+}
+
+void PathIntegrator::render() {
+  wr_path_params p{};
+  p.width = width;
+  p.height = height;
+  p.spp = samplesPerPixel;
+  p.max_depth = maxTracingDepth;
+  p.sample_begin = 0;
+  p.sample_count = samplesPerPixel;
+  p.seed = seed;
+  ok(wr_render_path(ctx_, &p, film.data(), 0, &stats));
+  const float inv = 1.f / samplesPerPixel;  // film->scale(1.f / samplesPerPixel) (:45)
+  for (float& v : film) v = v * inv;
+}
+
+void PathIntegrator::outputImage(const char* filename) {
+  ok(wr_film_write_ppm(film.data(), height, width, 1.f, 2.2f, 0, filename));
+}
+
+}  // namespace winmad

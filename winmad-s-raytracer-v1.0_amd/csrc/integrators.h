@@ -1,0 +1,65 @@
+// C++ host mirror of the reference's integrator seam, over the C ABI.
+//
+// The reference's drop-in point is SurfaceIntegrator
+// (src/surfaceIntegrator/surfaceIntegrator.h:14-34): main() picks an integrator by
+// flag and calls init(scene, para) / render() / outputImage(path)
+// (src/main.cpp:40-45 for -p, :65-70 for -bpt).  These classes keep those names
+// and that call order; the work happens on the GPU through include/winmad_rt.h.
+// Where the reference would crash (missing scene, no lights) these throw
+// std::runtime_error carrying wr_last_error().
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "winmad_rt.h"
+
+namespace winmad {
+
+// src/parameters.h / parameters.cpp:22-34 -- 8 positional ints, '#' lines skipped
+class Parameters {
+ public:
+  int MAX_TRACING_DEPTH = 7, SAMPLES_PER_PIXEL = 1, SAMPLES_OF_LIGHT = 8, SAMPLES_OF_HEMISPHERE = 4;
+  int WIDTH = 512, HEIGHT = 512, PHONG_POWER_INDEX = 5, POINT_LIGHT_NUM = 400;
+  void load_parameters(const char* filename);
+};
+
+class SurfaceIntegrator {
+ public:
+  int width = 0, height = 0, samplesPerPixel = 0;
+  int device = 0;
+  std::vector<float> film;  // ImageFilm color[height][width] (r, g, b)
+  wr_stats stats{};
+  virtual ~SurfaceIntegrator();
+  virtual void init(const char* filename, Parameters& para) = 0;
+  virtual void render() = 0;
+  virtual void outputImage(const char* filename) = 0;
+
+ protected:
+  wr_scene* scene_ = nullptr;
+  wr_context* ctx_ = nullptr;
+  void load(const char* filename);
+};
+
+// src/surfaceIntegrator/bidirPathTracing.{h,cpp}
+class BidirPathTracing : public SurfaceIntegrator {
+ public:
+  int minPathLength = 0, maxPathLength = 10, controlLength = 3;
+  int iterations = 1;  // bidirPathTracing.cpp:9
+  uint32_t seed = 5489;
+  void init(const char* filename, Parameters& para) override;  // :5-21
+  void render() override;                                        // :23-27
+  void outputImage(const char* filename) override;               // :29-46
+};
+
+// src/surfaceIntegrator/pathIntegrator.{h,cpp} + SurfaceIntegrator::render
+class PathIntegrator : public SurfaceIntegrator {
+ public:
+  int maxTracingDepth = 7, samplesOfLight = 8, samplesOfHemisphere = 4;
+  uint32_t seed = 5489;
+  void init(const char* filename, Parameters& para) override;  // pathIntegrator.cpp:3-15
+  void render() override;                                        // surfaceIntegrator.cpp:14-46
+  void outputImage(const char* filename) override;               // surfaceIntegrator.cpp:47-50
+};
+
+}  // namespace winmad

@@ -1,0 +1,1611 @@
+// MI355X (gfx950) implementation of the reference's hot path behind the C ABI of
+// include/winmad_rt.h:
+//   * KD-tree closest-hit traversal (wr_traverse.h) as one generic queue kernel
+//   * BidirPathTracing::runIteration (bidirPathTracing.cpp:53-265) as a wavefront:
+//       light pass  : gen -> [trace -> shade] x 9 -> trace(splat rays) -> resolve
+//       camera pass : gen -> [trace -> shade -> trace(shadow+aux) -> resolve -> DI] x 10
+//     path state lives in SoA buffers sized for the whole frame; queues are
+//     compacted with wave ballots + one atomic per wave
+//   * PathIntegrator::raytracing (pathIntegrator.cpp:29-148), one sample index per
+//     wavefront iteration
+//
+// Work is keyed by (iteration, path index) through the counter RNG, never by the
+// device or launch geometry, so any sharding of iterations over GPUs renders the
+// same film up to float summation order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "winmad_rt.h"
+#include "wr_scene.h"
+#include "wr_traverse.h"
+
+using namespace wrd;
+
+// =============================================================== errors
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess) return fail(WR_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+// =============================================================== device helpers
+namespace {
+
+constexpr int kVMax = 9;       // light vertices per subpath (pathLength 1..9, :77-124)
+constexpr int kTraceBlock = 128;
+constexpr int kShadeBlock = 256;
+
+enum SqKind { SQ_SPLAT = 0, SQ_CONN = 1, SQ_NEE = 2, SQ_DIB = 3 };
+enum DiFlag { DI_NEE = 1, DI_BSDF = 2, DI_EARLY = 4 };
+
+struct DevCounters {
+  int ext_count[2];
+  int sq_count;
+  int di_count;
+  unsigned long long closest, shadow, inner, leaves, refs;
+};
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// One atomic per wave: returns this lane's slot (or -1 if !want).
+__device__ __forceinline__ int wave_append(int* counter, bool want) {
+  const unsigned long long m = __ballot(want);
+  if (m == 0ull) return -1;
+  const int lane = lane_id();
+  const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader);
+  return want ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+__device__ __forceinline__ void wave_count(unsigned long long* counter, bool c) {
+  const unsigned long long m = __ballot(c);
+  if (m == 0ull) return;
+  if (lane_id() == __ffsll(static_cast<unsigned long long>(m)) - 1) atomicAdd(counter, (unsigned long long)__popcll(m));
+}
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ V3 ld3(const float* b, int stride, int i) {
+  return v3(b[i], b[stride + i], b[2 * stride + i]);
+}
+__device__ __forceinline__ void st3(float* b, int stride, int i, V3 v) {
+  b[i] = v.x;
+  b[stride + i] = v.y;
+  b[2 * stride + i] = v.z;
+}
+__device__ __forceinline__ void film_add(float* film, int pix, V3 v) {
+  if (pix < 0) return;
+  if (v.x != 0.f) atomicAdd(film + 3 * pix, v.x);
+  if (v.y != 0.f) atomicAdd(film + 3 * pix + 1, v.y);
+  if (v.z != 0.f) atomicAdd(film + 3 * pix + 2, v.z);
+}
+// ImageFilm::addColor bounds check (film.cpp:4-9) -> flat pixel or -1
+__device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
+  return (h < 0 || h >= H || w < 0 || w >= W) ? -1 : h * W + w;
+}
+
+// =============================================================== trace kernels
+// Generic queue traversal: rays [3][cap] SoA, count on device.
+template <bool COUNT>
+__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, const float* __restrict__ o3,
+                                                       const float* __restrict__ d3, int cap,
+                                                       const int* __restrict__ count, float* __restrict__ out_t,
+                                                       int* __restrict__ out_prim, DevCounters* ctr) {
+  extern __shared__ uint32_t smem[];
+  const int stride = blockDim.x;
+  uint32_t* sn = smem + threadIdx.x;
+  float* s0 = reinterpret_cast<float*>(smem + S.max_stack * stride) + threadIdx.x;
+  float* s1 = reinterpret_cast<float*>(smem + 2 * S.max_stack * stride) + threadIdx.x;
+  const int n = *count;
+  TraceCounters tc{0, 0, 0};
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const V3 o = ld3(o3, cap, i), d = ld3(d3, cap, i);
+    float t;
+    const int prim = traverse<COUNT>(S, o, d, 0.f, WR_INF, t, sn, s0, s1, stride, tc);
+    out_t[i] = t;
+    out_prim[i] = prim;
+  }
+  if (COUNT) {
+    unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs);
+    if (lane_id() == 0) {
+      atomicAdd(&ctr->inner, a);
+      atomicAdd(&ctr->leaves, b);
+      atomicAdd(&ctr->refs, c);
+    }
+  }
+}
+
+// C-ABI traversal: AoS wr_ray in, wr_hit (Intersection) / occluded flag out.
+__global__ void __launch_bounds__(kTraceBlock) k_trace_api(DevScene S, const wr_ray* rays, const float* targets,
+                                                           int64_t n, wr_hit* hits, uint8_t* occ) {
+  extern __shared__ uint32_t smem[];
+  const int stride = blockDim.x;
+  uint32_t* sn = smem + threadIdx.x;
+  float* s0 = reinterpret_cast<float*>(smem + S.max_stack * stride) + threadIdx.x;
+  float* s1 = reinterpret_cast<float*>(smem + 2 * S.max_stack * stride) + threadIdx.x;
+  TraceCounters tc{0, 0, 0};
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const wr_ray r = rays[i];
+    V3 o = v3(r.o[0], r.o[1], r.o[2]), d = v3(r.d[0], r.d[1], r.d[2]);
+    if (occ) d = normalize(d);  // Scene::occluded builds Ray(p1, dir) (scene.cpp:74)
+    float t;
+    const int prim = traverse<false>(S, o, d, r.tmin, r.tmax, t, sn, s0, s1, stride, tc);
+    if (occ) {
+      bool unocc = prim < 0 || near_eq(o + d * t, v3(targets[3 * i], targets[3 * i + 1], targets[3 * i + 2]));
+      occ[i] = unocc ? 0 : 1;
+    } else {
+      wr_hit h;
+      h.prim = prim;
+      if (prim >= 0) {
+        Hit x = rebuild_hit(S, prim, t, o, d);
+        h.t = x.t;
+        h.p[0] = x.p.x; h.p[1] = x.p.y; h.p[2] = x.p.z;
+        h.n[0] = x.n.x; h.n[1] = x.n.y; h.n[2] = x.n.z;
+        h.inside = x.inside;
+        h.mat_id = x.mat;
+      } else {
+        h.t = WR_INF;
+        h.p[0] = h.p[1] = h.p[2] = 0.f;
+        h.n[0] = h.n[1] = h.n[2] = 0.f;
+        h.inside = 0;
+        h.mat_id = 0;
+      }
+      hits[i] = h;
+    }
+  }
+}
+
+// =============================================================== BDPT state
+struct BdptBuf {
+  int P = 0, cap_sq = 0;
+  // light subpath state (bidirPathTracing.h:7-18)
+  float *l_o, *l_d, *l_thr, *l_dvcm, *l_dvc;
+  int *l_len, *l_nspec;
+  uint32_t* l_ctr;
+  // stored light vertices [kVMax][...][P]
+  float *v_pos, *v_n, *v_wi, *v_thr, *v_dvcm, *v_dvc, *v_cont, *v_pd, *v_pg;
+  int *v_len, *v_nspec, *v_mat, *v_count;
+  // camera subpath state
+  float *c_o, *c_d, *c_thr, *c_dvcm, *c_dvc;
+  int *c_len, *c_nspec, *c_pix;
+  uint32_t* c_ctr;
+  // extension-ray queues (double buffered)
+  float *q_o[2], *q_d[2], *q_t[2];
+  int *q_path[2], *q_prim[2];
+  // shadow + aux closest-hit queue (splat / connection / NEE / DI-BSDF)
+  float *s_o, *s_d, *s_tgt, *s_val, *s_t;
+  int *s_meta, *s_pix, *s_prim;
+  // direct-illumination records (getDirectIllumination, :484-608)
+  float *di_nee, *di_neew, *di_bsdf, *di_thr, *di_wlen;
+  int *di_flags, *di_light, *di_pix, *di_vis, *di_same, *di_list;
+};
+
+struct BdptArgs {
+  DevScene S;
+  BdptBuf B;
+  DevCounters* ctr;
+  float* film;
+  int W, H, P;
+  uint32_t seed, iter;
+  int ctl, maxlen, faithful;
+};
+
+__device__ __forceinline__ bool len_ok(int ctl, int L) { return ctl <= 0 || L == ctl; }
+
+// generateLightSample (:267-311) + the first extension ray
+__global__ void __launch_bounds__(kShadeBlock) k_light_gen(BdptArgs A) {
+  const BdptBuf& B = A.B;
+  const int P = A.P;
+  const float lpp = 1.f / static_cast<float>(A.S.nlights);
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), 0};
+    const int id = min(static_cast<int>(rng.f() * static_cast<float>(A.S.nlights)), A.S.nlights - 1);
+    const DLight L = A.S.lights[id];
+    V3 pos, dir, rad;
+    float epdf = 0.f, dpdf = 0.f;
+    for (int tries = 0; tries < 64; ++tries) {
+      // emit(..., rng.randVector3(), rng.randVector3(), ...): the reference's
+      // compiler evaluates the second argument (posRand3) first
+      V3 pr = rng.v();
+      V3 dr = rng.v();
+      rad = light_emit(L, dr, pr, &pos, &dir, &epdf, &dpdf);
+      if (epdf > 1e-7f) break;
+    }
+    V3 thr = rad;
+    epdf *= lpp;
+    dpdf *= lpp;
+    thr = div_plain(thr, epdf);
+    st3(B.l_o, P, p, pos);
+    st3(B.l_d, P, p, dir);
+    st3(B.l_thr, P, p, thr);
+    B.l_dvcm[p] = dpdf / epdf;
+    B.l_dvc[p] = 1.f / epdf;  // AreaLight::isDelta() == 0
+    B.l_len[p] = 1;
+    B.l_nspec[p] = 0;
+    B.l_ctr[p] = rng.ctr;
+    B.v_count[p] = 0;
+    // Ray(origin + dir * EPS, dir) (:79-80)
+    st3(B.q_o[0], P, p, pos + dir * WR_EPS);
+    st3(B.q_d[0], P, p, normalize(dir));
+    B.q_path[0][p] = p;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->ext_count[0] = P;
+}
+
+// sampleScattering (:370-416).  Returns false when the subpath ends.
+__device__ __forceinline__ bool sample_scatter(const DevScene& S, Rng& rng, const Bsdf& b, V3 hit, V3& o, V3& dir,
+                                               V3& thr, float& dvcm, float& dvc, int& nspec) {
+  float dpdf = 0.f, cos_wo = 0.f;
+  int type;
+  V3 wo = dir;
+  const V3 f = bsdf_sample(b, S.mats, rng.v(), &wo, &dpdf, &cos_wo, &type);
+  if (black(f)) return false;
+  dir = wo;
+  float rpdf = dpdf;
+  if ((type & T_SPEC) == 0) rpdf = bsdf_pdf(b, S.mats, dir, true);
+  const float cp = b.cont;
+  if (rng.f() > cp) return false;
+  dpdf *= cp;
+  rpdf *= cp;
+  if (type & T_SPEC) {
+    ++nspec;
+    dvcm = 0.f;
+    dvc *= cos_wo;
+  } else {
+    dvc = (1.f / dpdf) * (dvcm + dvc * rpdf);
+    dvcm = 1.f / dpdf;
+  }
+  o = hit;
+  thr = mul(thr, f) * (cos_wo / dpdf);
+  return true;
+}
+
+// One light-subpath vertex (:77-128)
+__global__ void __launch_bounds__(kShadeBlock) k_light_shade(BdptArgs A, int cur) {
+  const BdptBuf& B = A.B;
+  const DevScene& S = A.S;
+  const int P = A.P, nxt = cur ^ 1;
+  const int n = A.ctr->ext_count[cur];
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
+  const int gstride = gridDim.x * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;  // whole waves reach the appends
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    bool ext = false, splat = false;
+    V3 e_o, e_d, s_o, s_d, s_val;
+    int s_pix = -1, p = -1;
+    if (j < n) {
+      p = B.q_path[cur][j];
+      const int prim = B.q_prim[cur][j];
+      if (prim >= 0) {
+        const float t = B.q_t[cur][j];
+        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
+        const Hit h = rebuild_hit(S, prim, t, o, d);
+        Bsdf b;
+        bsdf_init(b, -d, h.n, h.mat, S.mats);
+        if (b.mat != 0) {
+          float dvcm = B.l_dvcm[p], dvc = B.l_dvc[p];
+          int len = B.l_len[p], nspec = B.l_nspec[p];
+          V3 thr = ld3(B.l_thr, P, p);
+          dvcm *= (t * t);  // pathLength > 1 || isFiniteLight: always for area lights (:94-97)
+          dvcm /= fabsf(b.wi.z);
+          dvc /= fabsf(b.wi.z);
+          if (!b.delta) {  // lightStates.push_back (:101-102)
+            const int k = B.v_count[p];
+            const int slot = k * P + p;
+            st3(B.v_pos, kVMax * P, slot, h.p);
+            st3(B.v_n, kVMax * P, slot, h.n);
+            st3(B.v_wi, kVMax * P, slot, b.wi);
+            st3(B.v_thr, kVMax * P, slot, thr);
+            B.v_dvcm[slot] = dvcm;
+            B.v_dvc[slot] = dvc;
+            B.v_cont[slot] = b.cont;
+            B.v_pd[slot] = b.pd;
+            B.v_pg[slot] = b.pg;
+            B.v_len[slot] = len;
+            B.v_nspec[slot] = nspec;
+            B.v_mat[slot] = b.mat;
+            B.v_count[p] = k + 1;
+            if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
+              const DCam& cam = S.cam;
+              const V3 ip = t_point(cam.w2r, h.p);
+              if (check_raster(cam, ip.x, ip.y)) {
+                V3 dtc = cam.pos - h.p;
+                if (dot(-dtc, cam.fwd) > 0) {
+                  const float d2 = sqr_len(dtc);
+                  const float dist = sqrtf(d2);
+                  dtc = div_guarded(dtc, dist);
+                  float cos_to = 0.f, dp, rp;
+                  const V3 f = bsdf_f(b, S.mats, dtc, &cos_to, &dp, &rp);
+                  if (!black(f)) {
+                    rp *= b.cont;
+                    const float cos_at = dot(-dtc, cam.fwd);
+                    const float ipd = cam.plane_dist / cos_at;
+                    const float i2sa = (ipd * ipd) / cos_at;
+                    const float i2s = i2sa * fabsf(cos_to) / d2;
+                    const float pdf_a = i2s;
+                    const float s2i = 1.f / i2s;
+                    const V3 res = div_plain(mul(thr, f), static_cast<float>(P) * s2i);
+                    if (!black(res)) {
+                      const float wl = (pdf_a / static_cast<float>(P)) * (dvcm + rp * dvc);
+                      const float w = 1.f / (wl + 1.f);
+                      splat = true;
+                      s_o = h.p;
+                      s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
+                      s_val = res * w;
+                      s_pix = pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W);
+                    }
+                  }
+                }
+              }
+            }
+          }
+          if (!(len + 2 > A.maxlen)) {  // (:123-127)
+            Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), B.l_ctr[p]};
+            V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
+            if (sample_scatter(S, rng, b, h.p, lo, ld, thr, dvcm, dvc, nspec)) {
+              ext = true;
+              ++len;
+              e_o = lo + ld * WR_EPS;
+              e_d = normalize(ld);
+              st3(B.l_o, P, p, lo);
+              st3(B.l_d, P, p, ld);
+              st3(B.l_thr, P, p, thr);
+              B.l_dvcm[p] = dvcm;
+              B.l_dvc[p] = dvc;
+              B.l_len[p] = len;
+              B.l_nspec[p] = nspec;
+            }
+            B.l_ctr[p] = rng.ctr;
+          }
+        }
+      }
+    }
+    const int ei = wave_append(&A.ctr->ext_count[nxt], ext);
+    if (ext) {
+      st3(B.q_o[nxt], P, ei, e_o);
+      st3(B.q_d[nxt], P, ei, e_d);
+      B.q_path[nxt][ei] = p;
+    }
+    const int si = wave_append(&A.ctr->sq_count, splat);
+    if (splat) {
+      st3(B.s_o, B.cap_sq, si, s_o);
+      st3(B.s_d, B.cap_sq, si, s_d);
+      st3(B.s_tgt, B.cap_sq, si, S.cam.pos);
+      st3(B.s_val, B.cap_sq, si, s_val);
+      B.s_meta[si] = SQ_SPLAT << 30;
+      B.s_pix[si] = s_pix;
+    }
+  }
+}
+
+// generateCameraSample (:418-452) + first extension ray
+__global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptArgs A) {
+  const BdptBuf& B = A.B;
+  const DCam& cam = A.S.cam;
+  const int P = A.P;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), 0};
+    const int y = p % A.W, x = p / A.W;
+    const V3 jit = rng.v();
+    const float sx = static_cast<float>(x) + jit.x, sy = static_cast<float>(y) + jit.y;
+    const V3 rp = t_point(cam.r2w, v3(sx, sy, 0.f));
+    const V3 d = normalize(rp - cam.pos);  // Ray(pos, p - pos) (camera.cpp:37-42)
+    const float cos_at = dot(cam.fwd, d);
+    const float ipd = cam.plane_dist / cos_at;
+    const float i2sa = (ipd * ipd) / cos_at;
+    st3(B.c_o, P, p, cam.pos);
+    st3(B.c_d, P, p, d);
+    st3(B.c_thr, P, p, v3(1.f, 1.f, 1.f));
+    B.c_dvcm[p] = static_cast<float>(P) / i2sa;
+    B.c_dvc[p] = 0.f;
+    B.c_len[p] = 1;
+    B.c_nspec[p] = 0;
+    B.c_ctr[p] = rng.ctr;
+    B.c_pix[p] = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
+    st3(B.q_o[0], P, p, cam.pos + d * WR_EPS);
+    st3(B.q_d[0], P, p, normalize(d));
+    B.q_path[0][p] = p;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->ext_count[0] = P;
+}
+
+// One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
+// connections (shadow rays queued), scattering.
+__global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int cur) {
+  const BdptBuf& B = A.B;
+  const DevScene& S = A.S;
+  const int P = A.P, nxt = cur ^ 1, cap = B.cap_sq;
+  const int n = A.ctr->ext_count[cur];
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
+  const int gstride = gridDim.x * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;
+  const float lpp = 1.f / static_cast<float>(S.nlights);
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    bool live = false, ext = false, conn_phase = false, nee = false, dib = false, di = false;
+    int p = -1, pix = -1, nv = 0, len = 0, nspec = 0, cnspec = 0;
+    V3 hp{}, thr{}, cthr{}, e_o{}, e_d{}, nee_tgt{}, nee_d{}, dib_o{}, dib_d{};
+    float dvcm = 0.f, dvc = 0.f, cdvcm = 0.f, cdvc = 0.f;
+    Bsdf b;
+    b.mat = 0;
+    if (j < n) {
+      p = B.q_path[cur][j];
+      const int prim = B.q_prim[cur][j];
+      if (prim >= 0) {
+        const float t = B.q_t[cur][j];
+        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
+        const Hit h = rebuild_hit(S, prim, t, o, d);
+        bsdf_init(b, -d, h.n, h.mat, S.mats);
+        if (b.mat != 0) {
+          hp = h.p;
+          pix = B.c_pix[p];
+          dvcm = B.c_dvcm[p];
+          dvc = B.c_dvc[p];
+          len = B.c_len[p];
+          nspec = B.c_nspec[p];
+          thr = ld3(B.c_thr, P, p);
+          dvcm *= (t * t);  // (:180-182)
+          dvcm /= fabsf(b.wi.z);
+          dvc /= fabsf(b.wi.z);
+          // this vertex's state, used by DI and the connections; the scatter
+          // below updates thr / dvcm / dvc / nspec for the next vertex
+          cthr = thr;
+          cdvcm = dvcm;
+          cdvc = dvc;
+          cnspec = nspec;
+          if (h.mat < 0) {  // hit an emitter (:184-199)
+            if (len_ok(A.ctl, len)) {
+              const DLight L = S.lights[-h.mat - 1];
+              float dpa, ep;
+              V3 r = light_radiance(L, d, &dpa, &ep);
+              if (!black(r)) {
+                if (len != 1) {  // getLightRadiance (:454-482)
+                  dpa *= lpp;
+                  ep *= lpp;
+                  const float wc = dpa * dvcm + ep * dvc;
+                  r = r * (1.f / (1.f + wc));
+                }
+                film_add(A.film, pix, mul(thr, r));
+              }
+            }
+          } else if (len < A.maxlen) {
+            live = true;
+            Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), B.c_ctr[p]};
+            if (!b.delta && len_ok(A.ctl, len + 1)) {  // getDirectIllumination (:205-217, :484-608)
+              di = true;
+              const float wlen = 1.f / (static_cast<float>(len) + 1.f - static_cast<float>(nspec));
+              const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
+              const DLight L = S.lights[lid];
+              V3 dtl;
+              float dist = 0.f, dpdf = 0.f, epdf = 0.f, cal = 0.f;
+              const V3 illu = light_illuminance(L, hp, rng.v(), &dtl, &dist, &dpdf, &epdf, &cal);
+              int flags = 0;
+              V3 nee_val = v3(0.f, 0.f, 0.f), bsdf_val = v3(0.f, 0.f, 0.f);
+              float nee_w = 0.f;
+              if (!black(illu) && dpdf > 0) {
+                float cos_to = 0.f, bdp, brp;
+                const V3 bf = bsdf_f(b, S.mats, dtl, &cos_to, &bdp, &brp);
+                if (!black(bf)) {
+                  bdp *= b.cont;
+                  brp *= b.cont;
+                  const V3 tmp = div_plain(mul(illu, bf) * cos_to, dpdf * lpp);
+                  if (!black(tmp)) {
+                    nee = true;
+                    flags |= DI_NEE;
+                    nee_d = normalize(dtl);
+                    nee_tgt = hp + dtl * dist;
+                    const float wl = bdp / (dpdf * lpp);
+                    const float wc = (epdf * cos_to / (dpdf * cal)) * (dvcm + brp * dvc);
+                    nee_w = 1.f / (wl + 1.f + wc);
+                    nee_val = tmp * (dpdf / (dpdf + bdp));
+                  }
+                }
+              }
+              V3 dtl2 = dtl;
+              float dpdf2 = dpdf, cos_s = 0.f;
+              int type;
+              const V3 bf2 = bsdf_sample(b, S.mats, rng.v(), &dtl2, &dpdf2, &cos_s, &type);
+              if (!black(bf2) && dpdf2 > 0) {
+                float w = 1.f;
+                V3 illu2 = illu;
+                bool early = false;
+                if (!(type & T_SPEC)) {
+                  float lpdf, ep2;
+                  illu2 = light_radiance(L, dtl2, &lpdf, &ep2);
+                  if (cmpf(lpdf) == 0) early = true;  // (:563-564) returns res unweighted
+                  else w = dpdf2 / (dpdf2 + lpdf);
+                }
+                if (early) {
+                  flags |= DI_EARLY;
+                } else {
+                  dib = true;
+                  flags |= DI_BSDF;
+                  dib_o = hp + dtl2 * WR_EPS;
+                  dib_d = normalize(dtl2);
+                  if (!black(illu2)) bsdf_val = div_plain(mul(illu2, bf2) * cos_s, dpdf2) * w;
+                }
+              }
+              B.di_flags[p] = flags;
+              st3(B.di_nee, P, p, nee_val);
+              B.di_neew[p] = nee_w;
+              st3(B.di_bsdf, P, p, bsdf_val);
+              st3(B.di_thr, P, p, thr);
+              B.di_wlen[p] = wlen;
+              B.di_light[p] = lid;
+              B.di_pix[p] = pix;
+              B.di_vis[p] = 0;
+              B.di_same[p] = 0;
+            }
+            if (!b.delta) {
+              conn_phase = true;
+              nv = B.v_count[p];
+            }
+            V3 so = ld3(B.c_o, P, p), sd = ld3(B.c_d, P, p);
+            if (sample_scatter(S, rng, b, hp, so, sd, thr, dvcm, dvc, nspec)) {
+              ext = true;
+              e_o = so + sd * WR_EPS;
+              e_d = normalize(sd);
+            }
+            B.c_ctr[p] = rng.ctr;
+            // state for the NEXT vertex; the connections below use the values of
+            // THIS vertex, so keep them (thr/dvcm/dvc/nspec are re-read below)
+            st3(B.c_o, P, p, so);
+            st3(B.c_d, P, p, sd);
+          }
+        }
+      }
+    }
+    // DI queue entries
+    {
+      const int di_i = wave_append(&A.ctr->di_count, di);
+      if (di) B.di_list[di_i] = p;
+      const int ni = wave_append(&A.ctr->sq_count, nee);
+      if (nee) {
+        st3(B.s_o, cap, ni, hp);
+        st3(B.s_d, cap, ni, nee_d);
+        st3(B.s_tgt, cap, ni, nee_tgt);
+        B.s_meta[ni] = (SQ_NEE << 30) | p;
+        B.s_pix[ni] = pix;
+      }
+      const int bi = wave_append(&A.ctr->sq_count, dib);
+      if (dib) {
+        st3(B.s_o, cap, bi, dib_o);
+        st3(B.s_d, cap, bi, dib_d);
+        B.s_meta[bi] = (SQ_DIB << 30) | p;
+        B.s_pix[bi] = pix;
+      }
+    }
+    // vertex connections to the paired light subpath (:219-257)
+    if (__ballot(conn_phase && nv > 0)) {
+      for (int k = 0; __ballot(conn_phase && k < nv); ++k) {
+        bool shoot = false;
+        V3 sdir{}, stgt{}, sval{};
+        if (conn_phase && k < nv) {
+          const int slot = k * P + p;
+          const int llen = B.v_len[slot];
+          if (llen + 1 + len > A.maxlen) {
+            nv = k;  // break (:237-239)
+          } else {
+            // connectVertices (:610-665)
+            const V3 lpos = ld3(B.v_pos, kVMax * P, slot);
+            V3 dir = lpos - hp;
+            const float d2 = sqr_len(dir);
+            const float dist = sqrtf(d2);
+            dir = div_guarded(dir, dist);
+            float cos_c = 0.f, cdp, crp;
+            const V3 cf = bsdf_f(b, S.mats, dir, &cos_c, &cdp, &crp);
+            if (!black(cf)) {
+              cdp *= b.cont;
+              crp *= b.cont;
+              Bsdf lb;
+              lb.mat = B.v_mat[slot];
+              lb.fr = frame_from_z(ld3(B.v_n, kVMax * P, slot));
+              lb.wi = ld3(B.v_wi, kVMax * P, slot);
+              lb.pd = B.v_pd[slot];
+              lb.pg = B.v_pg[slot];
+              lb.cont = B.v_cont[slot];
+              float cos_l = 0.f, ldp, lrp;
+              const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
+              if (!black(lf)) {
+                ldp *= lb.cont;
+                lrp *= lb.cont;
+                const float G = cos_l * cos_c / d2;
+                if (!(cmpf(G) < 0)) {
+                  const float cdpa = cdp * fabsf(cos_l) / (dist * dist);
+                  const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
+                  const V3 res = mul(cf, lf) * G;
+                  if (!black(res)) {
+                    const float wl = cdpa * (B.v_dvcm[slot] + lrp * B.v_dvc[slot]);
+                    const float wc = ldpa * (cdvcm + crp * cdvc);
+                    const float w = 1.f / (wl + 1.f + wc);
+                    const bool counts = len_ok(A.ctl, llen + 1 + len);
+                    if (counts || A.faithful) {
+                      shoot = true;
+                      sdir = normalize(dir);
+                      stgt = hp + dir * dist;
+                      if (counts) {
+                        const float wlen = 1.f / (static_cast<float>(llen) + 1.f + static_cast<float>(len) -
+                                                  static_cast<float>(B.v_nspec[slot]) - static_cast<float>(cnspec));
+                        const V3 lthr = ld3(B.v_thr, kVMax * P, slot);
+                        sval = mul(mul(cthr, lthr), res * w) * wlen;
+                      }
+                    }
+                  }
+                }
+              }
+            }
+          }
+        }
+        const int si = wave_append(&A.ctr->sq_count, shoot);
+        if (shoot) {
+          st3(B.s_o, cap, si, hp);
+          st3(B.s_d, cap, si, sdir);
+          st3(B.s_tgt, cap, si, stgt);
+          st3(B.s_val, cap, si, sval);
+          B.s_meta[si] = (SQ_CONN << 30) | p;
+          B.s_pix[si] = pix;
+        }
+      }
+    }
+    if (live) {  // commit scattered state (:259-260) and the loop increment
+      if (ext) {
+        st3(B.c_thr, P, p, thr);
+        B.c_dvcm[p] = dvcm;
+        B.c_dvc[p] = dvc;
+        B.c_nspec[p] = nspec;
+        B.c_len[p] = len + 1;
+      }
+    }
+    const int ei = wave_append(&A.ctr->ext_count[nxt], ext);
+    if (ext) {
+      st3(B.q_o[nxt], P, ei, e_o);
+      st3(B.q_d[nxt], P, ei, e_d);
+      B.q_path[nxt][ei] = p;
+    }
+  }
+}
+
+// Light-tracing splats and camera-pass shadow / aux rays after traversal.
+__global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptArgs A) {
+  const BdptBuf& B = A.B;
+  const DevScene& S = A.S;
+  const int n = A.ctr->sq_count, cap = B.cap_sq;
+  const int gstride = gridDim.x * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    bool is_shadow = false, is_closest = false;
+    if (j < n) {
+      const int meta = B.s_meta[j];
+      const int kind = (meta >> 30) & 3, p = meta & 0x3fffffff;
+      const int prim = B.s_prim[j];
+      const float t = B.s_t[j];
+      if (kind == SQ_DIB) {  // DI BSDF-sampled ray: same light? (:570-596)
+        is_closest = true;
+        int same = 0;
+        if (prim >= 0) {
+          const int m = S.prim_mat[prim];
+          same = (m < 0 && -m - 1 == B.di_light[p]) ? 1 : 0;
+        }
+        B.di_same[p] = same;
+      } else {  // Scene::occluded: position equality (scene.cpp:55-69)
+        is_shadow = true;
+        bool unocc = true;
+        if (prim >= 0) {
+          const V3 o = ld3(B.s_o, cap, j), d = ld3(B.s_d, cap, j);
+          unocc = near_eq(o + d * t, ld3(B.s_tgt, cap, j));
+        }
+        if (kind == SQ_NEE) {
+          B.di_vis[p] = unocc ? 1 : 0;
+        } else if (unocc) {
+          film_add(A.film, B.s_pix[j], ld3(B.s_val, cap, j));
+        }
+      }
+    }
+    wave_count(&A.ctr->shadow, is_shadow);
+    wave_count(&A.ctr->closest, is_closest);
+  }
+}
+
+// getDirectIllumination's final combination (:533-607)
+__global__ void __launch_bounds__(kShadeBlock) k_di_finalize(BdptArgs A) {
+  const BdptBuf& B = A.B;
+  const int n = A.ctr->di_count, P = A.P;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const int p = B.di_list[j];
+    const int flags = B.di_flags[p];
+    V3 res = v3(0.f, 0.f, 0.f);
+    float weight = 0.f;
+    if ((flags & DI_NEE) && B.di_vis[p]) {
+      weight = B.di_neew[p];
+      res = res + ld3(B.di_nee, P, p);
+    }
+    V3 di;
+    if (flags & DI_EARLY) {
+      di = res;
+    } else {
+      if ((flags & DI_BSDF) && B.di_same[p]) res = res + ld3(B.di_bsdf, P, p);
+      di = res * weight;
+    }
+    film_add(A.film, B.di_pix[p], mul(ld3(B.di_thr, P, p), di) * B.di_wlen[p]);
+  }
+}
+
+// =============================================================== PT
+struct PtBuf {
+  int P = 0;
+  float *o, *d, *pw, *last_pdf;
+  int *last_spec, *len, *pix;
+  uint32_t* ctr;
+  float *q_o[2], *q_d[2], *q_t[2];
+  int *q_path[2], *q_prim[2];
+  float *s_o, *s_d, *s_tgt, *s_val, *s_t;
+  int *s_pix, *s_prim;
+};
+struct PtArgs {
+  DevScene S;
+  PtBuf T;
+  DevCounters* ctr;
+  float* film;
+  int W, H, P, spp, grid_len, max_depth;
+  uint32_t seed, k;
+};
+
+// SurfaceIntegrator::render per-sample setup (surfaceIntegrator.cpp:26-34)
+__global__ void __launch_bounds__(kShadeBlock) k_pt_gen(PtArgs A) {
+  const PtBuf& T = A.T;
+  const DCam& cam = A.S.cam;
+  const int P = A.P;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    const int i = p / A.W, jj = p % A.W;
+    Rng rng{stream_key(A.seed, A.k, 2, static_cast<uint32_t>(p)), 0};
+    const V3 v0 = v3(static_cast<float>(jj) - 0.5f, static_cast<float>(i) - 0.5f, 0.f);
+    const V3 v1 = v3(static_cast<float>(jj) + 0.5f, static_cast<float>(i) - 0.5f, 0.f);
+    const V3 v2 = v3(static_cast<float>(jj) - 0.5f, static_cast<float>(i) + 0.5f, 0.f);
+    const V3 pr = sample_rect_strat(rng.v(), v0, v1, v2, static_cast<int>(A.k), A.grid_len);
+    const V3 wp = t_point(cam.r2w, v3(pr.x, pr.y, 0.f));
+    const V3 d = normalize(wp - cam.pos);
+    st3(T.o, P, p, cam.pos);
+    st3(T.d, P, p, d);
+    st3(T.pw, P, p, v3(1.f, 1.f, 1.f));
+    T.last_pdf[p] = 1.f;
+    T.last_spec[p] = 1;
+    T.len[p] = 1;
+    T.pix[p] = i * A.W + jj;
+    T.ctr[p] = rng.ctr;
+    st3(T.q_o[0], P, p, cam.pos);  // Ray r(ray): no EPS offset for the primary ray
+    st3(T.q_d[0], P, p, d);
+    T.q_path[0][p] = p;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->ext_count[0] = P;
+}
+
+// One PathIntegrator::raytracing iteration (pathIntegrator.cpp:43-146)
+__global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int cur) {
+  const PtBuf& T = A.T;
+  const DevScene& S = A.S;
+  const int P = A.P, nxt = cur ^ 1;
+  const int n = A.ctr->ext_count[cur];
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
+  const int gstride = gridDim.x * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;
+  const float lpp = 1.f / static_cast<float>(S.nlights);
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    bool ext = false, shadow = false;
+    int p = -1, pix = -1;
+    V3 e_o{}, e_d{}, s_o{}, s_d{}, s_tgt{}, s_val{};
+    if (j < n) {
+      p = T.q_path[cur][j];
+      const int prim = T.q_prim[cur][j];
+      if (prim >= 0) {
+        const float t = T.q_t[cur][j];
+        const V3 o = ld3(T.q_o[cur], P, j), d = ld3(T.q_d[cur], P, j);
+        const Hit h = rebuild_hit(S, prim, t, o, d);
+        Bsdf b;
+        bsdf_init(b, -d, h.n, h.mat, S.mats);
+        pix = T.pix[p];
+        if (b.mat != 0) {
+          V3 pw = ld3(T.pw, P, p);
+          const int len = T.len[p];
+          if (b.mat < 0) {  // (:53-73)
+            const DLight L = S.lights[-b.mat - 1];
+            float dpa, ep;
+            const V3 c = light_radiance(L, d, &dpa, &ep);
+            if (!black(c)) {
+              float mw = 1.f;
+              if (len > 1 && !T.last_spec[p]) {
+                const float dp = dpa * (t * t) / fabsf(b.wi.z);  // pdfAtoW
+                const float lp = T.last_pdf[p];
+                mw = lp / (lp + dp * lpp);
+              }
+              film_add(A.film, pix, mul(pw, c) * mw);
+            }
+          } else if (!(len > A.max_depth) && cmpf(b.cont) != 0) {
+            Rng rng{stream_key(A.seed, A.k, 2, static_cast<uint32_t>(p)), T.ctr[p]};
+            if (!b.delta) {  // (:81-118)
+              const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
+              const DLight L = S.lights[lid];
+              V3 dtl;
+              float dist = 0.f, dpdf = 0.f, ep, cal;
+              const V3 illu = light_illuminance(L, h.p, rng.v(), &dtl, &dist, &dpdf, &ep, &cal);
+              if (!black(illu)) {
+                shadow = true;
+                s_o = h.p + dtl * WR_EPS;
+                s_d = normalize(dtl);
+                s_tgt = h.p + dtl * (dist - WR_EPS);
+                float bp, cw = 0.f;
+                const V3 bf = bsdf_f(b, S.mats, dtl, &cw, &bp, nullptr);
+                s_val = v3(0.f, 0.f, 0.f);
+                if (!black(bf)) {
+                  bp *= b.cont;
+                  const float w = (dpdf * lpp) / ((dpdf * lpp) + bp);
+                  const V3 c = mul(illu, bf) * (w * cw / (lpp * dpdf));
+                  s_val = mul(c, pw);
+                }
+              }
+            }
+            float pdf = 0.f, cw = 0.f;
+            int type;
+            V3 dn = d;
+            const V3 bf = bsdf_sample(b, S.mats, rng.v(), &dn, &pdf, &cw, &type);
+            if (!black(bf)) {  // (:124-145)
+              const float cp = b.cont;
+              const int lspec = (type & T_SPEC) != 0;
+              const float lpdf = pdf * cp;
+              bool cont = true;
+              if (cmpf(cp - 1.f) < 0) {
+                if (cmpf(rng.f() - cp) > 0) cont = false;
+                else pdf *= cp;
+              }
+              if (cont) {
+                pw = mul(pw, bf) * (cw / pdf);
+                ext = true;
+                e_o = h.p + dn * WR_EPS;
+                e_d = dn;  // r.dir stays un-normalised (:144-145)
+                st3(T.pw, P, p, pw);
+                T.last_spec[p] = lspec;
+                T.last_pdf[p] = lpdf;
+                T.len[p] = len + 1;
+              }
+            }
+            T.ctr[p] = rng.ctr;
+          }
+        }
+      }
+    }
+    const int ei = wave_append(&A.ctr->ext_count[nxt], ext);
+    if (ext) {
+      st3(T.q_o[nxt], P, ei, e_o);
+      st3(T.q_d[nxt], P, ei, e_d);
+      T.q_path[nxt][ei] = p;
+    }
+    const int si = wave_append(&A.ctr->sq_count, shadow);
+    if (shadow) {
+      st3(T.s_o, P, si, s_o);
+      st3(T.s_d, P, si, s_d);
+      st3(T.s_tgt, P, si, s_tgt);
+      st3(T.s_val, P, si, s_val);
+      T.s_pix[si] = pix;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kShadeBlock) k_pt_resolve(PtArgs A) {
+  const PtBuf& T = A.T;
+  const int n = A.ctr->sq_count, P = A.P;
+  const int gstride = gridDim.x * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    bool is = false;
+    if (j < n) {
+      is = true;
+      bool unocc = true;
+      const int prim = T.s_prim[j];
+      if (prim >= 0) {
+        const V3 o = ld3(T.s_o, P, j), d = ld3(T.s_d, P, j);
+        unocc = near_eq(o + d * T.s_t[j], ld3(T.s_tgt, P, j));
+      }
+      if (unocc) film_add(A.film, T.s_pix[j], ld3(T.s_val, P, j));
+    }
+    wave_count(&A.ctr->shadow, is);
+  }
+}
+
+__global__ void k_film_accumulate(float* dst, const float* src, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = dst[i] + src[i];
+}
+
+}  // namespace
+
+// =============================================================== host side
+struct wr_scene {
+  wr::Scene s;
+};
+
+namespace {
+// Device memory arena: bump allocation out of one hipMalloc per arena.
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0, used = 0;
+  int reserve(size_t bytes) {
+    release();
+    if (hipMalloc(&base, bytes) != hipSuccess) {
+      base = nullptr;
+      return fail(WR_E_HIP, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+    }
+    cap = bytes;
+    used = 0;
+    return WR_OK;
+  }
+  template <class T>
+  T* take(size_t n) {
+    size_t off = (used + 255) & ~size_t(255);
+    used = off + n * sizeof(T);
+    return reinterpret_cast<T*>(base + off);
+  }
+  void release() {
+    if (base) (void)hipFree(base);
+    base = nullptr;
+    cap = used = 0;
+  }
+};
+
+template <class Fn>
+size_t measure(Fn fn) {  // bytes an arena layout needs
+  Arena a;
+  fn(a);
+  return a.used + 256;
+}
+}  // namespace
+
+struct wr_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DevScene ds{};
+  Arena scene_mem;
+  int64_t scene_bytes = 0;
+  Arena work;
+  size_t work_key = 0;  // P for which `work` is laid out
+  int work_kind = 0;    // 1 bdpt, 2 pt
+  BdptBuf bb{};
+  PtBuf pb{};
+  DevCounters* ctr = nullptr;
+  float* film_tmp = nullptr;
+  size_t film_tmp_n = 0;
+  int grid = 2048;
+  std::vector<hipEvent_t> events;
+  size_t ev_used = 0;
+  int ev_cat[4096];
+  bool timing = false;
+};
+
+namespace {
+
+void layout_bdpt(Arena& a, BdptBuf& B, int P) {
+  B.P = P;
+  B.cap_sq = P * (kVMax + 2);  // per camera vertex: <= kVMax connections + NEE + DI-BSDF
+  const size_t sP = P, sV = size_t(kVMax) * P, sQ = B.cap_sq;
+  B.l_o = a.take<float>(3 * sP);
+  B.l_d = a.take<float>(3 * sP);
+  B.l_thr = a.take<float>(3 * sP);
+  B.l_dvcm = a.take<float>(sP);
+  B.l_dvc = a.take<float>(sP);
+  B.l_len = a.take<int>(sP);
+  B.l_nspec = a.take<int>(sP);
+  B.l_ctr = a.take<uint32_t>(sP);
+  B.v_pos = a.take<float>(3 * sV);
+  B.v_n = a.take<float>(3 * sV);
+  B.v_wi = a.take<float>(3 * sV);
+  B.v_thr = a.take<float>(3 * sV);
+  B.v_dvcm = a.take<float>(sV);
+  B.v_dvc = a.take<float>(sV);
+  B.v_cont = a.take<float>(sV);
+  B.v_pd = a.take<float>(sV);
+  B.v_pg = a.take<float>(sV);
+  B.v_len = a.take<int>(sV);
+  B.v_nspec = a.take<int>(sV);
+  B.v_mat = a.take<int>(sV);
+  B.v_count = a.take<int>(sP);
+  B.c_o = a.take<float>(3 * sP);
+  B.c_d = a.take<float>(3 * sP);
+  B.c_thr = a.take<float>(3 * sP);
+  B.c_dvcm = a.take<float>(sP);
+  B.c_dvc = a.take<float>(sP);
+  B.c_len = a.take<int>(sP);
+  B.c_nspec = a.take<int>(sP);
+  B.c_pix = a.take<int>(sP);
+  B.c_ctr = a.take<uint32_t>(sP);
+  for (int q = 0; q < 2; ++q) {
+    B.q_o[q] = a.take<float>(3 * sP);
+    B.q_d[q] = a.take<float>(3 * sP);
+    B.q_t[q] = a.take<float>(sP);
+    B.q_path[q] = a.take<int>(sP);
+    B.q_prim[q] = a.take<int>(sP);
+  }
+  B.s_o = a.take<float>(3 * sQ);
+  B.s_d = a.take<float>(3 * sQ);
+  B.s_tgt = a.take<float>(3 * sQ);
+  B.s_val = a.take<float>(3 * sQ);
+  B.s_t = a.take<float>(sQ);
+  B.s_meta = a.take<int>(sQ);
+  B.s_pix = a.take<int>(sQ);
+  B.s_prim = a.take<int>(sQ);
+  B.di_nee = a.take<float>(3 * sP);
+  B.di_neew = a.take<float>(sP);
+  B.di_bsdf = a.take<float>(3 * sP);
+  B.di_thr = a.take<float>(3 * sP);
+  B.di_wlen = a.take<float>(sP);
+  B.di_flags = a.take<int>(sP);
+  B.di_light = a.take<int>(sP);
+  B.di_pix = a.take<int>(sP);
+  B.di_vis = a.take<int>(sP);
+  B.di_same = a.take<int>(sP);
+  B.di_list = a.take<int>(sP);
+}
+
+void layout_pt(Arena& a, PtBuf& T, int P) {
+  T.P = P;
+  const size_t sP = P;
+  T.o = a.take<float>(3 * sP);
+  T.d = a.take<float>(3 * sP);
+  T.pw = a.take<float>(3 * sP);
+  T.last_pdf = a.take<float>(sP);
+  T.last_spec = a.take<int>(sP);
+  T.len = a.take<int>(sP);
+  T.pix = a.take<int>(sP);
+  T.ctr = a.take<uint32_t>(sP);
+  for (int q = 0; q < 2; ++q) {
+    T.q_o[q] = a.take<float>(3 * sP);
+    T.q_d[q] = a.take<float>(3 * sP);
+    T.q_t[q] = a.take<float>(sP);
+    T.q_path[q] = a.take<int>(sP);
+    T.q_prim[q] = a.take<int>(sP);
+  }
+  T.s_o = a.take<float>(3 * sP);
+  T.s_d = a.take<float>(3 * sP);
+  T.s_tgt = a.take<float>(3 * sP);
+  T.s_val = a.take<float>(3 * sP);
+  T.s_t = a.take<float>(sP);
+  T.s_pix = a.take<int>(sP);
+  T.s_prim = a.take<int>(sP);
+}
+
+int ensure_work(wr_context* c, int kind, int P) {
+  if (c->work_kind == kind && c->work_key == static_cast<size_t>(P)) return WR_OK;
+  size_t bytes = kind == 1 ? measure([&](Arena& a) { BdptBuf b; layout_bdpt(a, b, P); })
+                           : measure([&](Arena& a) { PtBuf t; layout_pt(a, t, P); });
+  int rc = c->work.reserve(bytes);
+  if (rc) return rc;
+  if (kind == 1) layout_bdpt(c->work, c->bb, P);
+  else layout_pt(c->work, c->pb, P);
+  c->work_kind = kind;
+  c->work_key = P;
+  return WR_OK;
+}
+
+// ---- launch helpers with optional per-launch HIP events (context stream)
+struct Timer {
+  wr_context* c;
+  explicit Timer(wr_context* cc) : c(cc) {}
+  void mark(int cat) {
+    if (!c->timing) return;
+    if (c->ev_used >= c->events.size()) {
+      hipEvent_t e;
+      (void)hipEventCreate(&e);
+      c->events.push_back(e);
+    }
+    if (c->ev_used < 4096) c->ev_cat[c->ev_used] = cat;
+    (void)hipEventRecord(c->events[c->ev_used++], c->stream);
+  }
+};
+
+int trace_launch(wr_context* c, Timer& tm, bool count, const float* o3, const float* d3, int cap, const int* cnt,
+                 float* t, int* prim, int max_rays) {
+  const size_t lds = size_t(3) * sizeof(uint32_t) * std::max(1, c->ds.max_stack) * kTraceBlock;
+  const int grid = std::max(1, std::min(c->grid, (max_rays + kTraceBlock - 1) / kTraceBlock));
+  if (count)
+    hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, o3, d3, cap, cnt, t,
+                       prim, c->ctr);
+  else
+    hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, o3, d3, cap, cnt, t,
+                       prim, c->ctr);
+  tm.mark(WR_K_TRACE);
+  return WR_OK;
+}
+
+int shade_grid(wr_context* c, int n) { return std::max(1, std::min(c->grid, (n + kShadeBlock - 1) / kShadeBlock)); }
+
+void begin_stats(wr_context* c, const int time_kernels) {
+  c->timing = time_kernels != 0;
+  c->ev_used = 0;
+}
+
+int finish_stats(wr_context* c, wr_stats* st, double t0_host) {
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (!st) return WR_OK;
+  DevCounters h;
+  HIPCHK(hipMemcpy(&h, c->ctr, sizeof h, hipMemcpyDeviceToHost));
+  st->closest_rays += static_cast<int64_t>(h.closest);
+  st->shadow_rays += static_cast<int64_t>(h.shadow);
+  st->inner_visits += static_cast<int64_t>(h.inner);
+  st->leaf_visits += static_cast<int64_t>(h.leaves);
+  st->prim_refs += static_cast<int64_t>(h.refs);
+  const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  st->seconds += t1 - t0_host;
+  if (c->timing) {
+    for (size_t i = 1; i < c->ev_used; ++i) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, c->events[i - 1], c->events[i]);
+      const int cat = i < 4096 ? c->ev_cat[i] : WR_K_OTHER;
+      st->kernel_ms[cat] += ms;
+      st->kernel_launches[cat] += 1;
+    }
+  }
+  return WR_OK;
+}
+
+double host_now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int check_device() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(WR_E_NODEVICE, "no HIP device visible");
+  return WR_OK;
+}
+
+}  // namespace
+
+// =============================================================== C ABI
+extern "C" {
+
+const char* wr_last_error(void) { return g_err.c_str(); }
+int wr_api_version(void) { return WR_API_VERSION; }
+
+int wr_scene_load(const char* path, wr_scene** out) {
+  if (!path || !out) return fail(WR_E_ARG, "null argument");
+  *out = nullptr;
+  auto* s = new (std::nothrow) wr_scene();
+  if (!s) return fail(WR_E_ARG, "out of host memory");
+  std::string err;
+  if (!wr::load_scene(path, s->s, err)) {
+    delete s;
+    return fail(WR_E_IO, err);
+  }
+  *out = s;
+  return WR_OK;
+}
+
+int wr_scene_info_get(const wr_scene* sc, wr_scene_info* o) {
+  if (!sc || !o) return fail(WR_E_ARG, "null argument");
+  const wr::Scene& s = sc->s;
+  std::memset(o, 0, sizeof *o);
+  o->nprims = static_cast<int32_t>(s.prims.size());
+  for (const auto& p : s.prims) (p.type == wr::kTri ? o->ntriangles : o->nspheres)++;
+  o->nlights = static_cast<int32_t>(s.lights.size());
+  o->nmaterials = static_cast<int32_t>(s.mats.size());
+  o->kd_depth_max = s.dep_max;
+  for (const auto& n : s.nodes) (n.axis >= 0 ? o->kd_inner : o->kd_leaves)++;
+  o->kd_refs = static_cast<int64_t>(s.refs.size());
+  o->kd_max_stack = s.max_stack;
+  o->missing_files = s.missing_files;
+  o->camera_xres = s.cam.xres;
+  o->camera_yres = s.cam.yres;
+  o->device_bytes = static_cast<int64_t>(s.nodes.size() * 8 + s.refs.size() * 40 + s.prims.size() * 64);
+  return WR_OK;
+}
+
+int wr_scene_dump(const wr_scene* sc, const char* path) {
+  if (!sc || !path) return fail(WR_E_ARG, "null argument");
+  std::string txt = wr::dump_scene(sc->s);
+  FILE* f = std::fopen(path, "w");
+  if (!f) return fail(WR_E_IO, std::string("cannot write ") + path);
+  std::fwrite(txt.data(), 1, txt.size(), f);
+  std::fclose(f);
+  return WR_OK;
+}
+
+void wr_scene_free(wr_scene* s) { delete s; }
+
+int wr_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int wr_create(const wr_scene* sc, int device, wr_context** out) {
+  if (!sc || !out) return fail(WR_E_ARG, "null argument");
+  *out = nullptr;
+  if (int rc = check_device()) return rc;
+  const wr::Scene& s = sc->s;
+  if (s.prims.empty()) return fail(WR_E_SCENE, "scene has no primitives");
+  for (const auto& p : s.prims)  // the reference would index materials[] out of range
+    if (p.mat >= static_cast<int>(s.mats.size()))
+      return fail(WR_E_SCENE, "primitive material id " + std::to_string(p.mat) + " has no <material>");
+  HIPCHK(hipSetDevice(device));
+  auto* c = new wr_context();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(WR_E_HIP, "hipStreamCreate failed");
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->grid = std::max(256, prop.multiProcessorCount * 8);
+
+  // ---- flatten the tree + primitives into the HBM layout of wr_traverse.h
+  const size_t nn = s.nodes.size(), nr = s.refs.size(), np = s.prims.size();
+  std::vector<uint2> nodes(nn);
+  for (size_t i = 0; i < nn; ++i) {
+    const wr::KdNode& k = s.nodes[i];
+    if (k.axis >= 0) {
+      uint32_t bits;
+      std::memcpy(&bits, &k.split, 4);
+      nodes[i] = make_uint2(bits, (static_cast<uint32_t>(k.right) << 2) | static_cast<uint32_t>(k.axis));
+    } else {
+      nodes[i] = make_uint2(static_cast<uint32_t>(k.first), (static_cast<uint32_t>(k.count) << 2) | 3u);
+    }
+  }
+  std::vector<float4> ra(nr), rb(nr);
+  std::vector<float2> rcv(nr);
+  for (size_t i = 0; i < nr; ++i) {
+    const int pi = s.refs[i];
+    const wr::Prim& p = s.prims[pi];
+    if (p.type == wr::kTri) {
+      // A..F exactly as Triangle::hit forms them (triangle.cpp:24-30)
+      ra[i] = make_float4(p.p0.x, p.p0.y, p.p0.z, p.p0.x - p.p1.x);
+      rb[i] = make_float4(p.p0.y - p.p1.y, p.p0.z - p.p1.z, p.p0.x - p.p2.x, p.p0.y - p.p2.y);
+      float pb;
+      std::memcpy(&pb, &pi, 4);
+      rcv[i] = make_float2(p.p0.z - p.p2.z, pb);
+    } else {
+      ra[i] = make_float4(0, 0, 0, 0);
+      rb[i] = make_float4(0, 0, 0, 0);
+      int neg = -(pi + 1);
+      float pb;
+      std::memcpy(&pb, &neg, 4);
+      rcv[i] = make_float2(0.f, pb);
+    }
+  }
+  std::vector<int> pmat(np), ptype(np);
+  std::vector<float4> ptri(np), psph(np), psb0(np);
+  std::vector<float2> ptri2(np), psb1(np);
+  for (size_t i = 0; i < np; ++i) {
+    const wr::Prim& p = s.prims[i];
+    pmat[i] = p.mat;
+    ptype[i] = p.type;
+    ptri[i] = make_float4(p.p0.x - p.p1.x, p.p0.y - p.p1.y, p.p0.z - p.p1.z, p.p0.x - p.p2.x);
+    ptri2[i] = make_float2(p.p0.y - p.p2.y, p.p0.z - p.p2.z);
+    psph[i] = make_float4(p.c.x, p.c.y, p.c.z, p.r);
+    psb0[i] = make_float4(p.bl.x, p.bl.y, p.bl.z, p.br.x);
+    psb1[i] = make_float2(p.br.y, p.br.z);
+  }
+  std::vector<DLight> lights(s.lights.size());
+  for (size_t i = 0; i < lights.size(); ++i) {
+    const wr::Light& l = s.lights[i];
+    auto V = [](wr::F3 f) { return v3(f.x, f.y, f.z); };
+    lights[i] = DLight{V(l.p0), V(l.d1), V(l.d2), V(l.fx), V(l.fy), V(l.fz), V(l.le), l.inv_area};
+  }
+  std::vector<DMat> mats(std::max<size_t>(1, s.mats.size()));
+  for (size_t i = 0; i < s.mats.size(); ++i) {
+    const wr::Material& m = s.mats[i];
+    mats[i] = DMat{v3(m.diffuse.x, m.diffuse.y, m.diffuse.z), v3(m.phong.x, m.phong.y, m.phong.z),
+                   v3(m.specular.x, m.specular.y, m.specular.z), m.phong_exp, m.index};
+  }
+  auto total = measure([&](Arena& a) {
+    a.take<uint2>(nn); a.take<float4>(nr); a.take<float4>(nr); a.take<float2>(nr);
+    a.take<int>(np); a.take<int>(np); a.take<float4>(np); a.take<float2>(np); a.take<float4>(np);
+    a.take<float4>(np); a.take<float2>(np); a.take<DLight>(lights.size() + 1); a.take<DMat>(mats.size());
+    a.take<DevCounters>(1);
+  });
+  if (int rc = c->scene_mem.reserve(total)) {
+    delete c;
+    return rc;
+  }
+  Arena& A = c->scene_mem;
+  auto up = [&](auto* dst, const auto& v) {
+    return hipMemcpy(dst, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice);
+  };
+  DevScene& d = c->ds;
+  uint2* dn = A.take<uint2>(nn);
+  float4* dra = A.take<float4>(nr);
+  float4* drb = A.take<float4>(nr);
+  float2* drc = A.take<float2>(nr);
+  int* dpm = A.take<int>(np);
+  int* dpt = A.take<int>(np);
+  float4* dptri = A.take<float4>(np);
+  float2* dptri2 = A.take<float2>(np);
+  float4* dpsph = A.take<float4>(np);
+  float4* dpsb0 = A.take<float4>(np);
+  float2* dpsb1 = A.take<float2>(np);
+  DLight* dl = A.take<DLight>(lights.size() + 1);
+  DMat* dm = A.take<DMat>(mats.size());
+  c->ctr = A.take<DevCounters>(1);
+  hipError_t e = hipSuccess;
+  for (hipError_t x : {up(dn, nodes), up(dra, ra), up(drb, rb), up(drc, rcv), up(dpm, pmat), up(dpt, ptype),
+                       up(dptri, ptri), up(dptri2, ptri2), up(dpsph, psph), up(dpsb0, psb0), up(dpsb1, psb1),
+                       up(dm, mats)})
+    if (x != hipSuccess) e = x;
+  if (!lights.empty() && e == hipSuccess) e = up(dl, lights);
+  if (e != hipSuccess) {
+    wr_destroy(c);
+    return fail(WR_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));
+  }
+  d.nodes = dn;
+  d.ref_a = dra;
+  d.ref_b = drb;
+  d.ref_c = drc;
+  d.prim_mat = dpm;
+  d.prim_type = dpt;
+  d.prim_tri = dptri;
+  d.prim_tri2 = dptri2;
+  d.prim_sph = dpsph;
+  d.prim_sbox0 = dpsb0;
+  d.prim_sbox1 = dpsb1;
+  d.root_l = v3(s.root_l.x, s.root_l.y, s.root_l.z);
+  d.root_r = v3(s.root_r.x, s.root_r.y, s.root_r.z);
+  d.max_stack = std::max(1, s.max_stack);
+  d.nlights = static_cast<int>(s.lights.size());
+  d.lights = dl;
+  d.mats = dm;
+  d.cam.pos = v3(s.cam.pos.x, s.cam.pos.y, s.cam.pos.z);
+  d.cam.fwd = v3(s.cam.fwd.x, s.cam.fwd.y, s.cam.fwd.z);
+  d.cam.xres = s.cam.xres;
+  d.cam.yres = s.cam.yres;
+  d.cam.plane_dist = s.cam.plane_dist;
+  std::memcpy(d.cam.w2r, s.cam.w2r, sizeof d.cam.w2r);
+  std::memcpy(d.cam.r2w, s.cam.r2w, sizeof d.cam.r2w);
+  c->scene_bytes = static_cast<int64_t>(A.used);
+  *out = c;
+  return WR_OK;
+}
+
+void wr_destroy(wr_context* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+  if (c->film_tmp) (void)hipFree(c->film_tmp);
+  c->work.release();
+  c->scene_mem.release();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, int64_t n, wr_hit* hits,
+                     uint8_t* occ) {
+  if (!c || (!rays && n) || n < 0) return fail(WR_E_ARG, "bad argument");
+  if (n == 0) return WR_OK;
+  HIPCHK(hipSetDevice(c->device));
+  wr_ray* dr = nullptr;
+  float* dt = nullptr;
+  wr_hit* dh = nullptr;
+  uint8_t* dox = nullptr;
+  HIPCHK(hipMalloc(&dr, n * sizeof(wr_ray)));
+  HIPCHK(hipMemcpyAsync(dr, rays, n * sizeof(wr_ray), hipMemcpyHostToDevice, c->stream));
+  if (occ) {
+    HIPCHK(hipMalloc(&dt, n * 3 * sizeof(float)));
+    HIPCHK(hipMalloc(&dox, n));
+    HIPCHK(hipMemcpyAsync(dt, targets, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  } else {
+    HIPCHK(hipMalloc(&dh, n * sizeof(wr_hit)));
+  }
+  const size_t lds = size_t(3) * sizeof(uint32_t) * c->ds.max_stack * kTraceBlock;
+  const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(c->grid, (n + kTraceBlock - 1) / kTraceBlock)));
+  hipLaunchKernelGGL(k_trace_api, dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, dr, dt, n, dh, dox);
+  HIPCHK(hipGetLastError());
+  if (occ) HIPCHK(hipMemcpyAsync(occ, dox, n, hipMemcpyDeviceToHost, c->stream));
+  else HIPCHK(hipMemcpyAsync(hits, dh, n * sizeof(wr_hit), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  (void)hipFree(dr);
+  if (dt) (void)hipFree(dt);
+  if (dh) (void)hipFree(dh);
+  if (dox) (void)hipFree(dox);
+  return WR_OK;
+}
+
+int wr_trace_closest(wr_context* c, const wr_ray* rays, int64_t n, wr_hit* hits) {
+  if (!hits && n) return fail(WR_E_ARG, "null hits");
+  return trace_api(c, rays, nullptr, n, hits, nullptr);
+}
+
+int wr_occluded(wr_context* c, const wr_ray* rays, const float* targets, int64_t n, uint8_t* occluded) {
+  if ((!targets || !occluded) && n) return fail(WR_E_ARG, "null targets / output");
+  return trace_api(c, rays, targets, n, nullptr, occluded);
+}
+
+static int film_target(wr_context* c, float* film, int film_on_device, size_t nfloat, float** dev) {
+  if (film_on_device) {
+    *dev = film;
+    return WR_OK;
+  }
+  if (c->film_tmp_n < nfloat) {
+    if (c->film_tmp) (void)hipFree(c->film_tmp);
+    c->film_tmp = nullptr;
+    c->film_tmp_n = 0;
+    HIPCHK(hipMalloc(&c->film_tmp, nfloat * sizeof(float)));
+    c->film_tmp_n = nfloat;
+  }
+  HIPCHK(hipMemsetAsync(c->film_tmp, 0, nfloat * sizeof(float), c->stream));
+  *dev = c->film_tmp;
+  return WR_OK;
+}
+
+static int film_return(wr_context* c, float* film, int film_on_device, size_t nfloat) {
+  if (film_on_device) return WR_OK;
+  std::vector<float> tmp(nfloat);
+  HIPCHK(hipMemcpyAsync(tmp.data(), c->film_tmp, nfloat * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < nfloat; ++i) film[i] = film[i] + tmp[i];
+  return WR_OK;
+}
+
+int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int film_on_device, wr_stats* st) {
+  if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
+  if (prm->width <= 0 || prm->height <= 0 || prm->iterations < 0) return fail(WR_E_ARG, "bad film size");
+  if (static_cast<int64_t>(prm->width) * prm->height >= (1 << 30) / (kVMax + 2))
+    return fail(WR_E_ARG, "film too large for one context");
+  if (prm->max_path_length > kVMax + 1)
+    return fail(WR_E_ARG, "max_path_length > 10 is not supported (light-vertex store sized for the reference's 10)");
+  if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "BDPT needs at least one area light");
+  HIPCHK(hipSetDevice(c->device));
+  const double t0 = host_now();
+  const int P = prm->width * prm->height;
+  if (int rc = ensure_work(c, 1, P)) return rc;
+  float* dfilm = nullptr;
+  const size_t nf = size_t(P) * 3;
+  if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
+  HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(DevCounters), c->stream));
+  begin_stats(c, prm->time_kernels);
+  Timer tm(c);
+  tm.mark(WR_K_OTHER);
+  BdptArgs A;
+  A.S = c->ds;
+  A.B = c->bb;
+  A.ctr = c->ctr;
+  A.film = dfilm;
+  A.W = prm->width;
+  A.H = prm->height;
+  A.P = P;
+  A.seed = prm->seed;
+  A.ctl = prm->control_length;
+  A.maxlen = prm->max_path_length > 0 ? prm->max_path_length : 10;
+  A.faithful = prm->faithful;
+  const bool count = prm->count_work != 0;
+  const BdptBuf& B = c->bb;
+  int* ext_cnt = &c->ctr->ext_count[0];
+  int* sq_cnt = &c->ctr->sq_count;
+  const int g = shade_grid(c, P);
+  for (int it = 0; it < prm->iterations; ++it) {
+    A.iter = static_cast<uint32_t>(prm->iter_begin + it);
+    // ---------------- light pass (:67-131)
+    HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), c->stream));
+    hipLaunchKernelGGL(k_light_gen, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+    tm.mark(WR_K_GEN);
+    int cur = 0;
+    for (int b = 0; b < A.maxlen - 1; ++b) {
+      trace_launch(c, tm, count, B.q_o[cur], B.q_d[cur], P, ext_cnt + cur, B.q_t[cur], B.q_prim[cur], P);
+      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), c->stream));
+      hipLaunchKernelGGL(k_light_shade, dim3(g), dim3(kShadeBlock), 0, c->stream, A, cur);
+      tm.mark(WR_K_SHADE);
+      cur ^= 1;
+    }
+    trace_launch(c, tm, count, B.s_o, B.s_d, B.cap_sq, sq_cnt, B.s_t, B.s_prim, P);
+    hipLaunchKernelGGL(k_sq_resolve, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+    tm.mark(WR_K_RESOLVE);
+    // ---------------- camera pass (:133-264)
+    hipLaunchKernelGGL(k_camera_gen, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+    tm.mark(WR_K_GEN);
+    cur = 0;
+    for (int b = 0; b < A.maxlen; ++b) {
+      trace_launch(c, tm, count, B.q_o[cur], B.q_d[cur], P, ext_cnt + cur, B.q_t[cur], B.q_prim[cur], P);
+      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), c->stream));  // next extension queue
+      HIPCHK(hipMemsetAsync(sq_cnt, 0, 2 * sizeof(int), c->stream));           // sq_count, di_count
+      hipLaunchKernelGGL(k_camera_shade, dim3(g), dim3(kShadeBlock), 0, c->stream, A, cur);
+      tm.mark(WR_K_SHADE);
+      trace_launch(c, tm, count, B.s_o, B.s_d, B.cap_sq, sq_cnt, B.s_t, B.s_prim, B.cap_sq);
+      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, B.cap_sq)), dim3(kShadeBlock), 0, c->stream, A);
+      hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+      tm.mark(WR_K_RESOLVE);
+      cur ^= 1;
+    }
+  }
+  HIPCHK(hipGetLastError());
+  if (int rc = film_return(c, film, film_on_device, nf)) return rc;
+  return finish_stats(c, st, t0);
+}
+
+int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int film_on_device, wr_stats* st) {
+  if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
+  if (prm->width <= 0 || prm->height <= 0 || prm->spp <= 0) return fail(WR_E_ARG, "bad film size / spp");
+  if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "path tracing needs at least one area light");
+  HIPCHK(hipSetDevice(c->device));
+  const double t0 = host_now();
+  const int P = prm->width * prm->height;
+  if (int rc = ensure_work(c, 2, P)) return rc;
+  float* dfilm = nullptr;
+  const size_t nf = size_t(P) * 3;
+  if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
+  HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(DevCounters), c->stream));
+  begin_stats(c, prm->time_kernels);
+  Timer tm(c);
+  tm.mark(WR_K_OTHER);
+  PtArgs A;
+  A.S = c->ds;
+  A.T = c->pb;
+  A.ctr = c->ctr;
+  A.film = dfilm;
+  A.W = prm->width;
+  A.H = prm->height;
+  A.P = P;
+  A.spp = prm->spp;
+  A.grid_len = static_cast<int>(std::sqrt(static_cast<double>(prm->spp)));
+  A.max_depth = prm->max_depth;
+  A.seed = prm->seed;
+  const bool count = prm->count_work != 0;
+  const PtBuf& T = c->pb;
+  int* ext_cnt = &c->ctr->ext_count[0];
+  int* sq_cnt = &c->ctr->sq_count;
+  const int g = shade_grid(c, P);
+  const int k0 = prm->sample_begin;
+  const int k1 = prm->sample_count > 0 ? k0 + prm->sample_count : prm->spp;
+  for (int k = k0; k < k1; ++k) {
+    A.k = static_cast<uint32_t>(k);
+    hipLaunchKernelGGL(k_pt_gen, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+    tm.mark(WR_K_GEN);
+    int cur = 0;
+    for (int b = 0; b <= A.max_depth; ++b) {
+      trace_launch(c, tm, count, T.q_o[cur], T.q_d[cur], P, ext_cnt + cur, T.q_t[cur], T.q_prim[cur], P);
+      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), c->stream));
+      HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), c->stream));
+      hipLaunchKernelGGL(k_pt_shade, dim3(g), dim3(kShadeBlock), 0, c->stream, A, cur);
+      tm.mark(WR_K_SHADE);
+      trace_launch(c, tm, count, T.s_o, T.s_d, P, sq_cnt, T.s_t, T.s_prim, P);
+      hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+      tm.mark(WR_K_RESOLVE);
+      cur ^= 1;
+    }
+  }
+  HIPCHK(hipGetLastError());
+  if (int rc = film_return(c, film, film_on_device, nf)) return rc;
+  return finish_stats(c, st, t0);
+}
+
+int wr_film_write_ppm(const float* film, int height, int width, float scale, float gamma, int transpose,
+                      const char* path) {
+  if (!film || !path || height <= 0 || width <= 0) return fail(WR_E_ARG, "bad argument");
+  if (transpose && height != width) return fail(WR_E_ARG, "transpose needs a square film (bidirPathTracing.cpp:31-44)");
+  std::vector<unsigned char> img(size_t(height) * width * 3);
+  const float inv_gamma = 1.f / gamma;
+  for (int i = 0; i < height; ++i)
+    for (int j = 0; j < width; ++j) {
+      const float* c = transpose ? film + 3 * (size_t(j) * width + i) : film + 3 * (size_t(i) * width + j);
+      for (int ch = 0; ch < 3; ++ch) {
+        float v = c[ch] * scale;                                  // ImageFilm::scale
+        v = std::min(1.0f, std::max(v, 0.0f));                    // Color3::clamp
+        v = std::pow(v, inv_gamma);                               // Color3::gamma
+        img[3 * (size_t(i) * width + j) + ch] = static_cast<unsigned char>(v * 255.0);  // Color3::R()
+      }
+    }
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return fail(WR_E_IO, std::string("cannot write ") + path);
+  std::fprintf(f, "P6\n%d %d\n255\n", width, height);
+  std::fwrite(img.data(), 1, img.size(), f);
+  std::fclose(f);
+  return WR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,219 @@
+"""ctypes binding to libwinmad_rt.so (include/winmad_rt.h).
+
+The library is built in-tree (`make -C winmad-s-raytracer-v1.0_amd`, or
+`__graft_entry__.build()`).  There is no fallback: if the HIP library cannot be
+loaded every call raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libwinmad_rt.so")
+
+WR_OK, WR_E_ARG, WR_E_IO, WR_E_HIP, WR_E_SCENE, WR_E_NODEVICE = 0, -1, -2, -3, -4, -5
+K_TRACE, K_SHADE, K_RESOLVE, K_GEN, K_OTHER = 0, 1, 2, 3, 4
+
+# every entry point declared in include/winmad_rt.h
+EXPORTS = ["wr_scene_load", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free", "wr_device_count",
+           "wr_create", "wr_destroy", "wr_trace_closest", "wr_occluded", "wr_render_bdpt", "wr_render_path",
+           "wr_film_write_ppm", "wr_last_error", "wr_api_version"]
+
+
+class WrRay(C.Structure):
+    _fields_ = [("o", C.c_float * 3), ("d", C.c_float * 3), ("tmin", C.c_float), ("tmax", C.c_float)]
+
+
+class WrHit(C.Structure):
+    _fields_ = [("t", C.c_float), ("p", C.c_float * 3), ("n", C.c_float * 3), ("prim", C.c_int32),
+                ("inside", C.c_int32), ("mat_id", C.c_int32)]
+
+
+class WrSceneInfo(C.Structure):
+    _fields_ = [("nprims", C.c_int32), ("ntriangles", C.c_int32), ("nspheres", C.c_int32),
+                ("nlights", C.c_int32), ("nmaterials", C.c_int32), ("kd_depth_max", C.c_int32),
+                ("kd_inner", C.c_int32), ("kd_leaves", C.c_int32), ("kd_refs", C.c_int64),
+                ("kd_max_stack", C.c_int32), ("missing_files", C.c_int32), ("camera_xres", C.c_float),
+                ("camera_yres", C.c_float), ("device_bytes", C.c_int64)]
+
+
+class WrBdptParams(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("iterations", C.c_int32),
+                ("iter_begin", C.c_int32), ("control_length", C.c_int32), ("max_path_length", C.c_int32),
+                ("seed", C.c_uint32), ("faithful", C.c_int32), ("time_kernels", C.c_int32),
+                ("count_work", C.c_int32)]
+
+
+class WrPathParams(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32), ("max_depth", C.c_int32),
+                ("sample_begin", C.c_int32), ("sample_count", C.c_int32), ("seed", C.c_uint32),
+                ("time_kernels", C.c_int32), ("count_work", C.c_int32)]
+
+
+class WrStats(C.Structure):
+    _fields_ = [("closest_rays", C.c_int64), ("shadow_rays", C.c_int64), ("inner_visits", C.c_int64),
+                ("leaf_visits", C.c_int64), ("prim_refs", C.c_int64), ("seconds", C.c_double),
+                ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
+        d["kernel_ms"] = list(self.kernel_ms)
+        d["kernel_launches"] = list(self.kernel_launches)
+        return d
+
+
+class WrError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"winmad_rt error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C {PKG_DIR}` "
+                               "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        P, I, I64 = C.c_void_p, C.c_int, C.c_int64
+        L.wr_scene_load.argtypes = [C.c_char_p, C.POINTER(P)]
+        L.wr_scene_info_get.argtypes = [P, C.POINTER(WrSceneInfo)]
+        L.wr_scene_dump.argtypes = [P, C.c_char_p]
+        L.wr_scene_free.argtypes = [P]
+        L.wr_scene_free.restype = None
+        L.wr_create.argtypes = [P, I, C.POINTER(P)]
+        L.wr_destroy.argtypes = [P]
+        L.wr_destroy.restype = None
+        L.wr_trace_closest.argtypes = [P, C.POINTER(WrRay), I64, C.POINTER(WrHit)]
+        L.wr_occluded.argtypes = [P, C.POINTER(WrRay), C.POINTER(C.c_float), I64, C.POINTER(C.c_uint8)]
+        L.wr_render_bdpt.argtypes = [P, C.POINTER(WrBdptParams), P, I, C.POINTER(WrStats)]
+        L.wr_render_path.argtypes = [P, C.POINTER(WrPathParams), P, I, C.POINTER(WrStats)]
+        L.wr_film_write_ppm.argtypes = [C.POINTER(C.c_float), I, I, C.c_float, C.c_float, I, C.c_char_p]
+        L.wr_last_error.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != WR_OK:
+        raise WrError(rc, lib().wr_last_error().decode())
+    return rc
+
+
+def device_count():
+    return lib().wr_device_count()
+
+
+class Scene:
+    """Scene::init (scene.cpp:469-489): .scene + .obj + KD tree, host side."""
+
+    def __init__(self, path):
+        h = C.c_void_p()
+        check(lib().wr_scene_load(os.fsencode(path), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().wr_scene_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def info(self):
+        i = WrSceneInfo()
+        check(lib().wr_scene_info_get(self.h, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in i._fields_}
+
+    def dump(self, path):
+        check(lib().wr_scene_dump(self.h, os.fsencode(path)))
+        with open(path) as f:
+            return f.read()
+
+
+def rays_from_arrays(o, d, tmin=0.0, tmax=1e7):
+    n = o.shape[0]
+    arr = np.zeros((n, 8), np.float32)
+    arr[:, 0:3] = o
+    arr[:, 3:6] = d
+    arr[:, 6] = tmin
+    arr[:, 7] = tmax
+    return arr
+
+
+class Context:
+    """Scene resident in HBM on one device + one HIP stream."""
+
+    def __init__(self, scene, device=0):
+        h = C.c_void_p()
+        check(lib().wr_create(scene.h, device, C.byref(h)))
+        self.h = h
+        self.scene = scene
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().wr_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def trace_closest(self, rays8):
+        """rays8: (n, 8) float32 = o, d, tmin, tmax (d used as given)."""
+        rays8 = np.ascontiguousarray(rays8, np.float32)
+        n = rays8.shape[0]
+        hits = np.zeros(n, dtype=np.dtype([("t", "f4"), ("p", "f4", 3), ("n", "f4", 3), ("prim", "i4"),
+                                           ("inside", "i4"), ("mat_id", "i4")]))
+        check(lib().wr_trace_closest(self.h, rays8.ctypes.data_as(C.POINTER(WrRay)), n,
+                                     hits.ctypes.data_as(C.POINTER(WrHit))))
+        return hits
+
+    def occluded(self, rays8, targets):
+        rays8 = np.ascontiguousarray(rays8, np.float32)
+        targets = np.ascontiguousarray(targets, np.float32)
+        n = rays8.shape[0]
+        out = np.zeros(n, np.uint8)
+        check(lib().wr_occluded(self.h, rays8.ctypes.data_as(C.POINTER(WrRay)),
+                                targets.ctypes.data_as(C.POINTER(C.c_float)), n,
+                                out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out
+
+    def render_bdpt(self, width, height, iterations=1, seed=5489, iter_begin=0, control_length=3,
+                    max_path_length=10, faithful=1, time_kernels=0, count_work=0, film=None, film_ptr=None):
+        """BidirPathTracing::render.  Host film (numpy, accumulated) or a device
+        pointer (film_ptr, e.g. a torch tensor's data_ptr())."""
+        p = WrBdptParams(width, height, iterations, iter_begin, control_length, max_path_length, seed,
+                         faithful, time_kernels, count_work)
+        st = WrStats()
+        if film_ptr is not None:
+            check(lib().wr_render_bdpt(self.h, C.byref(p), C.c_void_p(film_ptr), 1, C.byref(st)))
+            return None, st
+        if film is None:
+            film = np.zeros((height, width, 3), np.float32)
+        check(lib().wr_render_bdpt(self.h, C.byref(p), film.ctypes.data_as(C.c_void_p), 0, C.byref(st)))
+        return film, st
+
+    def render_path(self, width, height, spp, max_depth=7, seed=5489, sample_begin=0, sample_count=0,
+                    time_kernels=0, count_work=0, film=None, film_ptr=None):
+        """SurfaceIntegrator::render + PathIntegrator (film = SUM over samples)."""
+        p = WrPathParams(width, height, spp, max_depth, sample_begin, sample_count, seed, time_kernels,
+                         count_work)
+        st = WrStats()
+        if film_ptr is not None:
+            check(lib().wr_render_path(self.h, C.byref(p), C.c_void_p(film_ptr), 1, C.byref(st)))
+            return None, st
+        if film is None:
+            film = np.zeros((height, width, 3), np.float32)
+        check(lib().wr_render_path(self.h, C.byref(p), film.ctypes.data_as(C.c_void_p), 0, C.byref(st)))
+        return film, st
+
+
+def write_ppm(film, path, scale=1.0, gamma=2.2, transpose=False):
+    """ImageFilm::outputImage pipeline (film.cpp:39-64) to a binary PPM."""
+    film = np.ascontiguousarray(film, np.float32)
+    h, w = film.shape[:2]
+    check(lib().wr_film_write_ppm(film.ctypes.data_as(C.POINTER(C.c_float)), h, w, scale, gamma,
+                                  1 if transpose else 0, os.fsencode(path)))
