@@ -34,19 +34,29 @@ def algorithmic_bytes(rays, inner, leaves, refs):
     return 48.0 * rays + 8.0 * (inner + leaves) + 4.0 * refs + 40.0 * refs
 
 
-def cpu_baseline(scene_path, W, H, budget_paths):
+def cpu_baseline(scene_path, W, H, budget_paths, chunks=16):
     """Oracle (oracle/cpuref.c, C port of the reference path), MT-serial RNG,
-    one thread, on the first `budget_paths` path indices of one iteration."""
+    one thread, on `budget_paths` path indices of one iteration taken as
+    `chunks` evenly spaced contiguous runs (so sky rows and floor rows are
+    sampled in proportion)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle
     s = _oracle.Scene(scene_path)
-    t0 = time.perf_counter()
-    _, st = s.bdpt(W, H, 1, 5489, mode=0, path_range=(0, budget_paths))
-    dt = time.perf_counter() - t0
-    rays = st.closest_rays + st.shadow_rays
+    P = W * H
+    per = budget_paths // chunks
+    rays = 0
+    dt = 0.0
+    for c in range(chunks):
+        b = c * P // chunks
+        t0 = time.perf_counter()
+        _, st = s.bdpt(W, H, 1, 5489 + c, mode=0, path_range=(b, b + per))
+        dt += time.perf_counter() - t0
+        rays += st.closest_rays + st.shadow_rays
+    n = per * chunks
     return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/cpuref.c MT-serial BDPT, torus 1920x1080, path indices [0,{budget_paths}) "
-                      f"of one iteration ({rays} rays, {dt:.1f} s); spp/s={budget_paths / dt:.0f}"}
+            "sample": f"oracle/cpuref.c MT-serial BDPT, torus {W}x{H}, {n} camera+light path pairs of one "
+                      f"iteration in {chunks} evenly spaced runs ({rays} rays, {dt:.1f} s CPU); "
+                      f"spp/s={n / dt:.0f}"}
 
 
 def main():
@@ -56,7 +66,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--cpu-paths", type=int, default=400000)
+    ap.add_argument("--cpu-paths", type=int, default=1000000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting replay")
     args = ap.parse_args()

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Profiling passes on the GPU box (run from the repo root via gpurun).
+# 1) kernel trace + stats for the bench command, 2) PMC passes (one counter
+# group per run, --kernel-trace only: no sys/runtime trace with --pmc).
+# Usage: scripts/profile_round.sh <tag> [bench args...]
+set -o pipefail
+TAG=${1:-r1}; shift
+ARGS=${@:---steps 4 --warmup 1 --no-cpu --no-count}
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace pass failed rc=$?"; tail -5 $OUT/trace.log; exit 1; }
+echo "trace pass ok"
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
+           "SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS TCC_HIT_sum TCC_MISS_sum" \
+           "FETCH_SIZE" "WRITE_SIZE" "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TA_BUSY_avr"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu --no-count > $OUT/pmc$i.log 2>&1
+  rc=$?
+  if [ $rc -ne 0 ]; then echo "pmc pass $i failed rc=$rc"; tail -5 $OUT/pmc$i.log; fi
+  if [ $rc -ge 124 ]; then exit 1; fi  # timeout / abort / segfault: stop using the GPU
+done
+echo done

@@ -44,7 +44,7 @@ static int fail(int code, const std::string& msg) {
 namespace {
 
 constexpr int kVMax = 9;       // light vertices per subpath (pathLength 1..9, :77-124)
-constexpr int kTraceBlock = 128;
+constexpr int kTraceBlock = 64;  // one wave per workgroup: persistent traversal
 constexpr int kShadeBlock = 256;
 
 enum SqKind { SQ_SPLAT = 0, SQ_CONN = 1, SQ_NEE = 2, SQ_DIB = 3 };
@@ -54,6 +54,7 @@ struct DevCounters {
   int ext_count[2];
   int sq_count;
   int di_count;
+  int fetch;  // persistent-traversal queue cursor (reset before every trace launch)
   unsigned long long closest, shadow, inner, leaves, refs;
 };
 
@@ -100,26 +101,22 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 }
 
 // =============================================================== trace kernels
-// Generic queue traversal: rays [3][cap] SoA, count on device.
-template <bool COUNT>
+// Generic persistent queue traversal: rays [3][cap] SoA, count on device.
+template <bool COUNT, bool SPH>
 __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, const float* __restrict__ o3,
                                                        const float* __restrict__ d3, int cap,
-                                                       const int* __restrict__ count, float* __restrict__ out_t,
+                                                       const int* __restrict__ count,
+                                                       const float* __restrict__ rtmin,
+                                                       const float* __restrict__ rtmax, float* __restrict__ out_t,
                                                        int* __restrict__ out_prim, DevCounters* ctr) {
   extern __shared__ uint32_t smem[];
   const int stride = blockDim.x;
   uint32_t* sn = smem + threadIdx.x;
   float* s0 = reinterpret_cast<float*>(smem + S.max_stack * stride) + threadIdx.x;
   float* s1 = reinterpret_cast<float*>(smem + 2 * S.max_stack * stride) + threadIdx.x;
-  const int n = *count;
   TraceCounters tc{0, 0, 0};
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const V3 o = ld3(o3, cap, i), d = ld3(d3, cap, i);
-    float t;
-    const int prim = traverse<COUNT>(S, o, d, 0.f, WR_INF, t, sn, s0, s1, stride, tc);
-    out_t[i] = t;
-    out_prim[i] = prim;
-  }
+  trace_queue<COUNT, SPH>(S, o3, d3, cap, *count, rtmin, rtmax, out_t, out_prim, &ctr->fetch, sn, s0, s1, stride,
+                          tc);
   if (COUNT) {
     unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs);
     if (lane_id() == 0) {
@@ -130,43 +127,49 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, const float* 
   }
 }
 
-// C-ABI traversal: AoS wr_ray in, wr_hit (Intersection) / occluded flag out.
-__global__ void __launch_bounds__(kTraceBlock) k_trace_api(DevScene S, const wr_ray* rays, const float* targets,
-                                                           int64_t n, wr_hit* hits, uint8_t* occ) {
-  extern __shared__ uint32_t smem[];
-  const int stride = blockDim.x;
-  uint32_t* sn = smem + threadIdx.x;
-  float* s0 = reinterpret_cast<float*>(smem + S.max_stack * stride) + threadIdx.x;
-  float* s1 = reinterpret_cast<float*>(smem + 2 * S.max_stack * stride) + threadIdx.x;
-  TraceCounters tc{0, 0, 0};
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+// C-ABI traversal, before: AoS wr_ray -> SoA queue (occlusion rays re-normalised
+// as Scene::occluded's Ray(p1, dir) does, scene.cpp:74)
+__global__ void __launch_bounds__(256) k_api_prep(const wr_ray* rays, int n, int occ, float* o3, float* d3,
+                                                  float* tmin, float* tmax) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const wr_ray r = rays[i];
-    V3 o = v3(r.o[0], r.o[1], r.o[2]), d = v3(r.d[0], r.d[1], r.d[2]);
-    if (occ) d = normalize(d);  // Scene::occluded builds Ray(p1, dir) (scene.cpp:74)
-    float t;
-    const int prim = traverse<false>(S, o, d, r.tmin, r.tmax, t, sn, s0, s1, stride, tc);
+    V3 d = v3(r.d[0], r.d[1], r.d[2]);
+    if (occ) d = normalize(d);
+    st3(o3, n, i, v3(r.o[0], r.o[1], r.o[2]));
+    st3(d3, n, i, d);
+    tmin[i] = r.tmin;
+    tmax[i] = r.tmax;
+  }
+}
+// ... after: rebuild the Intersection (scene.cpp:25-27) or the occlusion answer
+__global__ void __launch_bounds__(256) k_api_finish(DevScene S, const float* o3, const float* d3, const float* t,
+                                                    const int* prim, const float* targets, int n, wr_hit* hits,
+                                                    uint8_t* occ) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const V3 o = ld3(o3, n, i), d = ld3(d3, n, i);
+    const int p = prim[i];
     if (occ) {
-      bool unocc = prim < 0 || near_eq(o + d * t, v3(targets[3 * i], targets[3 * i + 1], targets[3 * i + 2]));
+      const bool unocc = p < 0 || near_eq(o + d * t[i], v3(targets[3 * i], targets[3 * i + 1], targets[3 * i + 2]));
       occ[i] = unocc ? 0 : 1;
-    } else {
-      wr_hit h;
-      h.prim = prim;
-      if (prim >= 0) {
-        Hit x = rebuild_hit(S, prim, t, o, d);
-        h.t = x.t;
-        h.p[0] = x.p.x; h.p[1] = x.p.y; h.p[2] = x.p.z;
-        h.n[0] = x.n.x; h.n[1] = x.n.y; h.n[2] = x.n.z;
-        h.inside = x.inside;
-        h.mat_id = x.mat;
-      } else {
-        h.t = WR_INF;
-        h.p[0] = h.p[1] = h.p[2] = 0.f;
-        h.n[0] = h.n[1] = h.n[2] = 0.f;
-        h.inside = 0;
-        h.mat_id = 0;
-      }
-      hits[i] = h;
+      continue;
     }
+    wr_hit h;
+    h.prim = p;
+    if (p >= 0) {
+      const Hit x = rebuild_hit(S, p, t[i], o, d);
+      h.t = x.t;
+      h.p[0] = x.p.x; h.p[1] = x.p.y; h.p[2] = x.p.z;
+      h.n[0] = x.n.x; h.n[1] = x.n.y; h.n[2] = x.n.z;
+      h.inside = x.inside;
+      h.mat_id = x.mat;
+    } else {
+      h.t = WR_INF;
+      h.p[0] = h.p[1] = h.p[2] = 0.f;
+      h.n[0] = h.n[1] = h.n[2] = 0.f;
+      h.inside = 0;
+      h.mat_id = 0;
+    }
+    hits[i] = h;
   }
 }
 
@@ -987,6 +990,9 @@ struct wr_context {
   float* film_tmp = nullptr;
   size_t film_tmp_n = 0;
   int grid = 2048;
+  int cus = 256;
+  bool spheres = false;
+  int trace_blocks = 4096;  // resident one-wave workgroups of the traversal
   std::vector<hipEvent_t> events;
   size_t ev_used = 0;
   int ev_cat[4096];
@@ -1114,15 +1120,21 @@ struct Timer {
 };
 
 int trace_launch(wr_context* c, Timer& tm, bool count, const float* o3, const float* d3, int cap, const int* cnt,
-                 float* t, int* prim, int max_rays) {
+                 float* t, int* prim, int max_rays, const float* rtmin = nullptr, const float* rtmax = nullptr) {
   const size_t lds = size_t(3) * sizeof(uint32_t) * std::max(1, c->ds.max_stack) * kTraceBlock;
-  const int grid = std::max(1, std::min(c->grid, (max_rays + kTraceBlock - 1) / kTraceBlock));
-  if (count)
-    hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, o3, d3, cap, cnt, t,
-                       prim, c->ctr);
-  else
-    hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, o3, d3, cap, cnt, t,
-                       prim, c->ctr);
+  const int grid = std::max(1, std::min(c->trace_blocks, (max_rays + kTraceBlock - 1) / kTraceBlock));
+  (void)hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream);
+#define WR_TRACE_LAUNCH(CNT, SP)                                                                             \
+  hipLaunchKernelGGL((k_trace<CNT, SP>), dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, o3, d3, cap, cnt, \
+                     rtmin, rtmax, t, prim, c->ctr)
+  if (count) {
+    if (c->spheres) WR_TRACE_LAUNCH(true, true);
+    else WR_TRACE_LAUNCH(true, false);
+  } else {
+    if (c->spheres) WR_TRACE_LAUNCH(false, true);
+    else WR_TRACE_LAUNCH(false, false);
+  }
+#undef WR_TRACE_LAUNCH
   tm.mark(WR_K_TRACE);
   return WR_OK;
 }
@@ -1369,6 +1381,18 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   std::memcpy(d.cam.w2r, s.cam.w2r, sizeof d.cam.w2r);
   std::memcpy(d.cam.r2w, s.cam.r2w, sizeof d.cam.r2w);
   c->scene_bytes = static_cast<int64_t>(A.used);
+  for (const auto& p : s.prims) c->spheres |= p.type != wr::kTri;
+  {
+    // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
+    // and registers); more would only queue behind the first wave of blocks
+    const size_t lds = size_t(3) * sizeof(uint32_t) * d.max_stack * kTraceBlock;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, kTraceBlock, lds) != hipSuccess ||
+        per_cu <= 0)
+      per_cu = 8;
+    c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    c->trace_blocks = c->cus * per_cu;
+  }
   *out = c;
   return WR_OK;
 }
@@ -1385,35 +1409,46 @@ void wr_destroy(wr_context* c) {
   delete c;
 }
 
-static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, int64_t n, wr_hit* hits,
+static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, int64_t n64, wr_hit* hits,
                      uint8_t* occ) {
-  if (!c || (!rays && n) || n < 0) return fail(WR_E_ARG, "bad argument");
-  if (n == 0) return WR_OK;
+  if (!c || (!rays && n64) || n64 < 0) return fail(WR_E_ARG, "bad argument");
+  if (n64 == 0) return WR_OK;
+  if (n64 > (1 << 28)) return fail(WR_E_ARG, "at most 2^28 rays per call");
+  const int n = static_cast<int>(n64);
   HIPCHK(hipSetDevice(c->device));
-  wr_ray* dr = nullptr;
-  float* dt = nullptr;
-  wr_hit* dh = nullptr;
-  uint8_t* dox = nullptr;
-  HIPCHK(hipMalloc(&dr, n * sizeof(wr_ray)));
-  HIPCHK(hipMemcpyAsync(dr, rays, n * sizeof(wr_ray), hipMemcpyHostToDevice, c->stream));
-  if (occ) {
-    HIPCHK(hipMalloc(&dt, n * 3 * sizeof(float)));
-    HIPCHK(hipMalloc(&dox, n));
-    HIPCHK(hipMemcpyAsync(dt, targets, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
-  } else {
-    HIPCHK(hipMalloc(&dh, n * sizeof(wr_hit)));
-  }
-  const size_t lds = size_t(3) * sizeof(uint32_t) * c->ds.max_stack * kTraceBlock;
-  const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(c->grid, (n + kTraceBlock - 1) / kTraceBlock)));
-  hipLaunchKernelGGL(k_trace_api, dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, dr, dt, n, dh, dox);
+  // one scratch block: rays, SoA queue, results, counters
+  char* buf = nullptr;
+  const size_t nb = size_t(n);
+  const size_t bytes = nb * (sizeof(wr_ray) + 4 * 13 + sizeof(wr_hit) + 1) + 16 * 256;
+  HIPCHK(hipMalloc(&buf, bytes));
+  char* q = buf;
+  auto take = [&](size_t sz) { char* r = q; q += (sz + 255) & ~size_t(255); return r; };
+  wr_ray* dr = reinterpret_cast<wr_ray*>(take(nb * sizeof(wr_ray)));
+  float* o3 = reinterpret_cast<float*>(take(nb * 12));
+  float* d3 = reinterpret_cast<float*>(take(nb * 12));
+  float* tmn = reinterpret_cast<float*>(take(nb * 4));
+  float* tmx = reinterpret_cast<float*>(take(nb * 4));
+  float* tt = reinterpret_cast<float*>(take(nb * 4));
+  int* pr = reinterpret_cast<int*>(take(nb * 4));
+  float* dtg = reinterpret_cast<float*>(take(nb * 12));
+  wr_hit* dh = reinterpret_cast<wr_hit*>(take(nb * sizeof(wr_hit)));
+  uint8_t* dox = reinterpret_cast<uint8_t*>(take(nb));
+  int* cnt = reinterpret_cast<int*>(take(sizeof(int)));
+  HIPCHK(hipMemcpyAsync(dr, rays, nb * sizeof(wr_ray), hipMemcpyHostToDevice, c->stream));
+  if (occ) HIPCHK(hipMemcpyAsync(dtg, targets, nb * 12, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(cnt, &n, sizeof(int), hipMemcpyHostToDevice, c->stream));
+  const int g = std::max(1, std::min(c->grid, (n + 255) / 256));
+  hipLaunchKernelGGL(k_api_prep, dim3(g), dim3(256), 0, c->stream, dr, n, occ ? 1 : 0, o3, d3, tmn, tmx);
+  c->timing = false;
+  Timer tm(c);
+  trace_launch(c, tm, false, o3, d3, n, cnt, tt, pr, n, tmn, tmx);
+  hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
+                     occ ? dox : nullptr);
   HIPCHK(hipGetLastError());
-  if (occ) HIPCHK(hipMemcpyAsync(occ, dox, n, hipMemcpyDeviceToHost, c->stream));
-  else HIPCHK(hipMemcpyAsync(hits, dh, n * sizeof(wr_hit), hipMemcpyDeviceToHost, c->stream));
+  if (occ) HIPCHK(hipMemcpyAsync(occ, dox, nb, hipMemcpyDeviceToHost, c->stream));
+  else HIPCHK(hipMemcpyAsync(hits, dh, nb * sizeof(wr_hit), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  (void)hipFree(dr);
-  if (dt) (void)hipFree(dt);
-  if (dh) (void)hipFree(dh);
-  if (dox) (void)hipFree(dox);
+  (void)hipFree(buf);
   return WR_OK;
 }
 

@@ -70,13 +70,18 @@ __device__ __forceinline__ bool box_hit(V3 l, V3 r, V3 o, V3 d, float& t1, float
   return true;
 }
 
-// Triangle::hit, returning t (or a value > every accepted t on rejection).
-// The three quotients are the reference's correctly rounded divisions; the beta
-// quotient is first screened with v_rcp_f32: a ray whose approximate beta lies
-// clearly outside [-EPS, 1] (margin 1e-5 relative, far above the rcp error)
-// would be rejected by the exact test too, so the screen never changes a result.
-__device__ __forceinline__ bool tri_hit(float4 a, float4 b, float f, V3 o, V3 d, float rtmin, float rtmax,
-                                        float& t_out) {
+// Triangle::hit (triangle.cpp:22-87) inside the closest-hit loop.
+// The reference forms beta, gamma and t with three correctly rounded divisions
+// by `denom`; here the quotients are first estimated with one v_rcp_f32 and a
+// candidate is dropped early only when the estimate proves the exact test would
+// drop it too (margins 1e-5 relative, ~40x the estimate's error):
+//   beta  < -EPS or > 1,  gamma < -EPS,  beta + gamma > 1,  t <= EPS,  t > tmax,
+//   or t cannot improve the current best (cmp(t - best) < 0 impossible) -- a hit
+//   that does not improve has no effect in the reference's leaf loop either.
+// Survivors take the exact divisions, so accept / reject and t are bit-exact.
+// Estimates are used only for |denom| in (1e-30, 1e30); NaN estimates fall through.
+__device__ __forceinline__ bool tri_test(float4 a, float4 b, float f, V3 o, V3 d, float rtmin, float rtmax,
+                                         float t_best, float& t_out) {
   const float A = a.w, B = b.x, C = b.y, D = b.z, E = b.w, F = f;
   const float G = d.x, H = d.y, I = d.z;
   const float J = a.x - o.x, K = a.y - o.y, L = a.z - o.z;
@@ -85,20 +90,26 @@ __device__ __forceinline__ bool tri_hit(float4 a, float4 b, float f, V3 o, V3 d,
   const float DHEG = D * H - E * G;
   const float denom = A * EIHF + B * GFDI + C * DHEG;
   const float bnum = J * EIHF + K * GFDI + L * DHEG;
-  const float ad = fabsf(denom);
-  if (ad > 1e-30f && ad < 1e30f) {
-    const float ba = bnum * __builtin_amdgcn_rcpf(denom);
-    const float m = 1e-5f * fabsf(ba);
-    if (ba < -WR_EPS - m || ba > 1.f + m) return false;
-  }
-  const float beta = bnum / denom;
-  if (cmpf(beta) < 0 || beta > 1.f) return false;
   const float AKJB = A * K - J * B;
   const float JCAL = J * C - A * L;
   const float BLKC = B * L - K * C;
-  const float gamma = (I * AKJB + H * JCAL + G * BLKC) / denom;
+  const float gnum = I * AKJB + H * JCAL + G * BLKC;
+  const float tnum = -(F * AKJB + E * JCAL + D * BLKC);
+  const float ad = fabsf(denom);
+  if (ad > 1e-30f && ad < 1e30f) {
+    const float r = __builtin_amdgcn_rcpf(denom);
+    const float ba = bnum * r, ga = gnum * r, ta = tnum * r;
+    const float mb = 1e-5f * fabsf(ba), mg = 1e-5f * fabsf(ga), mt = 1e-5f * fabsf(ta);
+    if (ba < -WR_EPS - mb || ba > 1.f + mb) return false;
+    if (ga < -WR_EPS - mg || ba + ga > 1.f + (mb + mg) + 1e-6f) return false;
+    if (ta < WR_EPS - mt || ta > rtmax + mt) return false;
+    if (ta - t_best > -WR_EPS + (mt + 1e-5f * fabsf(t_best))) return false;
+  }
+  const float beta = bnum / denom;
+  if (cmpf(beta) < 0 || beta > 1.f) return false;
+  const float gamma = gnum / denom;
   if (cmpf(gamma) < 0 || beta + gamma > 1.f) return false;
-  const float t = -(F * AKJB + E * JCAL + D * BLKC) / denom;
+  const float t = tnum / denom;
   if (cmpf(t) <= 0) return false;
   if (t < rtmin || t > rtmax) return false;
   t_out = t;
@@ -140,76 +151,147 @@ __device__ __forceinline__ bool sph_hit(const DevScene& S, int prim, V3 o, V3 d,
   return true;
 }
 
-// Closest hit.  `stk_*` point at this lane's LDS column (stride = blockDim).
-template <bool COUNT>
-__device__ __forceinline__ int traverse(const DevScene& S, V3 o, V3 d, float rtmin, float rtmax, float& t_best,
-                                        uint32_t* stk_node, float* stk_tmin, float* stk_tmax, int stride,
-                                        TraceCounters& ctr) {
-  t_best = WR_INF;
-  float tmin, tmax;
-  if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax)) return -1;
-  const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-  int sp = 0;
-  int best = -1;
+// Persistent closest-hit traversal over a ray queue (one wave per workgroup).
+//
+// KDtreeAccel::traverse semantics per ray; the SIMT structure is GPU-specific:
+//   * while-while: every live lane first descends inner nodes until it stands on
+//     a leaf, then all lanes test their leaves together, then pop -- so the
+//     expensive leaf loop runs with the wave full instead of interleaved with
+//     inner-node steps of other lanes;
+//   * lanes that finish their ray take the next one from a global counter (one
+//     atomic per wave per refill), so a wave stays full until the queue drains;
+//   * leaf references are prefetched one ahead (the 40-byte record of the next
+//     triangle is in flight while the current one is tested).
+// `rtmin3 / rtmax3` (optional) give per-ray [tmin, tmax]; default [0, INF].
+template <bool COUNT, bool SPH>
+__device__ __forceinline__ void trace_queue(const DevScene& S, const float* __restrict__ o3,
+                                            const float* __restrict__ d3, int cap, int n,
+                                            const float* __restrict__ rtmin_a, const float* __restrict__ rtmax_a,
+                                            float* __restrict__ out_t, int* __restrict__ out_prim, int* fetch,
+                                            uint32_t* stk_node, float* stk_tmin, float* stk_tmax, int stride,
+                                            TraceCounters& ctr) {
+  int r = -1;            // ray held by this lane (-1: none)
+  bool pool = true;      // wave-uniform: queue not yet exhausted
+  V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
+  float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmin = 0.f, rtmax = WR_INF;
+  int best = -1, sp = 0;
   uint32_t node = 0;
   for (;;) {
-    if (rtmax < tmin) break;
-    const uint2 nd = S.nodes[node];
-    const uint32_t axis = nd.y & 3u;
-    if (axis != 3u) {
-      if (COUNT) ++ctr.inner;
-      const float split = __uint_as_float(nd.x);
-      const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-      const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-      const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
-      const float t = (split - oa) * ia;
-      const bool below = (oa < split) || (oa == split && da <= 0);
-      const uint32_t left = node + 1, right = nd.y >> 2;
-      const uint32_t nearc = below ? left : right, farc = below ? right : left;
-      if (t > tmax || t <= 0) {
-        node = nearc;
-      } else if (t < tmin) {
-        node = farc;
-      } else {
-        stk_node[sp * stride] = farc;
-        stk_tmin[sp * stride] = t;
-        stk_tmax[sp * stride] = tmax;
-        ++sp;
-        node = nearc;
-        tmax = t;
+    // ---- refill idle lanes
+    if (pool) {
+      const bool idle = r < 0;
+      if (__ballot(idle)) {
+        const unsigned long long m = __ballot(idle);
+        const int lane = __lane_id();
+        const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(fetch, __popcll(m));
+        base = __shfl(base, leader);
+        const int idx = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (idle) {
+          if (idx < n) {
+            r = idx;
+            o = v3(o3[idx], o3[cap + idx], o3[2 * cap + idx]);
+            d = v3(d3[idx], d3[cap + idx], d3[2 * cap + idx]);
+            rtmin = rtmin_a ? rtmin_a[idx] : 0.f;
+            rtmax = rtmax_a ? rtmax_a[idx] : WR_INF;
+            t_best = WR_INF;
+            best = -1;
+            sp = 0;
+            node = 0;
+            if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) {
+              out_t[idx] = WR_INF;
+              out_prim[idx] = -1;
+              r = -1;
+            } else {
+              inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+            }
+          }
+        }
+        if (__ballot(idle && idx >= n)) pool = false;
       }
-    } else {
+    }
+    if (!__ballot(r >= 0)) {
+      if (!pool) break;
+      continue;
+    }
+    if (r >= 0) {
+      // ---- descend to a leaf (KDtreeAccel.cpp:325-358)
+      uint2 nd = S.nodes[node];
+      while ((nd.y & 3u) != 3u) {
+        if (COUNT) ++ctr.inner;
+        const uint32_t axis = nd.y & 3u;
+        const float split = __uint_as_float(nd.x);
+        const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+        const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+        const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
+        const float t = (split - oa) * ia;
+        const bool below = (oa < split) || (oa == split && da <= 0);
+        const uint32_t left = node + 1, right = nd.y >> 2;
+        const uint32_t nearc = below ? left : right, farc = below ? right : left;
+        if (t > tmax || t <= 0) {
+          node = nearc;
+        } else if (t < tmin) {
+          node = farc;
+        } else {
+          stk_node[sp * stride] = farc;
+          stk_tmin[sp * stride] = t;
+          stk_tmax[sp * stride] = tmax;
+          ++sp;
+          node = nearc;
+          tmax = t;
+        }
+        nd = S.nodes[node];
+      }
+      // ---- leaf: every primitive in objlist order, first-found wins (:359-373)
       const uint32_t first = nd.x, count = nd.y >> 2;
       if (COUNT) {
         ++ctr.leaves;
         ctr.refs += count;
       }
-      for (uint32_t i = 0; i < count; ++i) {
-        const float2 c = S.ref_c[first + i];
-        const int prim = __float_as_int(c.y);
-        float t;
-        bool h;
-        if (prim >= 0) {
-          h = tri_hit(S.ref_a[first + i], S.ref_b[first + i], c.x, o, d, rtmin, rtmax, t);
-        } else {
-          h = sph_hit(S, -prim - 1, o, d, rtmin, rtmax, t);
-        }
-        if (h && cmpf(t - t_best) < 0) {
-          t_best = t;
-          best = prim >= 0 ? prim : -prim - 1;
+      if (count) {
+        const uint32_t end = first + count;
+        float4 a = S.ref_a[first], b = S.ref_b[first];
+        float2 c = S.ref_c[first];
+        for (uint32_t i = first; i < end;) {
+          const float4 ca = a, cb = b;
+          const float2 cc = c;
+          ++i;
+          const uint32_t j = i < end ? i : end - 1;
+          a = S.ref_a[j];
+          b = S.ref_b[j];
+          c = S.ref_c[j];
+          const int prim = __float_as_int(cc.y);
+          float t;
+          bool h;
+          if (!SPH || prim >= 0) {
+            h = tri_test(ca, cb, cc.x, o, d, rtmin, rtmax, t_best, t);
+          } else {
+            h = sph_hit(S, -prim - 1, o, d, rtmin, rtmax, t);
+          }
+          if (h && cmpf(t - t_best) < 0) {
+            t_best = t;
+            best = (!SPH || prim >= 0) ? prim : -prim - 1;
+          }
         }
       }
+      // ---- pop (:375-383); tmin only changes here, so the `ray.tmax < tmin`
+      // check of :323 is evaluated after every pop
+      bool done = true;
       if (sp > 0) {
         --sp;
         node = stk_node[sp * stride];
         tmin = stk_tmin[sp * stride];
         tmax = stk_tmax[sp * stride];
-      } else {
-        break;
+        done = rtmax < tmin;
+      }
+      if (done) {
+        out_t[r] = t_best;
+        out_prim[r] = best;
+        r = -1;
       }
     }
   }
-  return best;
 }
 
 // Scene::intersect re-runs hit() on the winner (scene.cpp:25-27); from (t, prim)

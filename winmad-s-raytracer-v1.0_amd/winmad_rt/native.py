@@ -72,10 +72,24 @@ class WrError(RuntimeError):
 _lib = None
 
 
+def _share_torch_runtime():
+    """PyTorch-ROCm ships its own libamdhip64 with the same SONAME
+    (libamdhip64.so.7) as /opt/rocm's.  If torch is loaded first, the dynamic
+    linker binds libwinmad_rt.so to that copy and the process has ONE HIP
+    runtime (device pointers of torch tensors are then valid for wr_* calls).
+    Loaded the other way round there would be two runtimes and torch's fails to
+    initialise, so torch -- when installed -- is imported before our library."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib():
     """Load the in-tree HIP library (raises if it has not been built)."""
     global _lib
     if _lib is None:
+        _share_torch_runtime()
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C {PKG_DIR}` "
                                "(or __graft_entry__.build()); there is no CPU fallback")
