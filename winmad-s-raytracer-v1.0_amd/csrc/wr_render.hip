@@ -103,20 +103,10 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 // =============================================================== trace kernels
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
 template <bool COUNT, bool SPH>
-__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, const float* __restrict__ o3,
-                                                       const float* __restrict__ d3, int cap,
-                                                       const int* __restrict__ count,
-                                                       const float* __restrict__ rtmin,
-                                                       const float* __restrict__ rtmax, float* __restrict__ out_t,
-                                                       int* __restrict__ out_prim, DevCounters* ctr) {
+__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, RayQueue qa, RayQueue qb, DevCounters* ctr) {
   extern __shared__ uint32_t smem[];
-  const int stride = blockDim.x;
-  uint32_t* sn = smem + threadIdx.x;
-  float* s0 = reinterpret_cast<float*>(smem + S.max_stack * stride) + threadIdx.x;
-  float* s1 = reinterpret_cast<float*>(smem + 2 * S.max_stack * stride) + threadIdx.x;
   TraceCounters tc{0, 0, 0};
-  trace_queue<COUNT, SPH>(S, o3, d3, cap, *count, rtmin, rtmax, out_t, out_prim, &ctr->fetch, sn, s0, s1, stride,
-                          tc);
+  trace_queue<COUNT, SPH>(S, qa, qb, &ctr->fetch, smem, tc);
   if (COUNT) {
     unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs);
     if (lane_id() == 0) {
@@ -401,9 +391,22 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptArgs A) {
   const BdptBuf& B = A.B;
   const DCam& cam = A.S.cam;
   const int P = A.P;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+  // queue order: 8x8 raster tiles per wave (coherent primary rays); the
+  // path <-> pixel mapping stays the reference's (x = p / W, y = p % W, :422-423)
+  const bool tiled = (A.W % 8) == 0 && (A.H % 8) == 0;
+  const int tiles_y = A.W / 8;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < P; s += gridDim.x * blockDim.x) {
+    int x, y;
+    if (tiled) {
+      const int t = s >> 6, w = s & 63;
+      x = (t / tiles_y) * 8 + (w >> 3);
+      y = (t % tiles_y) * 8 + (w & 7);
+    } else {
+      x = s / A.W;
+      y = s % A.W;
+    }
+    const int p = x * A.W + y;
     Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), 0};
-    const int y = p % A.W, x = p / A.W;
     const V3 jit = rng.v();
     const float sx = static_cast<float>(x) + jit.x, sy = static_cast<float>(y) + jit.y;
     const V3 rp = t_point(cam.r2w, v3(sx, sy, 0.f));
@@ -420,9 +423,9 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptArgs A) {
     B.c_nspec[p] = 0;
     B.c_ctr[p] = rng.ctr;
     B.c_pix[p] = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
-    st3(B.q_o[0], P, p, cam.pos + d * WR_EPS);
-    st3(B.q_d[0], P, p, normalize(d));
-    B.q_path[0][p] = p;
+    st3(B.q_o[0], P, s, cam.pos + d * WR_EPS);
+    st3(B.q_d[0], P, s, normalize(d));
+    B.q_path[0][s] = p;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->ext_count[0] = P;
 }
@@ -1119,14 +1122,19 @@ struct Timer {
   }
 };
 
-int trace_launch(wr_context* c, Timer& tm, bool count, const float* o3, const float* d3, int cap, const int* cnt,
-                 float* t, int* prim, int max_rays, const float* rtmin = nullptr, const float* rtmax = nullptr) {
-  const size_t lds = size_t(3) * sizeof(uint32_t) * std::max(1, c->ds.max_stack) * kTraceBlock;
+RayQueue rq(const float* o3, const float* d3, int cap, const int* cnt, float* t, int* prim,
+            const float* tmin = nullptr, const float* tmax = nullptr) {
+  return RayQueue{o3, d3, cap, cnt, tmin, tmax, t, prim};
+}
+const RayQueue kNoQueue{nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+
+// One persistent traversal launch over qa then qb (max_rays bounds the grid).
+int trace_launch(wr_context* c, Timer& tm, bool count, const RayQueue& qa, const RayQueue& qb, int max_rays) {
+  const size_t lds = trace_lds_bytes(c->ds.max_stack);
   const int grid = std::max(1, std::min(c->trace_blocks, (max_rays + kTraceBlock - 1) / kTraceBlock));
   (void)hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream);
-#define WR_TRACE_LAUNCH(CNT, SP)                                                                             \
-  hipLaunchKernelGGL((k_trace<CNT, SP>), dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, o3, d3, cap, cnt, \
-                     rtmin, rtmax, t, prim, c->ctr)
+#define WR_TRACE_LAUNCH(CNT, SP) \
+  hipLaunchKernelGGL((k_trace<CNT, SP>), dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, qa, qb, c->ctr)
   if (count) {
     if (c->spheres) WR_TRACE_LAUNCH(true, true);
     else WR_TRACE_LAUNCH(true, false);
@@ -1385,7 +1393,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   {
     // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
     // and registers); more would only queue behind the first wave of blocks
-    const size_t lds = size_t(3) * sizeof(uint32_t) * d.max_stack * kTraceBlock;
+    const size_t lds = trace_lds_bytes(d.max_stack);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, kTraceBlock, lds) != hipSuccess ||
         per_cu <= 0)
@@ -1441,7 +1449,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   hipLaunchKernelGGL(k_api_prep, dim3(g), dim3(256), 0, c->stream, dr, n, occ ? 1 : 0, o3, d3, tmn, tmx);
   c->timing = false;
   Timer tm(c);
-  trace_launch(c, tm, false, o3, d3, n, cnt, tt, pr, n, tmn, tmx);
+  trace_launch(c, tm, false, rq(o3, d3, n, cnt, tt, pr, tmn, tmx), kNoQueue, n);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
   HIPCHK(hipGetLastError());
@@ -1524,6 +1532,9 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
   int* ext_cnt = &c->ctr->ext_count[0];
   int* sq_cnt = &c->ctr->sq_count;
   const int g = shade_grid(c, P);
+  const RayQueue sq = rq(B.s_o, B.s_d, B.cap_sq, sq_cnt, B.s_t, B.s_prim);
+  auto ext = [&](int q) { return rq(B.q_o[q], B.q_d[q], P, ext_cnt + q, B.q_t[q], B.q_prim[q]); };
+  const int sq_max = B.cap_sq;
   for (int it = 0; it < prm->iterations; ++it) {
     A.iter = static_cast<uint32_t>(prm->iter_begin + it);
     // ---------------- light pass (:67-131)
@@ -1532,29 +1543,29 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
     tm.mark(WR_K_GEN);
     int cur = 0;
     for (int b = 0; b < A.maxlen - 1; ++b) {
-      trace_launch(c, tm, count, B.q_o[cur], B.q_d[cur], P, ext_cnt + cur, B.q_t[cur], B.q_prim[cur], P);
+      trace_launch(c, tm, count, ext(cur), kNoQueue, P);
       HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), c->stream));
       hipLaunchKernelGGL(k_light_shade, dim3(g), dim3(kShadeBlock), 0, c->stream, A, cur);
       tm.mark(WR_K_SHADE);
       cur ^= 1;
     }
-    trace_launch(c, tm, count, B.s_o, B.s_d, B.cap_sq, sq_cnt, B.s_t, B.s_prim, P);
-    hipLaunchKernelGGL(k_sq_resolve, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
-    tm.mark(WR_K_RESOLVE);
-    // ---------------- camera pass (:133-264)
+    // ---------------- camera pass (:133-264).  The light pass's splat rays
+    // (connectToCamera) ride along with the primary rays; afterwards each
+    // bounce's shadow / aux rays ride along with the next bounce's extension rays.
     hipLaunchKernelGGL(k_camera_gen, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
     tm.mark(WR_K_GEN);
     cur = 0;
-    for (int b = 0; b < A.maxlen; ++b) {
-      trace_launch(c, tm, count, B.q_o[cur], B.q_d[cur], P, ext_cnt + cur, B.q_t[cur], B.q_prim[cur], P);
+    for (int b = 0; b <= A.maxlen; ++b) {
+      const bool more = b < A.maxlen;  // extension rays of bounce b exist
+      trace_launch(c, tm, count, sq, more ? ext(cur) : kNoQueue, (more ? P : 0) + sq_max);
+      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max)), dim3(kShadeBlock), 0, c->stream, A);
+      if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+      tm.mark(WR_K_RESOLVE);
+      if (!more) break;
       HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), c->stream));  // next extension queue
       HIPCHK(hipMemsetAsync(sq_cnt, 0, 2 * sizeof(int), c->stream));           // sq_count, di_count
       hipLaunchKernelGGL(k_camera_shade, dim3(g), dim3(kShadeBlock), 0, c->stream, A, cur);
       tm.mark(WR_K_SHADE);
-      trace_launch(c, tm, count, B.s_o, B.s_d, B.cap_sq, sq_cnt, B.s_t, B.s_prim, B.cap_sq);
-      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, B.cap_sq)), dim3(kShadeBlock), 0, c->stream, A);
-      hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
-      tm.mark(WR_K_RESOLVE);
       cur ^= 1;
     }
   }
@@ -1602,15 +1613,20 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
     hipLaunchKernelGGL(k_pt_gen, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
     tm.mark(WR_K_GEN);
     int cur = 0;
-    for (int b = 0; b <= A.max_depth; ++b) {
-      trace_launch(c, tm, count, T.q_o[cur], T.q_d[cur], P, ext_cnt + cur, T.q_t[cur], T.q_prim[cur], P);
+    HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), c->stream));
+    for (int b = 0; b <= A.max_depth + 1; ++b) {
+      // NEE shadow rays of the previous vertex ride along with this bounce's rays
+      const bool more = b <= A.max_depth;
+      trace_launch(c, tm, count, rq(T.s_o, T.s_d, P, sq_cnt, T.s_t, T.s_prim),
+                   more ? rq(T.q_o[cur], T.q_d[cur], P, ext_cnt + cur, T.q_t[cur], T.q_prim[cur]) : kNoQueue,
+                   2 * P);
+      hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+      tm.mark(WR_K_RESOLVE);
+      if (!more) break;
       HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), c->stream));
       HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), c->stream));
       hipLaunchKernelGGL(k_pt_shade, dim3(g), dim3(kShadeBlock), 0, c->stream, A, cur);
       tm.mark(WR_K_SHADE);
-      trace_launch(c, tm, count, T.s_o, T.s_d, P, sq_cnt, T.s_t, T.s_prim, P);
-      hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
-      tm.mark(WR_K_RESOLVE);
       cur ^= 1;
     }
   }

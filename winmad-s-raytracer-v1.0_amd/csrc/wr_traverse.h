@@ -151,72 +151,114 @@ __device__ __forceinline__ bool sph_hit(const DevScene& S, int prim, V3 o, V3 d,
   return true;
 }
 
-// Persistent closest-hit traversal over a ray queue (one wave per workgroup).
+// A ray queue: SoA origins / directions [3][cap], count on device, optional
+// per-ray [tmin, tmax], and the (t, prim) outputs.
+struct RayQueue {
+  const float* o3;
+  const float* d3;
+  int cap;
+  const int* count;
+  const float* tmin;
+  const float* tmax;
+  float* out_t;
+  int* out_prim;
+};
+
+// Per-wave LDS scratch of the traversal (one wave per workgroup, 64 lanes):
+//   stack  [depth][64] x (node, tmin, tmax)
+//   rays   origin, direction, [tmin, tmax], current best t of every lane
+//   leaf   exclusive prefix of leaf sizes and first ref of every lane
+//   res    kPairBatch pair results (t, or NaN for "no hit")
+constexpr int kPairBatch = 256;
+__host__ __device__ constexpr size_t trace_lds_bytes(int depth) {
+  return size_t(4) * (3 * size_t(depth) * 64 + 9 * 64 + 2 * 64 + kPairBatch);
+}
+
+// Persistent closest-hit traversal over up to two ray queues (one wave per
+// workgroup); queue `qa` is fetched first (the long shadow rays start early and
+// overlap the extension rays of `qb` instead of forming a tail of their own).
 //
 // KDtreeAccel::traverse semantics per ray; the SIMT structure is GPU-specific:
 //   * while-while: every live lane first descends inner nodes until it stands on
-//     a leaf, then all lanes test their leaves together, then pop -- so the
-//     expensive leaf loop runs with the wave full instead of interleaved with
-//     inner-node steps of other lanes;
+//     a leaf, then the wave tests all its leaves, then every lane pops;
+//   * leaf pairs spread over the wave: the (ray, triangle) pairs of the 64 leaves
+//     are numbered by a prefix sum and tested 64 at a time, so the expensive
+//     triangle test runs at full SIMD width however unequal the leaves are; each
+//     lane then walks ITS results in leaf order applying the reference's
+//     order-dependent rule `cmp(t - best) < 0` (first found wins);
 //   * lanes that finish their ray take the next one from a global counter (one
-//     atomic per wave per refill), so a wave stays full until the queue drains;
-//   * leaf references are prefetched one ahead (the 40-byte record of the next
-//     triangle is in flight while the current one is tested).
-// `rtmin3 / rtmax3` (optional) give per-ray [tmin, tmax]; default [0, INF].
+//     atomic per wave per refill), so a wave stays full until the queues drain.
 template <bool COUNT, bool SPH>
-__device__ __forceinline__ void trace_queue(const DevScene& S, const float* __restrict__ o3,
-                                            const float* __restrict__ d3, int cap, int n,
-                                            const float* __restrict__ rtmin_a, const float* __restrict__ rtmax_a,
-                                            float* __restrict__ out_t, int* __restrict__ out_prim, int* fetch,
-                                            uint32_t* stk_node, float* stk_tmin, float* stk_tmax, int stride,
-                                            TraceCounters& ctr) {
+__device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& qa, const RayQueue& qb, int* fetch,
+                                            uint32_t* lds, TraceCounters& ctr) {
+  const int lane = __lane_id();
+  const int depth = S.max_stack;
+  uint32_t* stk_node = lds + lane;
+  float* stk_tmin = reinterpret_cast<float*>(lds + depth * 64) + lane;
+  float* stk_tmax = reinterpret_cast<float*>(lds + 2 * depth * 64) + lane;
+  float* ray = reinterpret_cast<float*>(lds + 3 * depth * 64);  // [9][64]
+  int* seg_start = reinterpret_cast<int*>(ray + 9 * 64);
+  uint32_t* seg_first = reinterpret_cast<uint32_t*>(seg_start + 64);
+  float* res = reinterpret_cast<float*>(seg_first + 64);
+  const int na = qa.count ? *qa.count : 0;
+  const int n = na + (qb.count ? *qb.count : 0);
+  bool inb = false;      // the lane's ray comes from qb
   int r = -1;            // ray held by this lane (-1: none)
   bool pool = true;      // wave-uniform: queue not yet exhausted
   V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
-  float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmin = 0.f, rtmax = WR_INF;
+  float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmax = WR_INF;
   int best = -1, sp = 0;
   uint32_t node = 0;
   for (;;) {
     // ---- refill idle lanes
     if (pool) {
       const bool idle = r < 0;
-      if (__ballot(idle)) {
-        const unsigned long long m = __ballot(idle);
-        const int lane = __lane_id();
+      const unsigned long long m = __ballot(idle);
+      if (m) {
         const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
         int base = 0;
         if (lane == leader) base = atomicAdd(fetch, __popcll(m));
         base = __shfl(base, leader);
         const int idx = base + __popcll(m & ((1ull << lane) - 1ull));
-        if (idle) {
-          if (idx < n) {
-            r = idx;
-            o = v3(o3[idx], o3[cap + idx], o3[2 * cap + idx]);
-            d = v3(d3[idx], d3[cap + idx], d3[2 * cap + idx]);
-            rtmin = rtmin_a ? rtmin_a[idx] : 0.f;
-            rtmax = rtmax_a ? rtmax_a[idx] : WR_INF;
-            t_best = WR_INF;
-            best = -1;
-            sp = 0;
-            node = 0;
-            if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) {
-              out_t[idx] = WR_INF;
-              out_prim[idx] = -1;
-              r = -1;
-            } else {
-              inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-            }
+        if (idle && idx < n) {
+          inb = idx >= na;
+          const RayQueue& q = inb ? qb : qa;
+          r = inb ? idx - na : idx;
+          o = v3(q.o3[r], q.o3[q.cap + r], q.o3[2 * q.cap + r]);
+          d = v3(q.d3[r], q.d3[q.cap + r], q.d3[2 * q.cap + r]);
+          const float rtmin = q.tmin ? q.tmin[r] : 0.f;
+          rtmax = q.tmax ? q.tmax[r] : WR_INF;
+          t_best = WR_INF;
+          best = -1;
+          sp = 0;
+          node = 0;
+          if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) {
+            q.out_t[r] = WR_INF;
+            q.out_prim[r] = -1;
+            r = -1;
+          } else {
+            inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+            ray[0 * 64 + lane] = o.x;
+            ray[1 * 64 + lane] = o.y;
+            ray[2 * 64 + lane] = o.z;
+            ray[3 * 64 + lane] = d.x;
+            ray[4 * 64 + lane] = d.y;
+            ray[5 * 64 + lane] = d.z;
+            ray[6 * 64 + lane] = rtmin;
+            ray[7 * 64 + lane] = rtmax;
           }
         }
         if (__ballot(idle && idx >= n)) pool = false;
       }
     }
-    if (!__ballot(r >= 0)) {
+    const bool act = r >= 0;
+    if (!__ballot(act)) {
       if (!pool) break;
       continue;
     }
-    if (r >= 0) {
-      // ---- descend to a leaf (KDtreeAccel.cpp:325-358)
+    // ---- descend to a leaf (KDtreeAccel.cpp:325-358)
+    uint32_t first = 0, count = 0;
+    if (act) {
       uint2 nd = S.nodes[node];
       while ((nd.y & 3u) != 3u) {
         if (COUNT) ++ctr.inner;
@@ -234,60 +276,92 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const float* __re
         } else if (t < tmin) {
           node = farc;
         } else {
-          stk_node[sp * stride] = farc;
-          stk_tmin[sp * stride] = t;
-          stk_tmax[sp * stride] = tmax;
+          stk_node[sp * 64] = farc;
+          stk_tmin[sp * 64] = t;
+          stk_tmax[sp * 64] = tmax;
           ++sp;
           node = nearc;
           tmax = t;
         }
         nd = S.nodes[node];
       }
-      // ---- leaf: every primitive in objlist order, first-found wins (:359-373)
-      const uint32_t first = nd.x, count = nd.y >> 2;
+      first = nd.x;
+      count = nd.y >> 2;
       if (COUNT) {
         ++ctr.leaves;
         ctr.refs += count;
       }
-      if (count) {
-        const uint32_t end = first + count;
-        float4 a = S.ref_a[first], b = S.ref_b[first];
-        float2 c = S.ref_c[first];
-        for (uint32_t i = first; i < end;) {
-          const float4 ca = a, cb = b;
-          const float2 cc = c;
-          ++i;
-          const uint32_t j = i < end ? i : end - 1;
-          a = S.ref_a[j];
-          b = S.ref_b[j];
-          c = S.ref_c[j];
-          const int prim = __float_as_int(cc.y);
-          float t;
-          bool h;
-          if (!SPH || prim >= 0) {
-            h = tri_test(ca, cb, cc.x, o, d, rtmin, rtmax, t_best, t);
-          } else {
-            h = sph_hit(S, -prim - 1, o, d, rtmin, rtmax, t);
-          }
-          if (h && cmpf(t - t_best) < 0) {
+    }
+    // ---- leaf phase (:359-373): number the wave's (ray, ref) pairs
+    int incl = static_cast<int>(count);
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off);
+      if (lane >= off) incl += v;
+    }
+    const int excl = incl - static_cast<int>(count);
+    const int total = __shfl(incl, 63);
+    seg_start[lane] = excl;
+    seg_first[lane] = first;
+    ray[8 * 64 + lane] = t_best;
+    int best_ref = -1;
+    for (int base = 0; base < total; base += kPairBatch) {
+      const int lim = min(total - base, kPairBatch);
+      __syncthreads();
+      for (int j = lane; j < lim; j += 64) {
+        const int g = base + j;
+        int L = 0;  // largest lane whose segment starts at or before g (owns pair g)
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+          const int cand = L + step;
+          if (cand <= 63 && seg_start[cand] <= g) L = cand;
+        }
+        const uint32_t ref = seg_first[L] + static_cast<uint32_t>(g - seg_start[L]);
+        const V3 ro = v3(ray[0 * 64 + L], ray[1 * 64 + L], ray[2 * 64 + L]);
+        const V3 rd = v3(ray[3 * 64 + L], ray[4 * 64 + L], ray[5 * 64 + L]);
+        const float rmin = ray[6 * 64 + L], rmax = ray[7 * 64 + L], rbest = ray[8 * 64 + L];
+        const float2 c = S.ref_c[ref];
+        const int prim = __float_as_int(c.y);
+        float t = __int_as_float(0x7fc00000);  // NaN: no hit
+        float th;
+        bool h;
+        if (!SPH || prim >= 0) {
+          h = tri_test(S.ref_a[ref], S.ref_b[ref], c.x, ro, rd, rmin, rmax, rbest, th);
+        } else {
+          h = sph_hit(S, -prim - 1, ro, rd, rmin, rmax, th);
+        }
+        if (h) t = th;
+        res[j] = t;
+      }
+      __syncthreads();
+      if (act) {  // this lane's pairs of the batch, in leaf order
+        const int k0 = max(excl, base), k1 = min(excl + static_cast<int>(count), base + lim);
+        for (int k = k0; k < k1; ++k) {
+          const float t = res[k - base];
+          if (t == t && cmpf(t - t_best) < 0) {
             t_best = t;
-            best = (!SPH || prim >= 0) ? prim : -prim - 1;
+            best_ref = static_cast<int>(first) + (k - excl);
           }
         }
+      }
+    }
+    if (act) {
+      if (best_ref >= 0) {
+        const int prim = __float_as_int(S.ref_c[best_ref].y);
+        best = (!SPH || prim >= 0) ? prim : -prim - 1;
       }
       // ---- pop (:375-383); tmin only changes here, so the `ray.tmax < tmin`
       // check of :323 is evaluated after every pop
       bool done = true;
       if (sp > 0) {
         --sp;
-        node = stk_node[sp * stride];
-        tmin = stk_tmin[sp * stride];
-        tmax = stk_tmax[sp * stride];
+        node = stk_node[sp * 64];
+        tmin = stk_tmin[sp * 64];
+        tmax = stk_tmax[sp * 64];
         done = rtmax < tmin;
       }
       if (done) {
-        out_t[r] = t_best;
-        out_prim[r] = best;
+        (inb ? qb : qa).out_t[r] = t_best;
+        (inb ? qb : qa).out_prim[r] = best;
         r = -1;
       }
     }
