@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -55,6 +56,7 @@ struct DevCounters {
   int sq_count;
   int di_count;
   int fetch;  // persistent-traversal queue cursor (reset before every trace launch)
+  unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
   unsigned long long closest, shadow, inner, leaves, refs;
 };
 
@@ -102,11 +104,11 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 
 // =============================================================== trace kernels
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
-template <bool COUNT, bool SPH>
+template <bool COUNT, bool SPH, bool STAMP = false>
 __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, RayQueue qa, RayQueue qb, DevCounters* ctr) {
   extern __shared__ uint32_t smem[];
   TraceCounters tc{0, 0, 0};
-  trace_queue<COUNT, SPH>(S, qa, qb, &ctr->fetch, smem, tc);
+  trace_queue<COUNT, SPH, STAMP>(S, qa, qb, &ctr->fetch, smem, tc, ctr->stamps);
   if (COUNT) {
     unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs);
     if (lane_id() == 0) {
@@ -995,6 +997,7 @@ struct wr_context {
   int grid = 2048;
   int cus = 256;
   bool spheres = false;
+  bool stamps = false;  // WR_TRACE_STAMPS=1: diagnostic traversal with phase stamps
   int trace_blocks = 4096;  // resident one-wave workgroups of the traversal
   std::vector<hipEvent_t> events;
   size_t ev_used = 0;
@@ -1135,7 +1138,10 @@ int trace_launch(wr_context* c, Timer& tm, bool count, const RayQueue& qa, const
   (void)hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream);
 #define WR_TRACE_LAUNCH(CNT, SP) \
   hipLaunchKernelGGL((k_trace<CNT, SP>), dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, qa, qb, c->ctr)
-  if (count) {
+  if (c->stamps) {
+    hipLaunchKernelGGL((k_trace<false, false, true>), dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, qa, qb,
+                       c->ctr);
+  } else if (count) {
     if (c->spheres) WR_TRACE_LAUNCH(true, true);
     else WR_TRACE_LAUNCH(true, false);
   } else {
@@ -1164,6 +1170,14 @@ int finish_stats(wr_context* c, wr_stats* st, double t0_host) {
   st->inner_visits += static_cast<int64_t>(h.inner);
   st->leaf_visits += static_cast<int64_t>(h.leaves);
   st->prim_refs += static_cast<int64_t>(h.refs);
+  if (c->stamps) {
+    static const char* names[6] = {"refill", "descend", "leaf-setup", "pair-tests", "owner-scan", "pop"};
+    double tot = 0;
+    for (int k = 0; k < 6; ++k) tot += static_cast<double>(h.stamps[k]);
+    std::fprintf(stderr, "[wr stamps]");
+    for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %s=%.1f%%", names[k], 100.0 * h.stamps[k] / std::max(1.0, tot));
+    std::fprintf(stderr, " (wave-cycles %.3g)\n", tot);
+  }
   const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   st->seconds += t1 - t0_host;
   if (c->timing) {
@@ -1390,6 +1404,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   std::memcpy(d.cam.r2w, s.cam.r2w, sizeof d.cam.r2w);
   c->scene_bytes = static_cast<int64_t>(A.used);
   for (const auto& p : s.prims) c->spheres |= p.type != wr::kTri;
+  if (const char* e = std::getenv("WR_TRACE_STAMPS")) c->stamps = std::atoi(e) != 0 && !c->spheres;
   {
     // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
     // and registers); more would only queue behind the first wave of blocks

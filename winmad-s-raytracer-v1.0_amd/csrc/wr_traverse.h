@@ -166,12 +166,13 @@ struct RayQueue {
 
 // Per-wave LDS scratch of the traversal (one wave per workgroup, 64 lanes):
 //   stack  [depth][64] x (node, tmin, tmax)
-//   rays   origin, direction, [tmin, tmax], current best t of every lane
+//   rays   per lane 8 floats (o.xyz, d.x | d.yz, tmin, tmax) + best t   (AoS, b128 reads)
 //   leaf   exclusive prefix of leaf sizes and first ref of every lane
+//   own    owner lane of each pair of the batch (bytes)
 //   res    kPairBatch pair results (t, or NaN for "no hit")
 constexpr int kPairBatch = 256;
 __host__ __device__ constexpr size_t trace_lds_bytes(int depth) {
-  return size_t(4) * (3 * size_t(depth) * 64 + 9 * 64 + 2 * 64 + kPairBatch);
+  return size_t(4) * (3 * size_t(depth) * 64 + 8 * 64 + 64 + 2 * 64 + kPairBatch / 4 + kPairBatch + 3 * 64);
 }
 
 // Persistent closest-hit traversal over up to two ray queues (one wave per
@@ -188,18 +189,52 @@ __host__ __device__ constexpr size_t trace_lds_bytes(int depth) {
 //     order-dependent rule `cmp(t - best) < 0` (first found wins);
 //   * lanes that finish their ray take the next one from a global counter (one
 //     atomic per wave per refill), so a wave stays full until the queues drain.
-template <bool COUNT, bool SPH>
+// monotone int key of a float (signed-int order == float order, -0 < +0)
+__device__ __forceinline__ int order_key(float f) {
+  const int b = __float_as_int(f);
+  return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float order_val(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff); }
+
+// Diagnostic build only (STAMP = true, WR_TRACE_STAMPS=1): s_memtime at the
+// phase boundaries, per-wave sums added to stamps[0..5] = refill, descend,
+// leaf setup, pair tests, owner scan, pop.  Never compiled into timed runs.
+__device__ __forceinline__ uint64_t stamp_now() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+template <bool COUNT, bool SPH, bool STAMP = false>
 __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& qa, const RayQueue& qb, int* fetch,
-                                            uint32_t* lds, TraceCounters& ctr) {
+                                            uint32_t* lds, TraceCounters& ctr,
+                                            unsigned long long* stamps = nullptr) {
+  uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t ts = 0;
+  if constexpr (STAMP) ts = stamp_now();
+#define WR_STAMP(k)                       \
+  if constexpr (STAMP) {                  \
+    const uint64_t now_ = stamp_now();    \
+    acc[k] += now_ - ts;                  \
+    ts = now_;                            \
+  }
   const int lane = __lane_id();
   const int depth = S.max_stack;
   uint32_t* stk_node = lds + lane;
   float* stk_tmin = reinterpret_cast<float*>(lds + depth * 64) + lane;
   float* stk_tmax = reinterpret_cast<float*>(lds + 2 * depth * 64) + lane;
-  float* ray = reinterpret_cast<float*>(lds + 3 * depth * 64);  // [9][64]
-  int* seg_start = reinterpret_cast<int*>(ray + 9 * 64);
+  float4* ray4 = reinterpret_cast<float4*>(lds + 3 * depth * 64);  // [64][2] float4
+  float* rbest = reinterpret_cast<float*>(ray4 + 2 * 64);            // [64]
+  int* seg_start = reinterpret_cast<int*>(rbest + 64);
   uint32_t* seg_first = reinterpret_cast<uint32_t*>(seg_start + 64);
-  float* res = reinterpret_cast<float*>(seg_first + 64);
+  uint8_t* own = reinterpret_cast<uint8_t*>(seg_first + 64);        // [kPairBatch]
+  uint32_t* own32 = reinterpret_cast<uint32_t*>(own);
+  float* res = reinterpret_cast<float*>(own + kPairBatch);           // [kPairBatch]
+  int* omin = reinterpret_cast<int*>(res + kPairBatch);              // [64] per-owner min (order key)
+  int* ocnt = omin + 64;                                             // [64]
+  int* oidx = ocnt + 64;                                             // [64]
   const int na = qa.count ? *qa.count : 0;
   const int n = na + (qb.count ? *qb.count : 0);
   bool inb = false;      // the lane's ray comes from qb
@@ -238,19 +273,14 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
             r = -1;
           } else {
             inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-            ray[0 * 64 + lane] = o.x;
-            ray[1 * 64 + lane] = o.y;
-            ray[2 * 64 + lane] = o.z;
-            ray[3 * 64 + lane] = d.x;
-            ray[4 * 64 + lane] = d.y;
-            ray[5 * 64 + lane] = d.z;
-            ray[6 * 64 + lane] = rtmin;
-            ray[7 * 64 + lane] = rtmax;
+            ray4[2 * lane] = make_float4(o.x, o.y, o.z, d.x);
+            ray4[2 * lane + 1] = make_float4(d.y, d.z, rtmin, rtmax);
           }
         }
         if (__ballot(idle && idx >= n)) pool = false;
       }
     }
+    WR_STAMP(0)
     const bool act = r >= 0;
     if (!__ballot(act)) {
       if (!pool) break;
@@ -292,6 +322,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         ctr.refs += count;
       }
     }
+    WR_STAMP(1)
     // ---- leaf phase (:359-373): number the wave's (ray, ref) pairs
     int incl = static_cast<int>(count);
     for (int off = 1; off < 64; off <<= 1) {
@@ -302,47 +333,111 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
     const int total = __shfl(incl, 63);
     seg_start[lane] = excl;
     seg_first[lane] = first;
-    ray[8 * 64 + lane] = t_best;
+    rbest[lane] = t_best;
     int best_ref = -1;
     for (int base = 0; base < total; base += kPairBatch) {
       const int lim = min(total - base, kPairBatch);
+      const int k0 = max(excl, base), k1 = min(excl + static_cast<int>(count), base + lim);
       __syncthreads();
-      for (int j = lane; j < lim; j += 64) {
-        const int g = base + j;
-        int L = 0;  // largest lane whose segment starts at or before g (owns pair g)
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-          const int cand = L + step;
-          if (cand <= 63 && seg_start[cand] <= g) L = cand;
+      own32[lane] = 0u;
+      omin[lane] = 0x7f800000;  // order key of +inf
+      ocnt[lane] = 0;
+      __syncthreads();
+      // owner table: each segment marks its first slot, then a max-scan over the
+      // batch in slot order (owners increase with the slot)
+      if (k0 < k1) own[k0 - base] = static_cast<uint8_t>(lane);
+      __syncthreads();
+      {
+        const uint32_t w = own32[lane];
+        const uint32_t m0 = w & 0xffu, m1 = max(m0, (w >> 8) & 0xffu), m2 = max(m1, (w >> 16) & 0xffu),
+                       m3 = max(m2, w >> 24);
+        uint32_t run = m3;
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t v = __shfl_up(run, off);
+          if (lane >= off) run = max(run, v);
         }
-        const uint32_t ref = seg_first[L] + static_cast<uint32_t>(g - seg_start[L]);
-        const V3 ro = v3(ray[0 * 64 + L], ray[1 * 64 + L], ray[2 * 64 + L]);
-        const V3 rd = v3(ray[3 * 64 + L], ray[4 * 64 + L], ray[5 * 64 + L]);
-        const float rmin = ray[6 * 64 + L], rmax = ray[7 * 64 + L], rbest = ray[8 * 64 + L];
-        const float2 c = S.ref_c[ref];
-        const int prim = __float_as_int(c.y);
-        float t = __int_as_float(0x7fc00000);  // NaN: no hit
-        float th;
-        bool h;
-        if (!SPH || prim >= 0) {
-          h = tri_test(S.ref_a[ref], S.ref_b[ref], c.x, ro, rd, rmin, rmax, rbest, th);
-        } else {
-          h = sph_hit(S, -prim - 1, ro, rd, rmin, rmax, th);
-        }
-        if (h) t = th;
-        res[j] = t;
+        uint32_t prev = __shfl_up(run, 1);
+        if (lane == 0) prev = 0u;
+        own32[lane] = max(m0, prev) | (max(m1, prev) << 8) | (max(m2, prev) << 16) | (max(m3, prev) << 24);
       }
       __syncthreads();
-      if (act) {  // this lane's pairs of the batch, in leaf order
-        const int k0 = max(excl, base), k1 = min(excl + static_cast<int>(count), base + lim);
-        for (int k = k0; k < k1; ++k) {
-          const float t = res[k - base];
-          if (t == t && cmpf(t - t_best) < 0) {
-            t_best = t;
-            best_ref = static_cast<int>(first) + (k - excl);
+      WR_STAMP(2)
+      // two pairs in flight per lane: pair j and j + 64 of the batch
+      for (int j = lane; j < lim; j += 128) {
+        const int j2 = j + 64;
+        const bool two = j2 < lim;
+        const int L1 = own[j], L2 = own[two ? j2 : j];
+        const uint32_t ref1 = seg_first[L1] + static_cast<uint32_t>(base + j - seg_start[L1]);
+        const uint32_t ref2 = seg_first[L2] + static_cast<uint32_t>(base + (two ? j2 : j) - seg_start[L2]);
+        const float2 c1 = S.ref_c[ref1], c2 = S.ref_c[ref2];
+        const float4 a1 = S.ref_a[ref1], a2 = S.ref_a[ref2];
+        const float4 b1 = S.ref_b[ref1], b2 = S.ref_b[ref2];
+        const float4 x1 = ray4[2 * L1], y1 = ray4[2 * L1 + 1], x2 = ray4[2 * L2], y2 = ray4[2 * L2 + 1];
+        const float rb1 = rbest[L1], rb2 = rbest[L2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (u == 1 && !two) break;
+          const float4 x = u ? x2 : x1, y = u ? y2 : y1;
+          const float2 c = u ? c2 : c1;
+          const V3 ro = v3(x.x, x.y, x.z), rd = v3(x.w, y.x, y.y);
+          const int prim = __float_as_int(c.y);
+          float t = __int_as_float(0x7fc00000);  // NaN: no hit
+          float th;
+          bool h;
+          if (!SPH || prim >= 0) {
+            h = tri_test(u ? a2 : a1, u ? b2 : b1, c.x, ro, rd, y.z, y.w, u ? rb2 : rb1, th);
+          } else {
+            h = sph_hit(S, -prim - 1, ro, rd, y.z, y.w, th);
+          }
+          if (h) {
+            t = th;
+            atomicMin(omin + (u ? L2 : L1), order_key(t));
+          }
+          res[u ? j2 : j] = t;
+        }
+      }
+      __syncthreads();
+      // hits within 2 EPS of their owner's minimum (the minimum itself included)
+      for (int j = lane; j < lim; j += 64) {
+        const float t = res[j];
+        if (t == t) {
+          const int L = own[j];
+          const int key = omin[L];
+          if (t - order_val(key) <= 2.f * WR_EPS) {
+            atomicAdd(ocnt + L, 1);
+            if (order_key(t) == key) oidx[L] = j;
           }
         }
       }
+      __syncthreads();
+      WR_STAMP(3)
+      // first-found-wins (cmp(t - best) < 0, in leaf order).  The sequential rule
+      // keeps best within EPS of the minimum m once m is seen, so when m is the
+      // only hit within 2 EPS of itself and the incoming best is 2 EPS away from
+      // m either way, the outcome is decided by m alone; otherwise this owner
+      // replays its pairs in order.
+      if (act && k0 < k1 && ocnt[lane] > 0) {
+        const float m = order_val(omin[lane]);
+        bool decided = ocnt[lane] == 1;
+        if (decided) {
+          if (t_best - m > 2.f * WR_EPS) {
+            t_best = m;
+            best_ref = static_cast<int>(first) + (base + oidx[lane] - excl);
+          } else if (!(m - t_best > 2.f * WR_EPS)) {
+            decided = false;
+          }
+        }
+        if (!decided) {
+          for (int k = k0; k < k1; ++k) {
+            const float t = res[k - base];
+            if (t == t && cmpf(t - t_best) < 0) {
+              t_best = t;
+              best_ref = static_cast<int>(first) + (k - excl);
+            }
+          }
+        }
+      }
+      WR_STAMP(4)
     }
     if (act) {
       if (best_ref >= 0) {
@@ -365,6 +460,12 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         r = -1;
       }
     }
+    WR_STAMP(5)
+  }
+#undef WR_STAMP
+  if constexpr (STAMP) {
+    if (lane == 0)
+      for (int k = 0; k < 6; ++k) atomicAdd(stamps + k, static_cast<unsigned long long>(acc[k]));
   }
 }
 
