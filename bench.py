@@ -26,6 +26,19 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "winmad-s-raytracer-v1.0_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# HBM bytes per k_trace launch from the PMC passes of the same bench command
+# (scripts/profile_round.sh + scripts/summarize_profile.py; counters cannot be
+# read from inside the timed run)
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r1", "traffic.json")
+
+
+def pmc_traffic():
+    try:
+        with open(TRAFFIC_JSON) as f:
+            t = json.load(f)
+        return t.get("hbm_bytes_per_launch"), os.path.relpath(TRAFFIC_JSON, REPO)
+    except (OSError, ValueError):
+        return None, None
 
 
 def algorithmic_bytes(rays, inner, leaves, refs):
@@ -82,6 +95,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from winmad_rt import native, scenes
+    from winmad_rt import dist as wdist
 
     W, H, K = args.width, args.height, args.steps
     tmp = tempfile.mkdtemp(prefix=f"wr_bench_{rank}_")
@@ -100,10 +114,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    _, st = ctx.render_bdpt(W, H, iterations=K, seed=5489, iter_begin=rank * K, film_ptr=film.data_ptr(),
+    it0 = wdist.bdpt_iteration_begin(rank, K)
+    _, st = ctx.render_bdpt(W, H, iterations=K, seed=5489, iter_begin=it0, film_ptr=film.data_ptr(),
                             time_kernels=1)
-    if dist:
-        dist.reduce(film, dst=0, op=dist.ReduceOp.SUM)  # one film reduction per batch (RCCL)
+    wdist.reduce_film(film, dist)  # one film reduction per batch (RCCL)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -113,29 +127,23 @@ def main():
     rays = st.closest_rays + st.shadow_rays
     trace_ms = st.kernel_ms[native.K_TRACE]
     trace_launches = st.kernel_launches[native.K_TRACE]
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=film.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        r = torch.tensor([rays], dtype=torch.float64, device=film.device)
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        total_rays = float(r.item())
-    else:
-        total_rays = float(rays)
+    elapsed, total_rays = wdist.job_totals(elapsed, rays, dist, film.device)
 
     roofline = None
     if not args.no_count and rank == 0:
         # replay the same iterations with per-traversal counters (identical ray set:
         # the counter RNG makes the work a pure function of (seed, iteration, path))
-        _, cst = ctx.render_bdpt(W, H, iterations=K, seed=5489, iter_begin=rank * K, count_work=1,
+        _, cst = ctx.render_bdpt(W, H, iterations=K, seed=5489, iter_begin=it0, count_work=1,
                                  film=None)
         assert cst.closest_rays == st.closest_rays and cst.shadow_rays == st.shadow_rays
         total_bytes = algorithmic_bytes(rays, cst.inner_visits, cst.leaf_visits, cst.prim_refs)
         per_launch = total_bytes / max(1, trace_launches)
         avg_launch_s = trace_ms / 1e3 / max(1, trace_launches)
         achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        traffic, traffic_src = pmc_traffic()
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                     "kernel": "k_trace (KD closest-hit traversal)",
                     "bytes_per_launch": round(per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                     "launches": int(trace_launches),

@@ -1,0 +1,86 @@
+"""N > 1 path on the CPU: two gloo ranks run the multi-GPU layout of
+bench.py (winmad_rt.dist) with the oracle standing in for the GPU renderer.
+
+Checks that iteration sharding + one reduce(sum) reproduces the single-process
+render of all iterations, and that the job totals are max(time) / sum(rays).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+import _oracle  # noqa: E402
+import _scenes  # noqa: E402
+from winmad_rt import dist as wdist  # noqa: E402
+
+W, H, K = 32, 24, 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, scene, out_dir):
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(os.path.dirname(here), "winmad-s-raytracer-v1.0_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        it0 = wdist.bdpt_iteration_begin(rank, K)
+        film, st = _oracle.Scene(scene).bdpt(W, H, K, 5489, mode=1, iter_begin=it0)
+        t = torch.from_numpy(film)
+        wdist.reduce_film(t, dist)
+        elapsed, rays = wdist.job_totals(0.5 + rank, st.closest_rays + st.shadow_rays, dist)
+        if rank == 0:
+            np.save(os.path.join(out_dir, "film.npy"), t.numpy())
+            np.save(os.path.join(out_dir, "totals.npy"), np.array([elapsed, rays]))
+        np.save(os.path.join(out_dir, f"rays{rank}.npy"), np.array([st.closest_rays + st.shadow_rays]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bdpt_iteration_sharding_over_two_gloo_ranks(tmp_path):
+    scene = _scenes.torus(W, H)
+    mp.spawn(_rank_main, args=(2, _free_port(), scene, str(tmp_path)), nprocs=2, join=True)
+    film = np.load(tmp_path / "film.npy")
+    ref, rst = _oracle.Scene(scene).bdpt(W, H, 2 * K, 5489, mode=1)
+    assert np.allclose(film, ref, rtol=1e-5, atol=1e-7)
+    elapsed, rays = np.load(tmp_path / "totals.npy")
+    assert elapsed == 1.5  # max over ranks
+    assert rays == np.load(tmp_path / "rays0.npy")[0] + np.load(tmp_path / "rays1.npy")[0]
+    assert rays == rst.closest_rays + rst.shadow_rays
+
+
+def test_single_process_is_identity():
+    t = torch.ones(3)
+    assert wdist.reduce_film(t, None) is t
+    assert wdist.job_totals(2.0, 7, None) == (2.0, 7.0)
+
+
+@pytest.mark.parametrize("world,spp", [(1, 16), (2, 16), (3, 16), (8, 5), (4, 0)])
+def test_pt_sample_ranges_partition_the_samples(world, spp):
+    ranges = [wdist.pt_sample_range(r, world, spp) for r in range(world)]
+    nxt = 0
+    for b, c in ranges:
+        assert b == nxt and c >= 0
+        nxt = b + c
+    assert nxt == spp
+    assert max(c for _, c in ranges) - min(c for _, c in ranges) <= 1
+
+
+def test_bad_arguments_raise():
+    with pytest.raises(ValueError):
+        wdist.pt_sample_range(2, 2, 4)
+    with pytest.raises(ValueError):
+        wdist.bdpt_iteration_begin(-1, 4)
