@@ -104,11 +104,11 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 
 // =============================================================== trace kernels
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
-template <bool COUNT, bool SPH, bool STAMP = false>
+template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
 __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, RayQueue qa, RayQueue qb, DevCounters* ctr) {
   extern __shared__ uint32_t smem[];
   TraceCounters tc{0, 0, 0};
-  trace_queue<COUNT, SPH, STAMP>(S, qa, qb, &ctr->fetch, smem, tc, ctr->stamps);
+  trace_queue<COUNT, SPH, NARROW, STAMP>(S, qa, qb, &ctr->fetch, smem, tc, ctr->stamps);
   if (COUNT) {
     unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs);
     if (lane_id() == 0) {
@@ -997,6 +997,7 @@ struct wr_context {
   int grid = 2048;
   int cus = 256;
   bool spheres = false;
+  bool narrow = false;  // tree of <= 65536 nodes: 16-bit stack entries
   bool stamps = false;  // WR_TRACE_STAMPS=1: diagnostic traversal with phase stamps
   int trace_blocks = 4096;  // resident one-wave workgroups of the traversal
   std::vector<hipEvent_t> events;
@@ -1131,24 +1132,24 @@ RayQueue rq(const float* o3, const float* d3, int cap, const int* cnt, float* t,
 }
 const RayQueue kNoQueue{nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
 
+using TraceKernel = void (*)(DevScene, RayQueue, RayQueue, DevCounters*);
+TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps) {
+  if (stamps) return narrow ? k_trace<false, false, true, true> : k_trace<false, false, false, true>;
+  if (count) {
+    if (spheres) return narrow ? k_trace<true, true, true> : k_trace<true, true, false>;
+    return narrow ? k_trace<true, false, true> : k_trace<true, false, false>;
+  }
+  if (spheres) return narrow ? k_trace<false, true, true> : k_trace<false, true, false>;
+  return narrow ? k_trace<false, false, true> : k_trace<false, false, false>;
+}
+
 // One persistent traversal launch over qa then qb (max_rays bounds the grid).
 int trace_launch(wr_context* c, Timer& tm, bool count, const RayQueue& qa, const RayQueue& qb, int max_rays) {
-  const size_t lds = trace_lds_bytes(c->ds.max_stack);
+  const size_t lds = trace_lds_bytes(c->ds.max_stack, c->narrow);
   const int grid = std::max(1, std::min(c->trace_blocks, (max_rays + kTraceBlock - 1) / kTraceBlock));
   (void)hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream);
-#define WR_TRACE_LAUNCH(CNT, SP) \
-  hipLaunchKernelGGL((k_trace<CNT, SP>), dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, qa, qb, c->ctr)
-  if (c->stamps) {
-    hipLaunchKernelGGL((k_trace<false, false, true>), dim3(grid), dim3(kTraceBlock), lds, c->stream, c->ds, qa, qb,
-                       c->ctr);
-  } else if (count) {
-    if (c->spheres) WR_TRACE_LAUNCH(true, true);
-    else WR_TRACE_LAUNCH(true, false);
-  } else {
-    if (c->spheres) WR_TRACE_LAUNCH(false, true);
-    else WR_TRACE_LAUNCH(false, false);
-  }
-#undef WR_TRACE_LAUNCH
+  hipLaunchKernelGGL(trace_kernel(count, c->spheres, c->narrow, c->stamps), dim3(grid), dim3(kTraceBlock), lds,
+                     c->stream, c->ds, qa, qb, c->ctr);
   tm.mark(WR_K_TRACE);
   return WR_OK;
 }
@@ -1239,7 +1240,7 @@ int wr_scene_info_get(const wr_scene* sc, wr_scene_info* o) {
   o->missing_files = s.missing_files;
   o->camera_xres = s.cam.xres;
   o->camera_yres = s.cam.yres;
-  o->device_bytes = static_cast<int64_t>(s.nodes.size() * 8 + s.refs.size() * 40 + s.prims.size() * 64);
+  o->device_bytes = static_cast<int64_t>(s.nodes.size() * 24 + s.refs.size() * 40 + s.prims.size() * 64);
   return WR_OK;
 }
 
@@ -1293,6 +1294,17 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       nodes[i] = make_uint2(static_cast<uint32_t>(k.first), (static_cast<uint32_t>(k.count) << 2) | 3u);
     }
   }
+  std::vector<uint4> nrec(nn);
+  std::vector<uint2> nrec_r(nn, make_uint2(0u, 0u));
+  for (size_t i = 0; i < nn; ++i) {
+    const uint2 self = nodes[i];
+    uint2 l = make_uint2(0u, 0u);
+    if (s.nodes[i].axis >= 0) {
+      l = nodes[i + 1];
+      nrec_r[i] = nodes[static_cast<size_t>(s.nodes[i].right)];
+    }
+    nrec[i] = make_uint4(self.x, self.y, l.x, l.y);
+  }
   std::vector<float4> ra(nr), rb(nr);
   std::vector<float2> rcv(nr);
   for (size_t i = 0; i < nr; ++i) {
@@ -1340,7 +1352,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                    v3(m.specular.x, m.specular.y, m.specular.z), m.phong_exp, m.index};
   }
   auto total = measure([&](Arena& a) {
-    a.take<uint2>(nn); a.take<float4>(nr); a.take<float4>(nr); a.take<float2>(nr);
+    a.take<uint4>(nn); a.take<uint2>(nn); a.take<float4>(nr); a.take<float4>(nr); a.take<float2>(nr);
     a.take<int>(np); a.take<int>(np); a.take<float4>(np); a.take<float2>(np); a.take<float4>(np);
     a.take<float4>(np); a.take<float2>(np); a.take<DLight>(lights.size() + 1); a.take<DMat>(mats.size());
     a.take<DevCounters>(1);
@@ -1354,7 +1366,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     return hipMemcpy(dst, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice);
   };
   DevScene& d = c->ds;
-  uint2* dn = A.take<uint2>(nn);
+  uint4* dn = A.take<uint4>(nn);
+  uint2* dnr = A.take<uint2>(nn);
   float4* dra = A.take<float4>(nr);
   float4* drb = A.take<float4>(nr);
   float2* drc = A.take<float2>(nr);
@@ -1369,7 +1382,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   DMat* dm = A.take<DMat>(mats.size());
   c->ctr = A.take<DevCounters>(1);
   hipError_t e = hipSuccess;
-  for (hipError_t x : {up(dn, nodes), up(dra, ra), up(drb, rb), up(drc, rcv), up(dpm, pmat), up(dpt, ptype),
+  for (hipError_t x : {up(dn, nrec), up(dnr, nrec_r), up(dra, ra), up(drb, rb), up(drc, rcv), up(dpm, pmat), up(dpt, ptype),
                        up(dptri, ptri), up(dptri2, ptri2), up(dpsph, psph), up(dpsb0, psb0), up(dpsb1, psb1),
                        up(dm, mats)})
     if (x != hipSuccess) e = x;
@@ -1378,7 +1391,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     wr_destroy(c);
     return fail(WR_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));
   }
-  d.nodes = dn;
+  d.nrec = dn;
+  d.nrec_r = dnr;
   d.ref_a = dra;
   d.ref_b = drb;
   d.ref_c = drc;
@@ -1408,9 +1422,11 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   {
     // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
     // and registers); more would only queue behind the first wave of blocks
-    const size_t lds = trace_lds_bytes(d.max_stack);
+    c->narrow = nn <= 65536;
+    const size_t lds = trace_lds_bytes(d.max_stack, c->narrow);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, kTraceBlock, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel(false, c->spheres, c->narrow, false),
+                                                     kTraceBlock, lds) != hipSuccess ||
         per_cu <= 0)
       per_cu = 8;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;

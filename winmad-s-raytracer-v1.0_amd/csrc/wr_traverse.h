@@ -18,12 +18,17 @@
 // NO early exit (every leaf the ray crosses is visited), closest hit with the
 // EPS tie rule `cmp(t - best) < 0` in leaf order (first-found wins).
 #pragma once
+#include <type_traits>
 #include "wr_devmath.h"
 
 namespace wrd {
 
 struct DevScene {
-  const uint2* nodes;
+  // node i as (self, left child) and (right child): one pair of loads resolves
+  // two levels of the descent.  self/child words: inner (split bits,
+  // right << 2 | axis) with left = i + 1; leaf (first ref, count << 2 | 3)
+  const uint4* nrec;
+  const uint2* nrec_r;
   const float4* ref_a;
   const float4* ref_b;
   const float2* ref_c;
@@ -165,14 +170,16 @@ struct RayQueue {
 };
 
 // Per-wave LDS scratch of the traversal (one wave per workgroup, 64 lanes):
-//   stack  [depth][64] x (node, tmin, tmax)
+//   stack  [depth][64] tmin (float) + [depth][64] node (u16 when the tree has
+//          <= 65536 nodes, NARROW; u32 otherwise)
 //   rays   per lane 8 floats (o.xyz, d.x | d.yz, tmin, tmax) + best t   (AoS, b128 reads)
 //   leaf   exclusive prefix of leaf sizes and first ref of every lane
 //   own    owner lane of each pair of the batch (bytes)
 //   res    kPairBatch pair results (t, or NaN for "no hit")
 constexpr int kPairBatch = 256;
-__host__ __device__ constexpr size_t trace_lds_bytes(int depth) {
-  return size_t(4) * (3 * size_t(depth) * 64 + 8 * 64 + 64 + 2 * 64 + kPairBatch / 4 + kPairBatch + 3 * 64);
+__host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
+  return size_t(depth) * 64 * (narrow ? 6 : 8) +
+         size_t(4) * (8 * 64 + 64 + 2 * 64 + kPairBatch / 4 + kPairBatch + 3 * 64);
 }
 
 // Persistent closest-hit traversal over up to two ray queues (one wave per
@@ -207,7 +214,7 @@ __device__ __forceinline__ uint64_t stamp_now() {
   return t;
 }
 
-template <bool COUNT, bool SPH, bool STAMP = false>
+template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
 __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& qa, const RayQueue& qb, int* fetch,
                                             uint32_t* lds, TraceCounters& ctr,
                                             unsigned long long* stamps = nullptr) {
@@ -222,10 +229,13 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
   }
   const int lane = __lane_id();
   const int depth = S.max_stack;
-  uint32_t* stk_node = lds + lane;
-  float* stk_tmin = reinterpret_cast<float*>(lds + depth * 64) + lane;
-  float* stk_tmax = reinterpret_cast<float*>(lds + 2 * depth * 64) + lane;
-  float4* ray4 = reinterpret_cast<float4*>(lds + 3 * depth * 64);  // [64][2] float4
+  using NodeIdx = typename std::conditional<NARROW, uint16_t, uint32_t>::type;
+  float* stk_tmin = reinterpret_cast<float*>(lds) + lane;
+  NodeIdx* stk_node = reinterpret_cast<NodeIdx*>(lds + depth * 64) + lane;
+  // Stack entries hold (node, tmin) only: tmax changes only at a push
+  // (tmax = t), so entry k's tmax is entry k-1's tmin and entry 0's is the
+  // root-box tmax -- exactly the floats the reference's todo[] would hold.
+  float4* ray4 = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds) + size_t(depth) * 64 * (NARROW ? 6 : 8));
   float* rbest = reinterpret_cast<float*>(ray4 + 2 * 64);            // [64]
   int* seg_start = reinterpret_cast<int*>(rbest + 64);
   uint32_t* seg_first = reinterpret_cast<uint32_t*>(seg_start + 64);
@@ -241,7 +251,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
   int r = -1;            // ray held by this lane (-1: none)
   bool pool = true;      // wave-uniform: queue not yet exhausted
   V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
-  float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmax = WR_INF;
+  float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmax = WR_INF, root_tmax = 0.f;
   int best = -1, sp = 0;
   uint32_t node = 0;
   for (;;) {
@@ -267,7 +277,9 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
           best = -1;
           sp = 0;
           node = 0;
-          if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) {
+          const bool boxed = box_hit(S.root_l, S.root_r, o, d, tmin, tmax);
+          root_tmax = tmax;
+          if (!boxed || rtmax < tmin) {
             q.out_t[r] = WR_INF;
             q.out_prim[r] = -1;
             r = -1;
@@ -289,31 +301,37 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
     // ---- descend to a leaf (KDtreeAccel.cpp:325-358)
     uint32_t first = 0, count = 0;
     if (act) {
-      uint2 nd = S.nodes[node];
-      while ((nd.y & 3u) != 3u) {
+      // one level of KDtreeAccelNode descent from inner node `at` (word w)
+      auto step = [&](uint2 w, uint32_t at) -> uint32_t {
         if (COUNT) ++ctr.inner;
-        const uint32_t axis = nd.y & 3u;
-        const float split = __uint_as_float(nd.x);
+        const uint32_t axis = w.y & 3u;
+        const float split = __uint_as_float(w.x);
         const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
         const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
         const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
         const float t = (split - oa) * ia;
         const bool below = (oa < split) || (oa == split && da <= 0);
-        const uint32_t left = node + 1, right = nd.y >> 2;
+        const uint32_t left = at + 1, right = w.y >> 2;
         const uint32_t nearc = below ? left : right, farc = below ? right : left;
-        if (t > tmax || t <= 0) {
-          node = nearc;
-        } else if (t < tmin) {
-          node = farc;
-        } else {
-          stk_node[sp * 64] = farc;
-          stk_tmin[sp * 64] = t;
-          stk_tmax[sp * 64] = tmax;
-          ++sp;
-          node = nearc;
-          tmax = t;
-        }
-        nd = S.nodes[node];
+        if (t > tmax || t <= 0) return nearc;
+        if (t < tmin) return farc;
+        stk_node[sp * 64] = static_cast<NodeIdx>(farc);
+        stk_tmin[sp * 64] = t;
+        ++sp;
+        tmax = t;
+        return nearc;
+      };
+      uint2 nd;
+      for (;;) {
+        const uint4 q = S.nrec[node];
+        const uint2 qr = S.nrec_r[node];
+        nd = make_uint2(q.x, q.y);
+        if ((nd.y & 3u) == 3u) break;  // popped / refilled onto a leaf
+        const uint32_t at = node;
+        node = step(nd, at);
+        nd = node == at + 1 ? make_uint2(q.z, q.w) : qr;
+        if ((nd.y & 3u) == 3u) break;
+        node = step(nd, node);
       }
       first = nd.x;
       count = nd.y >> 2;
@@ -451,7 +469,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         --sp;
         node = stk_node[sp * 64];
         tmin = stk_tmin[sp * 64];
-        tmax = stk_tmax[sp * 64];
+        tmax = sp > 0 ? stk_tmin[(sp - 1) * 64] : root_tmax;
         done = rtmax < tmin;
       }
       if (done) {
