@@ -173,13 +173,23 @@ struct RayQueue {
 //   stack  [depth][64] tmin (float) + [depth][64] node (u16 when the tree has
 //          <= 65536 nodes, NARROW; u32 otherwise)
 //   rays   per lane 8 floats (o.xyz, d.x | d.yz, tmin, tmax) + best t   (AoS, b128 reads)
-//   leaf   exclusive prefix of leaf sizes and first ref of every lane
+//   leaf   per lane: exclusive prefix of its pair count, and (first, count) of
+//          each of its kLeavesPerRound leaves of the round
 //   own    owner lane of each pair of the batch (bytes)
 //   res    kPairBatch pair results (t, or NaN for "no hit")
+//   omin   per-owner minimum hit (order key); otie = (hits within 2 EPS) << 16 | slot
 constexpr int kPairBatch = 256;
+#ifndef WR_LEAVES_PER_ROUND
+#define WR_LEAVES_PER_ROUND 4
+#endif
+#ifndef WR_LEAVES_WAIT
+#define WR_LEAVES_WAIT 2
+#endif
+constexpr int kLeavesPerRound = WR_LEAVES_PER_ROUND;  // leaves a lane may collect per round
+constexpr int kLeavesWait = WR_LEAVES_WAIT;           // the walk runs until every lane has this many
 __host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
   return size_t(depth) * 64 * (narrow ? 6 : 8) +
-         size_t(4) * (8 * 64 + 64 + 2 * 64 + kPairBatch / 4 + kPairBatch + 3 * 64);
+         size_t(4) * (8 * 64 + 64 + (1 + 2 * kLeavesPerRound) * 64 + kPairBatch / 4 + kPairBatch + 2 * 64);
 }
 
 // Persistent closest-hit traversal over up to two ray queues (one wave per
@@ -187,13 +197,16 @@ __host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
 // overlap the extension rays of `qb` instead of forming a tail of their own).
 //
 // KDtreeAccel::traverse semantics per ray; the SIMT structure is GPU-specific:
-//   * while-while: every live lane first descends inner nodes until it stands on
-//     a leaf, then the wave tests all its leaves, then every lane pops;
-//   * leaf pairs spread over the wave: the (ray, triangle) pairs of the 64 leaves
-//     are numbered by a prefix sum and tested 64 at a time, so the expensive
-//     triangle test runs at full SIMD width however unequal the leaves are; each
-//     lane then walks ITS results in leaf order applying the reference's
-//     order-dependent rule `cmp(t - best) < 0` (first found wins);
+//   * the reference never stops early (it walks to the far end of the root box
+//     whatever it has hit), so a ray's sequence of leaves does not depend on its
+//     hits.  Each round, every lane walks to its next leaf; lanes that get there
+//     first walk on to a second one while the others are still descending
+//     (up to kLeavesPerRound), and the round's leaves are tested together;
+//   * leaf pairs spread over the wave: the (ray, triangle) pairs of the round
+//     are numbered by a prefix sum and tested 64 at a time, so the triangle test
+//     runs at full SIMD width however unequal the leaves are;
+//   * first-found-wins (`cmp(t - best) < 0` in leaf order, :363-372) per ray
+//     over its pairs of the round, concatenated in leaf order;
 //   * lanes that finish their ray take the next one from a global counter (one
 //     atomic per wave per refill), so a wave stays full until the queues drain.
 // monotone int key of a float (signed-int order == float order, -0 < +0)
@@ -204,8 +217,9 @@ __device__ __forceinline__ int order_key(float f) {
 __device__ __forceinline__ float order_val(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff); }
 
 // Diagnostic build only (STAMP = true, WR_TRACE_STAMPS=1): s_memtime at the
-// phase boundaries, per-wave sums added to stamps[0..5] = refill, descend,
-// leaf setup, pair tests, owner scan, pop.  Never compiled into timed runs.
+// phase boundaries, per-wave sums added to stamps[0..5] = refill, leaf walk,
+// leaf setup, pair tests, first-found-wins decision, result write.  Never
+// compiled into timed runs.
 __device__ __forceinline__ uint64_t stamp_now() {
   uint64_t t;
   __builtin_amdgcn_sched_barrier(0);
@@ -236,24 +250,45 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
   // (tmax = t), so entry k's tmax is entry k-1's tmin and entry 0's is the
   // root-box tmax -- exactly the floats the reference's todo[] would hold.
   float4* ray4 = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds) + size_t(depth) * 64 * (NARROW ? 6 : 8));
-  float* rbest = reinterpret_cast<float*>(ray4 + 2 * 64);            // [64]
-  int* seg_start = reinterpret_cast<int*>(rbest + 64);
-  uint32_t* seg_first = reinterpret_cast<uint32_t*>(seg_start + 64);
-  uint8_t* own = reinterpret_cast<uint8_t*>(seg_first + 64);        // [kPairBatch]
+  float* rbest = reinterpret_cast<float*>(ray4 + 2 * 64);  // [64]
+  int* seg_start = reinterpret_cast<int*>(rbest + 64);    // [64]
+  uint32_t* seg_f = reinterpret_cast<uint32_t*>(seg_start + 64);  // [kLeavesPerRound][64]
+  uint32_t* seg_c = seg_f + kLeavesPerRound * 64;                  // [kLeavesPerRound][64]
+  uint8_t* own = reinterpret_cast<uint8_t*>(seg_c + kLeavesPerRound * 64);  // [kPairBatch]
   uint32_t* own32 = reinterpret_cast<uint32_t*>(own);
-  float* res = reinterpret_cast<float*>(own + kPairBatch);           // [kPairBatch]
-  int* omin = reinterpret_cast<int*>(res + kPairBatch);              // [64] per-owner min (order key)
-  int* ocnt = omin + 64;                                             // [64]
-  int* oidx = ocnt + 64;                                             // [64]
+  float* res = reinterpret_cast<float*>(own + kPairBatch);  // [kPairBatch]
+  int* omin = reinterpret_cast<int*>(res + kPairBatch);     // [64]
+  int* otie = omin + 64;                                    // [64]
   const int na = qa.count ? *qa.count : 0;
   const int n = na + (qb.count ? *qb.count : 0);
   bool inb = false;      // the lane's ray comes from qb
   int r = -1;            // ray held by this lane (-1: none)
   bool pool = true;      // wave-uniform: queue not yet exhausted
+  bool more = false;     // the lane's ray has nodes left to visit
   V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
   float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmax = WR_INF, root_tmax = 0.f;
   int best = -1, sp = 0;
   uint32_t node = 0;
+  // one level of KDtreeAccelNode descent (:325-358) from inner node `at` (word w)
+  auto step = [&](uint2 w, uint32_t at) -> uint32_t {
+    if (COUNT) ++ctr.inner;
+    const uint32_t axis = w.y & 3u;
+    const float split = __uint_as_float(w.x);
+    const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+    const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+    const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
+    const float t = (split - oa) * ia;
+    const bool below = (oa < split) || (oa == split && da <= 0);
+    const uint32_t left = at + 1, right = w.y >> 2;
+    const uint32_t nearc = below ? left : right, farc = below ? right : left;
+    if (t > tmax || t <= 0) return nearc;
+    if (t < tmin) return farc;
+    stk_node[sp * 64] = static_cast<NodeIdx>(farc);
+    stk_tmin[sp * 64] = t;
+    ++sp;
+    tmax = t;
+    return nearc;
+  };
   for (;;) {
     // ---- refill idle lanes
     if (pool) {
@@ -279,10 +314,12 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
           node = 0;
           const bool boxed = box_hit(S.root_l, S.root_r, o, d, tmin, tmax);
           root_tmax = tmax;
-          if (!boxed || rtmax < tmin) {
+          more = true;
+          if (!boxed || rtmax < tmin) {  // :312-313, and the :323 check before the root
             q.out_t[r] = WR_INF;
             q.out_prim[r] = -1;
             r = -1;
+            more = false;
           } else {
             inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
             ray4[2 * lane] = make_float4(o.x, o.y, o.z, d.x);
@@ -298,68 +335,83 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       if (!pool) break;
       continue;
     }
-    // ---- descend to a leaf (KDtreeAccel.cpp:325-358)
-    uint32_t first = 0, count = 0;
-    if (act) {
-      // one level of KDtreeAccelNode descent from inner node `at` (word w)
-      auto step = [&](uint2 w, uint32_t at) -> uint32_t {
-        if (COUNT) ++ctr.inner;
-        const uint32_t axis = w.y & 3u;
-        const float split = __uint_as_float(w.x);
-        const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-        const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-        const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
-        const float t = (split - oa) * ia;
-        const bool below = (oa < split) || (oa == split && da <= 0);
-        const uint32_t left = at + 1, right = w.y >> 2;
-        const uint32_t nearc = below ? left : right, farc = below ? right : left;
-        if (t > tmax || t <= 0) return nearc;
-        if (t < tmin) return farc;
-        stk_node[sp * 64] = static_cast<NodeIdx>(farc);
-        stk_tmin[sp * 64] = t;
-        ++sp;
-        tmax = t;
-        return nearc;
-      };
-      uint2 nd;
-      for (;;) {
+    // ---- walk to the next leaves (:321-358, pops :375-383).  One record pair
+    // per iteration resolves up to two levels; the walk goes on while any lane
+    // still has no leaf this round.
+    // the round's leaves of this lane go straight to its LDS column
+#pragma unroll
+    for (int i = 0; i < kLeavesPerRound; ++i) seg_c[i * 64 + lane] = 0u;
+    int nl = 0, count = 0;
+    while (__ballot(more && nl < kLeavesWait)) {
+      if (more && nl < kLeavesPerRound) {
         const uint4 q = S.nrec[node];
         const uint2 qr = S.nrec_r[node];
-        nd = make_uint2(q.x, q.y);
-        if ((nd.y & 3u) == 3u) break;  // popped / refilled onto a leaf
-        const uint32_t at = node;
-        node = step(nd, at);
-        nd = node == at + 1 ? make_uint2(q.z, q.w) : qr;
-        if ((nd.y & 3u) == 3u) break;
-        node = step(nd, node);
-      }
-      first = nd.x;
-      count = nd.y >> 2;
-      if (COUNT) {
-        ++ctr.leaves;
-        ctr.refs += count;
+        uint2 nd = make_uint2(q.x, q.y);
+        bool leaf = (nd.y & 3u) == 3u;
+        if (!leaf) {
+          const uint32_t at = node;
+          node = step(nd, at);
+          nd = node == at + 1 ? make_uint2(q.z, q.w) : qr;
+          leaf = (nd.y & 3u) == 3u;
+          if (!leaf) node = step(nd, node);
+        }
+        if (leaf) {
+          seg_f[nl * 64 + lane] = nd.x;
+          seg_c[nl * 64 + lane] = nd.y >> 2;
+          count += static_cast<int>(nd.y >> 2);
+          ++nl;
+          if (COUNT) {
+            ++ctr.leaves;
+            ctr.refs += nd.y >> 2;
+          }
+          // pop; tmin only changes here, so the `ray.tmax < tmin` check of :323
+          // is evaluated after every pop
+          if (sp > 0) {
+            --sp;
+            node = stk_node[sp * 64];
+            tmin = stk_tmin[sp * 64];
+            tmax = sp > 0 ? stk_tmin[(sp - 1) * 64] : root_tmax;
+            more = !(rtmax < tmin);
+          } else {
+            more = false;
+          }
+        }
       }
     }
     WR_STAMP(1)
     // ---- leaf phase (:359-373): number the wave's (ray, ref) pairs
-    int incl = static_cast<int>(count);
+    int incl = count;
     for (int off = 1; off < 64; off <<= 1) {
       const int v = __shfl_up(incl, off);
       if (lane >= off) incl += v;
     }
-    const int excl = incl - static_cast<int>(count);
+    const int excl = incl - count;
     const int total = __shfl(incl, 63);
     seg_start[lane] = excl;
-    seg_first[lane] = first;
     rbest[lane] = t_best;
+    // ref of lane L's q-th pair of the round (its leaves concatenated in order)
+    auto pair_ref = [&](int L, int q) -> uint32_t {
+      uint32_t ref = 0;
+      bool found = false;
+#pragma unroll
+      for (int i = 0; i < kLeavesPerRound; ++i) {
+        const uint32_t c = seg_c[i * 64 + L];
+        if (!found && static_cast<uint32_t>(q) < c) {
+          ref = seg_f[i * 64 + L] + q;
+          found = true;
+        }
+        if (!found) q -= static_cast<int>(c);
+      }
+      return ref;
+    };
     int best_ref = -1;
     for (int base = 0; base < total; base += kPairBatch) {
       const int lim = min(total - base, kPairBatch);
-      const int k0 = max(excl, base), k1 = min(excl + static_cast<int>(count), base + lim);
+      const int k0 = max(excl, base), k1 = min(excl + count, base + lim);
       __syncthreads();
       own32[lane] = 0u;
       omin[lane] = 0x7f800000;  // order key of +inf
-      ocnt[lane] = 0;
+      otie[lane] = 0;
       __syncthreads();
       // owner table: each segment marks its first slot, then a max-scan over the
       // batch in slot order (owners increase with the slot)
@@ -385,9 +437,9 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         const int j2 = j + 64;
         const bool two = j2 < lim;
         const int L1 = own[j], L2 = own[two ? j2 : j];
-        const uint32_t ref1 = seg_first[L1] + static_cast<uint32_t>(base + j - seg_start[L1]);
-        const uint32_t ref2 = seg_first[L2] + static_cast<uint32_t>(base + (two ? j2 : j) - seg_start[L2]);
-        const float2 c1 = S.ref_c[ref1], c2 = S.ref_c[ref2];
+        const uint32_t ref1 = pair_ref(L1, base + j - seg_start[L1]);
+        const uint32_t ref2 = pair_ref(L2, base + (two ? j2 : j) - seg_start[L2]);
+        const float2 cc1 = S.ref_c[ref1], cc2 = S.ref_c[ref2];
         const float4 a1 = S.ref_a[ref1], a2 = S.ref_a[ref2];
         const float4 b1 = S.ref_b[ref1], b2 = S.ref_b[ref2];
         const float4 x1 = ray4[2 * L1], y1 = ray4[2 * L1 + 1], x2 = ray4[2 * L2], y2 = ray4[2 * L2 + 1];
@@ -396,7 +448,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         for (int u = 0; u < 2; ++u) {
           if (u == 1 && !two) break;
           const float4 x = u ? x2 : x1, y = u ? y2 : y1;
-          const float2 c = u ? c2 : c1;
+          const float2 c = u ? cc2 : cc1;
           const V3 ro = v3(x.x, x.y, x.z), rd = v3(x.w, y.x, y.y);
           const int prim = __float_as_int(c.y);
           float t = __int_as_float(0x7fc00000);  // NaN: no hit
@@ -415,16 +467,14 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         }
       }
       __syncthreads();
-      // hits within 2 EPS of their owner's minimum (the minimum itself included)
+      // hits within 2 EPS of their owner's minimum (the minimum itself included):
+      // otie = count << 16 | slot of the minimum (meaningful when count == 1)
       for (int j = lane; j < lim; j += 64) {
         const float t = res[j];
         if (t == t) {
           const int L = own[j];
           const int key = omin[L];
-          if (t - order_val(key) <= 2.f * WR_EPS) {
-            atomicAdd(ocnt + L, 1);
-            if (order_key(t) == key) oidx[L] = j;
-          }
+          if (t - order_val(key) <= 2.f * WR_EPS) atomicAdd(otie + L, (1 << 16) + (order_key(t) == key ? j : 0));
         }
       }
       __syncthreads();
@@ -434,23 +484,26 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       // only hit within 2 EPS of itself and the incoming best is 2 EPS away from
       // m either way, the outcome is decided by m alone; otherwise this owner
       // replays its pairs in order.
-      if (act && k0 < k1 && ocnt[lane] > 0) {
-        const float m = order_val(omin[lane]);
-        bool decided = ocnt[lane] == 1;
-        if (decided) {
-          if (t_best - m > 2.f * WR_EPS) {
-            t_best = m;
-            best_ref = static_cast<int>(first) + (base + oidx[lane] - excl);
-          } else if (!(m - t_best > 2.f * WR_EPS)) {
-            decided = false;
+      if (act && k0 < k1) {
+        const int tie = otie[lane];
+        if (tie) {
+          const float m = order_val(omin[lane]);
+          bool decided = (tie >> 16) == 1;
+          if (decided) {
+            if (t_best - m > 2.f * WR_EPS) {
+              t_best = m;
+              best_ref = static_cast<int>(pair_ref(lane, base + (tie & 0xffff) - excl));
+            } else if (!(m - t_best > 2.f * WR_EPS)) {
+              decided = false;
+            }
           }
-        }
-        if (!decided) {
-          for (int k = k0; k < k1; ++k) {
-            const float t = res[k - base];
-            if (t == t && cmpf(t - t_best) < 0) {
-              t_best = t;
-              best_ref = static_cast<int>(first) + (k - excl);
+          if (!decided) {
+            for (int k = k0; k < k1; ++k) {
+              const float t = res[k - base];
+              if (t == t && cmpf(t - t_best) < 0) {
+                t_best = t;
+                best_ref = static_cast<int>(pair_ref(lane, k - excl));
+              }
             }
           }
         }
@@ -462,17 +515,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         const int prim = __float_as_int(S.ref_c[best_ref].y);
         best = (!SPH || prim >= 0) ? prim : -prim - 1;
       }
-      // ---- pop (:375-383); tmin only changes here, so the `ray.tmax < tmin`
-      // check of :323 is evaluated after every pop
-      bool done = true;
-      if (sp > 0) {
-        --sp;
-        node = stk_node[sp * 64];
-        tmin = stk_tmin[sp * 64];
-        tmax = sp > 0 ? stk_tmin[(sp - 1) * 64] : root_tmax;
-        done = rtmax < tmin;
-      }
-      if (done) {
+      if (!more) {
         (inb ? qb : qa).out_t[r] = t_best;
         (inb ? qb : qa).out_prim[r] = best;
         r = -1;

@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libwinmad_rt.so")
+# WR_LIB selects another build of the same library (kernel variants under test)
+LIB_PATH = os.environ.get("WR_LIB") or os.path.join(PKG_DIR, "libwinmad_rt.so")
 
 WR_OK, WR_E_ARG, WR_E_IO, WR_E_HIP, WR_E_SCENE, WR_E_NODEVICE = 0, -1, -2, -3, -4, -5
 K_TRACE, K_SHADE, K_RESOLVE, K_GEN, K_OTHER = 0, 1, 2, 3, 4
