@@ -177,7 +177,8 @@ struct RayQueue {
 //          each of its kLeavesPerRound leaves of the round
 //   own    owner lane of each pair of the batch (bytes)
 //   res    kPairBatch pair results (t, or NaN for "no hit")
-//   omin   per-owner minimum hit (order key); otie = (hits within 2 EPS) << 16 | slot
+//   owner  per ray: (min hit key, smallest prim at it) and (min hit key, largest
+//          prim at it) as 64-bit atomics, + a flag for hits in (min, min + 2 EPS]
 constexpr int kPairBatch = 256;
 #ifndef WR_LEAVES_PER_ROUND
 #define WR_LEAVES_PER_ROUND 4
@@ -189,7 +190,7 @@ constexpr int kLeavesPerRound = WR_LEAVES_PER_ROUND;  // leaves a lane may colle
 constexpr int kLeavesWait = WR_LEAVES_WAIT;           // the walk runs until every lane has this many
 __host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
   return size_t(depth) * 64 * (narrow ? 6 : 8) +
-         size_t(4) * (8 * 64 + 64 + (1 + 2 * kLeavesPerRound) * 64 + kPairBatch / 4 + kPairBatch + 2 * 64);
+         size_t(4) * (8 * 64 + 64 + (1 + 2 * kLeavesPerRound) * 64 + kPairBatch / 4 + kPairBatch + 4 * 64 + 16);
 }
 
 // Persistent closest-hit traversal over up to two ray queues (one wave per
@@ -257,8 +258,9 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
   uint8_t* own = reinterpret_cast<uint8_t*>(seg_c + kLeavesPerRound * 64);  // [kPairBatch]
   uint32_t* own32 = reinterpret_cast<uint32_t*>(own);
   float* res = reinterpret_cast<float*>(own + kPairBatch);  // [kPairBatch]
-  int* omin = reinterpret_cast<int*>(res + kPairBatch);     // [64]
-  int* otie = omin + 64;                                    // [64]
+  unsigned long long* olo = reinterpret_cast<unsigned long long*>(res + kPairBatch);  // [64] key << 32 | prim
+  unsigned long long* ohi = olo + 64;  // [64] (INT_MAX - key) << 32 | prim
+  uint8_t* onear = reinterpret_cast<uint8_t*>(ohi + 64);  // [64]
   const int na = qa.count ? *qa.count : 0;
   const int n = na + (qb.count ? *qb.count : 0);
   bool inb = false;      // the lane's ray comes from qb
@@ -404,14 +406,14 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       }
       return ref;
     };
-    int best_ref = -1;
     for (int base = 0; base < total; base += kPairBatch) {
       const int lim = min(total - base, kPairBatch);
       const int k0 = max(excl, base), k1 = min(excl + count, base + lim);
       __syncthreads();
       own32[lane] = 0u;
-      omin[lane] = 0x7f800000;  // order key of +inf
-      otie[lane] = 0;
+      olo[lane] = ~0ull;
+      ohi[lane] = 0ull;
+      onear[lane] = 0;
       __syncthreads();
       // owner table: each segment marks its first slot, then a max-scan over the
       // batch in slot order (owners increase with the slot)
@@ -459,40 +461,44 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
           } else {
             h = sph_hit(S, -prim - 1, ro, rd, y.z, y.w, th);
           }
-          if (h) {
+          if (h) {  // t > EPS > 0: the order key is the float's bits
             t = th;
-            atomicMin(omin + (u ? L2 : L1), order_key(t));
+            const unsigned long long key = static_cast<uint32_t>(__float_as_int(t));
+            const unsigned long long pr = static_cast<uint32_t>((!SPH || prim >= 0) ? prim : -prim - 1);
+            atomicMin(olo + (u ? L2 : L1), (key << 32) | pr);
+            atomicMax(ohi + (u ? L2 : L1), ((0x7fffffffull - key) << 32) | pr);
           }
           res[u ? j2 : j] = t;
         }
       }
       __syncthreads();
-      // hits within 2 EPS of their owner's minimum (the minimum itself included):
-      // otie = count << 16 | slot of the minimum (meaningful when count == 1)
+      // flag owners with a hit in (min, min + 2 EPS]
       for (int j = lane; j < lim; j += 64) {
         const float t = res[j];
         if (t == t) {
           const int L = own[j];
-          const int key = omin[L];
-          if (t - order_val(key) <= 2.f * WR_EPS) atomicAdd(otie + L, (1 << 16) + (order_key(t) == key ? j : 0));
+          const float m = __int_as_float(static_cast<int>(olo[L] >> 32));
+          if (t != m && t - m <= 2.f * WR_EPS) onear[L] = 1;
         }
       }
       __syncthreads();
       WR_STAMP(3)
       // first-found-wins (cmp(t - best) < 0, in leaf order).  The sequential rule
-      // keeps best within EPS of the minimum m once m is seen, so when m is the
-      // only hit within 2 EPS of itself and the incoming best is 2 EPS away from
-      // m either way, the outcome is decided by m alone; otherwise this owner
-      // replays its pairs in order.
+      // keeps best within EPS of the minimum m once m is seen, and a repeat of a
+      // value already seen is never taken.  So when every hit within 2 EPS of m
+      // is exactly m on one primitive (a triangle met again in a later leaf of
+      // the round) and the incoming best is 2 EPS away from m either way, m
+      // decides the outcome; otherwise this owner replays its pairs in order.
       if (act && k0 < k1) {
-        const int tie = otie[lane];
-        if (tie) {
-          const float m = order_val(omin[lane]);
-          bool decided = (tie >> 16) == 1;
+        const unsigned long long lo = olo[lane];
+        if (lo != ~0ull) {  // at least one hit
+          const float m = __int_as_float(static_cast<int>(lo >> 32));
+          const int pmin = static_cast<int>(lo & 0xffffffffull);
+          bool decided = onear[lane] == 0 && pmin == static_cast<int>(ohi[lane] & 0xffffffffull);
           if (decided) {
             if (t_best - m > 2.f * WR_EPS) {
               t_best = m;
-              best_ref = static_cast<int>(pair_ref(lane, base + (tie & 0xffff) - excl));
+              best = pmin;
             } else if (!(m - t_best > 2.f * WR_EPS)) {
               decided = false;
             }
@@ -502,7 +508,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
               const float t = res[k - base];
               if (t == t && cmpf(t - t_best) < 0) {
                 t_best = t;
-                best_ref = static_cast<int>(pair_ref(lane, k - excl));
+                const int c = __float_as_int(S.ref_c[pair_ref(lane, k - excl)].y);
+                best = (!SPH || c >= 0) ? c : -c - 1;
               }
             }
           }
@@ -511,10 +518,6 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       WR_STAMP(4)
     }
     if (act) {
-      if (best_ref >= 0) {
-        const int prim = __float_as_int(S.ref_c[best_ref].y);
-        best = (!SPH || prim >= 0) ? prim : -prim - 1;
-      }
       if (!more) {
         (inb ? qb : qa).out_t[r] = t_best;
         (inb ? qb : qa).out_prim[r] = best;
