@@ -100,25 +100,27 @@ __device__ __forceinline__ bool tri_test(float4 a, float4 b, float f, V3 o, V3 d
   const float BLKC = B * L - K * C;
   const float gnum = I * AKJB + H * JCAL + G * BLKC;
   const float tnum = -(F * AKJB + E * JCAL + D * BLKC);
+  // one combined screen predicate and one branch (divergent early returns cost
+  // exec-mask bookkeeping per test); NaN estimates compare false and fall through
   const float ad = fabsf(denom);
-  if (ad > 1e-30f && ad < 1e30f) {
-    const float r = __builtin_amdgcn_rcpf(denom);
-    const float ba = bnum * r, ga = gnum * r, ta = tnum * r;
-    const float mb = 1e-5f * fabsf(ba), mg = 1e-5f * fabsf(ga), mt = 1e-5f * fabsf(ta);
-    if (ba < -WR_EPS - mb || ba > 1.f + mb) return false;
-    if (ga < -WR_EPS - mg || ba + ga > 1.f + (mb + mg) + 1e-6f) return false;
-    if (ta < WR_EPS - mt || ta > rtmax + mt) return false;
-    if (ta - t_best > -WR_EPS + (mt + 1e-5f * fabsf(t_best))) return false;
-  }
+  const float r = __builtin_amdgcn_rcpf(denom);
+  const float ba = bnum * r, ga = gnum * r, ta = tnum * r;
+  const float mb = 1e-5f * fabsf(ba), mg = 1e-5f * fabsf(ga), mt = 1e-5f * fabsf(ta);
+  const bool drop = (ba < -WR_EPS - mb) | (ba > 1.f + mb) | (ga < -WR_EPS - mg) |
+                    (ba + ga > 1.f + (mb + mg) + 1e-6f) | (ta < WR_EPS - mt) | (ta > rtmax + mt) |
+                    (ta - t_best > -WR_EPS + (mt + 1e-5f * fabsf(t_best)));
+  if (drop & (ad > 1e-30f) & (ad < 1e30f)) return false;
+  // the reference's test, exactly (its early outs only skip work, never change
+  // the outcome, so all three quotients are formed here)
   const float beta = bnum / denom;
-  if (cmpf(beta) < 0 || beta > 1.f) return false;
   const float gamma = gnum / denom;
-  if (cmpf(gamma) < 0 || beta + gamma > 1.f) return false;
   const float t = tnum / denom;
-  if (cmpf(t) <= 0) return false;
-  if (t < rtmin || t > rtmax) return false;
+  const bool beta_ok = !(cmpf(beta) < 0 || beta > 1.f);
+  const bool gamma_ok = !(cmpf(gamma) < 0 || beta + gamma > 1.f);
+  const bool t_ok = cmpf(t) > 0 && !(t < rtmin || t > rtmax);
+  const bool ok = beta_ok && gamma_ok && t_ok;
   t_out = t;
-  return true;
+  return ok;
 }
 
 // Sphere::hit (sphere.cpp:17-78): only t and the accept decision
