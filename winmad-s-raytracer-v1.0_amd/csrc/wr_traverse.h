@@ -212,6 +212,32 @@ __host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
 //     over its pairs of the round, concatenated in leaf order;
 //   * lanes that finish their ray take the next one from a global counter (one
 //     atomic per wave per refill), so a wave stays full until the queues drain.
+// Wave64 inclusive scans on DPP (no LDS round trip, unlike __shfl_up's
+// ds_bpermute): Hillis-Steele inside each 16-lane row (row_shr 1, 2, 4, 8;
+// out-of-row sources read 0), then row 0's total into row 1 and row 2's into
+// row 3 (row_bcast:15), then rows 0-1's total into rows 2-3 (row_bcast:31).
+// Values must be >= 0 for the max scan (0 is its identity).  Full wave only.
+__device__ __forceinline__ int wave_scan_add(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+__device__ __forceinline__ int wave_scan_max(int v) {
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+// value of lane - 1 (0 in lane 0): DPP wave_shr:1
+__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, true); }
+
 // monotone int key of a float (signed-int order == float order, -0 < +0)
 __device__ __forceinline__ int order_key(float f) {
   const int b = __float_as_int(f);
@@ -302,7 +328,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
         int base = 0;
         if (lane == leader) base = atomicAdd(fetch, __popcll(m));
-        base = __shfl(base, leader);
+        base = __builtin_amdgcn_readlane(base, leader);
         const int idx = base + __popcll(m & ((1ull << lane) - 1ull));
         if (idle && idx < n) {
           inb = idx >= na;
@@ -384,13 +410,9 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
     }
     WR_STAMP(1)
     // ---- leaf phase (:359-373): number the wave's (ray, ref) pairs
-    int incl = count;
-    for (int off = 1; off < 64; off <<= 1) {
-      const int v = __shfl_up(incl, off);
-      if (lane >= off) incl += v;
-    }
+    const int incl = wave_scan_add(count);
     const int excl = incl - count;
-    const int total = __shfl(incl, 63);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
     seg_start[lane] = excl;
     rbest[lane] = t_best;
     // ref of lane L's q-th pair of the round (its leaves concatenated in order)
@@ -425,13 +447,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         const uint32_t w = own32[lane];
         const uint32_t m0 = w & 0xffu, m1 = max(m0, (w >> 8) & 0xffu), m2 = max(m1, (w >> 16) & 0xffu),
                        m3 = max(m2, w >> 24);
-        uint32_t run = m3;
-        for (int off = 1; off < 64; off <<= 1) {
-          const uint32_t v = __shfl_up(run, off);
-          if (lane >= off) run = max(run, v);
-        }
-        uint32_t prev = __shfl_up(run, 1);
-        if (lane == 0) prev = 0u;
+        const uint32_t run = static_cast<uint32_t>(wave_scan_max(static_cast<int>(m3)));
+        const uint32_t prev = static_cast<uint32_t>(wave_shr1(static_cast<int>(run)));
         own32[lane] = max(m0, prev) | (max(m1, prev) << 8) | (max(m2, prev) << 16) | (max(m3, prev) << 24);
       }
       __syncthreads();
