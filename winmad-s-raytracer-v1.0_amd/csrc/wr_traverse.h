@@ -175,9 +175,9 @@ struct RayQueue {
 //   stack  [depth][64] tmin (float) + [depth][64] node (u16 when the tree has
 //          <= 65536 nodes, NARROW; u32 otherwise)
 //   rays   per lane 8 floats (o.xyz, d.x | d.yz, tmin, tmax) + best t   (AoS, b128 reads)
-//   leaf   per lane: exclusive prefix of its pair count, and (first, count) of
-//          each of its kLeavesPerRound leaves of the round
-//   own    owner lane of each pair of the batch (bytes)
+//   leaf   per lane: exclusive prefix of its pair count; per leaf id
+//          (lane * kLeavesPerRound + i): first ref and its offset in the lane's pairs
+//   own    leaf id of each pair of the batch (bytes)
 //   res    kPairBatch pair results (t, or NaN for "no hit")
 //   owner  per ray: (min hit key, smallest prim at it) and (min hit key, largest
 //          prim at it) as 64-bit atomics, + a flag for hits in (min, min + 2 EPS]
@@ -281,9 +281,9 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
   float4* ray4 = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds) + size_t(depth) * 64 * (NARROW ? 6 : 8));
   float* rbest = reinterpret_cast<float*>(ray4 + 2 * 64);  // [64]
   int* seg_start = reinterpret_cast<int*>(rbest + 64);    // [64]
-  uint32_t* seg_f = reinterpret_cast<uint32_t*>(seg_start + 64);  // [kLeavesPerRound][64]
-  uint32_t* seg_c = seg_f + kLeavesPerRound * 64;                  // [kLeavesPerRound][64]
-  uint8_t* own = reinterpret_cast<uint8_t*>(seg_c + kLeavesPerRound * 64);  // [kPairBatch]
+  uint32_t* leaf_first = reinterpret_cast<uint32_t*>(seg_start + 64);  // [64 * kLeavesPerRound]
+  int* leaf_off = reinterpret_cast<int*>(leaf_first + kLeavesPerRound * 64);  // [64 * kLeavesPerRound]
+  uint8_t* own = reinterpret_cast<uint8_t*>(leaf_off + kLeavesPerRound * 64);  // [kPairBatch]
   uint32_t* own32 = reinterpret_cast<uint32_t*>(own);
   float* res = reinterpret_cast<float*>(own + kPairBatch);  // [kPairBatch]
   unsigned long long* olo = reinterpret_cast<unsigned long long*>(res + kPairBatch);  // [64] key << 32 | prim
@@ -368,14 +368,15 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
     // ---- walk to the next leaves (:321-358, pops :375-383).  One record pair
     // per iteration resolves up to two levels; the walk goes on while any lane
     // still has no leaf this round.
-    // the round's leaves of this lane go straight to its LDS column
-#pragma unroll
-    for (int i = 0; i < kLeavesPerRound; ++i) seg_c[i * 64 + lane] = 0u;
+    // the round's leaves of this lane: first ref and pair offset, in LDS
     int nl = 0, count = 0;
     while (__ballot(more && nl < kLeavesWait)) {
       if (more && nl < kLeavesPerRound) {
         const uint4 q = S.nrec[node];
         const uint2 qr = S.nrec_r[node];
+        // keep both loads in flight together: otherwise the second is sunk into
+        // the inner-node branch and its latency is paid after the first's
+        asm volatile("" : : "v"(q.y), "v"(qr.x), "v"(qr.y));
         uint2 nd = make_uint2(q.x, q.y);
         bool leaf = (nd.y & 3u) == 3u;
         if (!leaf) {
@@ -386,8 +387,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
           if (!leaf) node = step(nd, node);
         }
         if (leaf) {
-          seg_f[nl * 64 + lane] = nd.x;
-          seg_c[nl * 64 + lane] = nd.y >> 2;
+          leaf_first[lane * kLeavesPerRound + nl] = nd.x;
+          leaf_off[lane * kLeavesPerRound + nl] = count;
           count += static_cast<int>(nd.y >> 2);
           ++nl;
           if (COUNT) {
@@ -415,20 +416,12 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
     const int total = __builtin_amdgcn_readlane(incl, 63);
     seg_start[lane] = excl;
     rbest[lane] = t_best;
-    // ref of lane L's q-th pair of the round (its leaves concatenated in order)
-    auto pair_ref = [&](int L, int q) -> uint32_t {
-      uint32_t ref = 0;
-      bool found = false;
-#pragma unroll
-      for (int i = 0; i < kLeavesPerRound; ++i) {
-        const uint32_t c = seg_c[i * 64 + L];
-        if (!found && static_cast<uint32_t>(q) < c) {
-          ref = seg_f[i * 64 + L] + q;
-          found = true;
-        }
-        if (!found) q -= static_cast<int>(c);
-      }
-      return ref;
+    // ref of this lane's q-th pair of the round (its leaves concatenated in order)
+    auto own_ref = [&](int q) -> uint32_t {
+      int i = 0;
+      for (int k = 1; k < nl; ++k)
+        if (q >= leaf_off[lane * kLeavesPerRound + k]) i = k;
+      return leaf_first[lane * kLeavesPerRound + i] + static_cast<uint32_t>(q - leaf_off[lane * kLeavesPerRound + i]);
     };
     for (int base = 0; base < total; base += kPairBatch) {
       const int lim = min(total - base, kPairBatch);
@@ -439,9 +432,17 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       ohi[lane] = 0ull;
       onear[lane] = 0;
       __syncthreads();
-      // owner table: each segment marks its first slot, then a max-scan over the
-      // batch in slot order (owners increase with the slot)
-      if (k0 < k1) own[k0 - base] = static_cast<uint8_t>(lane);
+      // leaf table: each leaf marks its first slot in the batch, then a max-scan
+      // over the batch in slot order (leaf ids increase with the slot)
+      if (k0 < k1) {
+        int s0 = leaf_off[lane * kLeavesPerRound];
+        for (int i = 0; i < nl; ++i) {
+          const int s1 = i + 1 < nl ? leaf_off[lane * kLeavesPerRound + i + 1] : count;
+          const int a0 = max(excl + s0, base), a1 = min(excl + s1, base + lim);
+          if (a0 < a1) own[a0 - base] = static_cast<uint8_t>(lane * kLeavesPerRound + i);
+          s0 = s1;
+        }
+      }
       __syncthreads();
       {
         const uint32_t w = own32[lane];
@@ -457,9 +458,11 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       for (int j = lane; j < lim; j += 128) {
         const int j2 = j + 64;
         const bool two = j2 < lim;
-        const int L1 = own[j], L2 = own[two ? j2 : j];
-        const uint32_t ref1 = pair_ref(L1, base + j - seg_start[L1]);
-        const uint32_t ref2 = pair_ref(L2, base + (two ? j2 : j) - seg_start[L2]);
+        const int id1 = own[j], id2 = own[two ? j2 : j];
+        const int L1 = id1 / kLeavesPerRound, L2 = id2 / kLeavesPerRound;
+        const uint32_t ref1 = leaf_first[id1] + static_cast<uint32_t>(base + j - seg_start[L1] - leaf_off[id1]);
+        const uint32_t ref2 =
+            leaf_first[id2] + static_cast<uint32_t>(base + (two ? j2 : j) - seg_start[L2] - leaf_off[id2]);
         const float2 cc1 = S.ref_c[ref1], cc2 = S.ref_c[ref2];
         const float4 a1 = S.ref_a[ref1], a2 = S.ref_a[ref2];
         const float4 b1 = S.ref_b[ref1], b2 = S.ref_b[ref2];
@@ -495,7 +498,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       for (int j = lane; j < lim; j += 64) {
         const float t = res[j];
         if (t == t) {
-          const int L = own[j];
+          const int L = own[j] / kLeavesPerRound;
           const float m = __int_as_float(static_cast<int>(olo[L] >> 32));
           if (t != m && t - m <= 2.f * WR_EPS) onear[L] = 1;
         }
@@ -527,7 +530,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
               const float t = res[k - base];
               if (t == t && cmpf(t - t_best) < 0) {
                 t_best = t;
-                const int c = __float_as_int(S.ref_c[pair_ref(lane, k - excl)].y);
+                const int c = __float_as_int(S.ref_c[own_ref(k - excl)].y);
                 best = (!SPH || c >= 0) ? c : -c - 1;
               }
             }
