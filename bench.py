@@ -8,8 +8,12 @@ in HBM; one RCCL reduce(sum) of the films to rank 0 per batch is inside the
 timed region.  value = (closest + shadow traversals of all ranks) / max-rank
 wall time, in Mrays/s.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
     torchrun --nproc-per-node N bench.py --gpus N ...   (the driver's N > 1 form)
+
+--config picks the SURVEY.md 8(d) configuration: c2 (default; the BASELINE.json
+metric), c3 (cbox + dragon PT, one step = one sample index of a 512-spp
+stratified render), c4 (the 1M-triangle synthetic torus, BDPT).
 
 Extra JSON keys: spp_per_sec, roofline (dominant kernel = KD traversal, HIP
 events on the context stream), cpu_baseline (the oracle's C port, MT-serial,
@@ -47,29 +51,53 @@ def algorithmic_bytes(rays, inner, leaves, refs):
     return 48.0 * rays + 8.0 * (inner + leaves) + 4.0 * refs + 40.0 * refs
 
 
-def cpu_baseline(scene_path, W, H, budget_paths, chunks=16):
+def cpu_baseline(kind, scene_path, W, H, budget, chunks=16):
     """Oracle (oracle/cpuref.c, C port of the reference path), MT-serial RNG,
-    one thread, on `budget_paths` path indices of one iteration taken as
-    `chunks` evenly spaced contiguous runs (so sky rows and floor rows are
-    sampled in proportion)."""
+    one thread, on a bounded sample of the same frame: `budget` path indices
+    (BDPT) or pixels at 1 spp (PT), taken as `chunks` evenly spaced contiguous
+    runs so sky rows and geometry rows are sampled in proportion."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle
     s = _oracle.Scene(scene_path)
     P = W * H
-    per = budget_paths // chunks
+    per = budget // chunks
     rays = 0
     dt = 0.0
     for c in range(chunks):
         b = c * P // chunks
         t0 = time.perf_counter()
-        _, st = s.bdpt(W, H, 1, 5489 + c, mode=0, path_range=(b, b + per))
+        if kind == "bdpt":
+            _, st = s.bdpt(W, H, 1, 5489 + c, mode=0, path_range=(b, b + per))
+        else:
+            _, st = s.pt(W, H, 1, 7, 5489 + c, mode=0, pix_range=(b, b + per))
         dt += time.perf_counter() - t0
         rays += st.closest_rays + st.shadow_rays
     n = per * chunks
+    what = "camera+light path pairs of one iteration" if kind == "bdpt" else "pixels at 1 spp"
     return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/cpuref.c MT-serial BDPT, torus {W}x{H}, {n} camera+light path pairs of one "
-                      f"iteration in {chunks} evenly spaced runs ({rays} rays, {dt:.1f} s CPU); "
+            "sample": f"oracle/cpuref.c MT-serial {kind.upper()}, {os.path.basename(scene_path)} {W}x{H}, "
+                      f"{n} {what} in {chunks} evenly spaced runs ({rays} rays, {dt:.1f} s CPU); "
                       f"spp/s={n / dt:.0f}"}
+
+
+# SURVEY.md 8(d) configurations a bench line can be quoted on
+CONFIGS = {
+    "c2": {"desc": "torus.scene BDPT", "integrator": "bdpt"},
+    "c3": {"desc": "cbox + dragon PT, 512 spp stratification, MAX_TRACING_DEPTH 7", "integrator": "pt"},
+    "c4": {"desc": "1M-triangle synthetic torus BDPT", "integrator": "bdpt"},
+}
+METRIC = "Mrays/sec + spp/sec at 1920x1080, torus.scene BDPT, 1/2/4/8 MI355X"
+
+
+def make_scene(cfg, W, H, tmp):
+    from winmad_rt import scenes
+    if cfg == "c2":
+        return scenes.write(os.path.join(tmp, "torus.scene"), scenes.torus_scene(W, H))
+    if cfg == "c3":
+        return scenes.write(os.path.join(tmp, "cbox.scene"), scenes.cbox_scene(W, H))
+    obj = os.path.join(tmp, "torus_1m.obj")
+    scenes.synth_torus_obj(obj)
+    return scenes.write(os.path.join(tmp, "torus_1m.scene"), scenes.torus_scene(W, H, torus_obj=obj))
 
 
 def main():
@@ -79,6 +107,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                    help="c2 (default, the BASELINE metric), c3 PT, c4 1M triangles")
+    ap.add_argument("--spp", type=int, default=512, help="c3: stratification grid of the PT render")
     ap.add_argument("--cpu-paths", type=int, default=1000000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting replay")
@@ -94,20 +125,30 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from winmad_rt import native, scenes
+    from winmad_rt import native
     from winmad_rt import dist as wdist
 
     W, H, K = args.width, args.height, args.steps
+    cfg = CONFIGS[args.config]
+    pt = cfg["integrator"] == "pt"
     tmp = tempfile.mkdtemp(prefix=f"wr_bench_{rank}_")
-    scene_path = scenes.write(os.path.join(tmp, "torus.scene"), scenes.torus_scene(W, H))
+    scene_path = make_scene(args.config, W, H, tmp)
     sc = native.Scene(scene_path)
     ctx = native.Context(sc, local)
     film = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
 
-    # warmup (iteration indices outside the timed ones)
-    if args.warmup > 0:
-        ctx.render_bdpt(W, H, iterations=args.warmup, seed=5489, iter_begin=1 << 20,
-                        film_ptr=film.data_ptr())
+    # one step = one iteration (BDPT) / one sample index of the spp grid (PT);
+    # every rank renders K of its own (weak scaling)
+    def render(begin, count, **kw):
+        if pt:
+            return ctx.render_path(W, H, spp=args.spp, max_depth=7, seed=5489, sample_begin=begin,
+                                   sample_count=count, **kw)
+        return ctx.render_bdpt(W, H, iterations=count, seed=5489, iter_begin=begin, **kw)
+
+    if pt and (world * K > args.spp or args.warmup > args.spp):
+        raise SystemExit(f"c3: --steps x ranks ({world * K}) must not exceed --spp ({args.spp})")
+    if args.warmup > 0:  # warm-up samples / iterations outside the timed ones
+        render((args.spp - args.warmup) if pt else (1 << 20), args.warmup, film_ptr=film.data_ptr())
     film.zero_()
     torch.cuda.synchronize()
     if dist:
@@ -115,8 +156,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     it0 = wdist.bdpt_iteration_begin(rank, K)
-    _, st = ctx.render_bdpt(W, H, iterations=K, seed=5489, iter_begin=it0, film_ptr=film.data_ptr(),
-                            time_kernels=1)
+    _, st = render(it0, K, film_ptr=film.data_ptr(), time_kernels=1)
     wdist.reduce_film(film, dist)  # one film reduction per batch (RCCL)
     torch.cuda.synchronize()
     if dist:
@@ -133,14 +173,13 @@ def main():
     if not args.no_count and rank == 0:
         # replay the same iterations with per-traversal counters (identical ray set:
         # the counter RNG makes the work a pure function of (seed, iteration, path))
-        _, cst = ctx.render_bdpt(W, H, iterations=K, seed=5489, iter_begin=it0, count_work=1,
-                                 film=None)
+        _, cst = render(it0, K, count_work=1, film=None)
         assert cst.closest_rays == st.closest_rays and cst.shadow_rays == st.shadow_rays
         total_bytes = algorithmic_bytes(rays, cst.inner_visits, cst.leaf_visits, cst.prim_refs)
         per_launch = total_bytes / max(1, trace_launches)
         avg_launch_s = trace_ms / 1e3 / max(1, trace_launches)
         achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic() if args.config == "c2" else (None, None)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
@@ -153,21 +192,26 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(scene_path, W, H, args.cpu_paths)
+        budget = {"c2": args.cpu_paths, "c3": args.cpu_paths // 4, "c4": args.cpu_paths // 20}[args.config]
+        cpu = cpu_baseline(cfg["integrator"], scene_path, W, H, budget)
 
     if rank == 0:
         value = total_rays / elapsed / 1e6
+        unit_name = "samples (spp)" if pt else "iterations (spp)"
+        metric = METRIC if args.config == "c2" else \
+            f"Mrays/sec + spp/sec at {W}x{H}, {cfg['desc']} ({args.config.upper()}), MI355X"
         out = {
-            "metric": "Mrays/sec + spp/sec at 1920x1080, torus.scene BDPT, 1/2/4/8 MI355X",
+            "metric": metric,
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: torus.scene (reference assets), counter RNG, faithful ray set",
-            "config": {"workload": f"torus.scene BDPT {W}x{H}, {K} iterations (spp) per GPU, controlLength 3, "
-                                   f"maxPathLength 10", "width": W, "height": H,
-                       "iterations_per_gpu": K, "parallelism": f"sample-batch x{world}"},
+            "data": "synthetic: reference scene assets, counter RNG, faithful ray set",
+            "config": {"workload": f"{cfg['desc']} {W}x{H}, {K} {unit_name} per GPU"
+                                   + ("" if pt else ", controlLength 3, maxPathLength 10"),
+                       "scene_config": args.config.upper(), "width": W, "height": H,
+                       "steps_per_gpu": K, "parallelism": f"sample-batch x{world}"},
             "spp_per_sec": round(W * H * K * world / elapsed, 1),
-            "rays_per_iteration": round(total_rays / (K * world)),
+            "rays_per_step": round(total_rays / (K * world)),
             "roofline": roofline, "cpu_baseline": cpu,
         }
         if cpu:
