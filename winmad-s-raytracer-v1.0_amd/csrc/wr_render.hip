@@ -1423,6 +1423,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
     // and registers); more would only queue behind the first wave of blocks
     c->narrow = nn <= 65536;
+    // test knob: WR_TRACE_WIDE=1 runs the 32-bit-stack variant on any tree
+    if (const char* e = std::getenv("WR_TRACE_WIDE")) c->narrow = c->narrow && std::atoi(e) == 0;
     const size_t lds = trace_lds_bytes(d.max_stack, c->narrow);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel(false, c->spheres, c->narrow, false),
