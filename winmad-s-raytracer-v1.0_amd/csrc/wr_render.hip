@@ -997,7 +997,7 @@ struct wr_context {
   int grid = 2048;
   int cus = 256;
   bool spheres = false;
-  bool narrow = false;  // tree of <= 65536 nodes: 16-bit stack entries
+  bool narrow = false;  // <= 65536 nodes, leaves <= 255 refs: 16-bit stack / pair offsets
   bool stamps = false;  // WR_TRACE_STAMPS=1: diagnostic traversal with phase stamps
   int trace_blocks = 4096;  // resident one-wave workgroups of the traversal
   std::vector<hipEvent_t> events;
@@ -1422,7 +1422,12 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   {
     // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
     // and registers); more would only queue behind the first wave of blocks
-    c->narrow = nn <= 65536;
+    // 16-bit stack nodes and 16-bit pair offsets (64 lanes x kLeavesPerRound
+    // leaves x max leaf size < 65536)
+    int max_leaf = 0;
+    for (const auto& k : s.nodes)
+      if (k.axis < 0) max_leaf = std::max(max_leaf, k.count);
+    c->narrow = nn <= 65536 && static_cast<int64_t>(max_leaf) * 64 * kLeavesPerRound < 65536;
     // test knob: WR_TRACE_WIDE=1 runs the 32-bit-stack variant on any tree
     if (const char* e = std::getenv("WR_TRACE_WIDE")) c->narrow = c->narrow && std::atoi(e) == 0;
     const size_t lds = trace_lds_bytes(d.max_stack, c->narrow);

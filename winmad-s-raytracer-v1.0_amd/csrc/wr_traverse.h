@@ -178,7 +178,6 @@ struct RayQueue {
 //   leaf   per lane: exclusive prefix of its pair count; per leaf id
 //          (lane * kLeavesPerRound + i): first ref and its offset in the lane's pairs
 //   own    leaf id of each pair of the batch (bytes)
-//   res    kPairBatch pair results (t, or NaN for "no hit")
 //   owner  per ray: (min hit key, smallest prim at it) and (min hit key, largest
 //          prim at it) as 64-bit atomics, + a flag for hits in (min, min + 2 EPS]
 constexpr int kPairBatch = 256;
@@ -188,11 +187,16 @@ constexpr int kPairBatch = 256;
 #ifndef WR_LEAVES_WAIT
 #define WR_LEAVES_WAIT 2
 #endif
+#ifndef WR_PAIRS_IN_FLIGHT
+#define WR_PAIRS_IN_FLIGHT 2
+#endif
+constexpr int kPairsInFlight = WR_PAIRS_IN_FLIGHT;     // (ray, triangle) records requested per lane per trip
 constexpr int kLeavesPerRound = WR_LEAVES_PER_ROUND;  // leaves a lane may collect per round
 constexpr int kLeavesWait = WR_LEAVES_WAIT;           // the walk runs until every lane has this many
 __host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
   return size_t(depth) * 64 * (narrow ? 6 : 8) +
-         size_t(4) * (8 * 64 + 64 + (1 + 2 * kLeavesPerRound) * 64 + kPairBatch / 4 + kPairBatch + 4 * 64 + 16);
+         size_t(4) * (8 * 64 + 64 + kLeavesPerRound * 64 + kLeavesPerRound * (narrow ? 32 : 64) + kPairBatch / 4 +
+                      4 * 64 + 16);
 }
 
 // Persistent closest-hit traversal over up to two ray queues (one wave per
@@ -280,13 +284,13 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
   // root-box tmax -- exactly the floats the reference's todo[] would hold.
   float4* ray4 = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds) + size_t(depth) * 64 * (NARROW ? 6 : 8));
   float* rbest = reinterpret_cast<float*>(ray4 + 2 * 64);  // [64]
-  int* seg_start = reinterpret_cast<int*>(rbest + 64);    // [64]
-  uint32_t* leaf_first = reinterpret_cast<uint32_t*>(seg_start + 64);  // [64 * kLeavesPerRound]
-  int* leaf_off = reinterpret_cast<int*>(leaf_first + kLeavesPerRound * 64);  // [64 * kLeavesPerRound]
+  uint32_t* leaf_first = reinterpret_cast<uint32_t*>(rbest + 64);  // [64 * kLeavesPerRound]
+  // first pair of each leaf in the round's numbering (lane-local during the walk)
+  using PairIdx = typename std::conditional<NARROW, uint16_t, uint32_t>::type;
+  PairIdx* leaf_off = reinterpret_cast<PairIdx*>(leaf_first + kLeavesPerRound * 64);  // [64 * kLeavesPerRound]
   uint8_t* own = reinterpret_cast<uint8_t*>(leaf_off + kLeavesPerRound * 64);  // [kPairBatch]
   uint32_t* own32 = reinterpret_cast<uint32_t*>(own);
-  float* res = reinterpret_cast<float*>(own + kPairBatch);  // [kPairBatch]
-  unsigned long long* olo = reinterpret_cast<unsigned long long*>(res + kPairBatch);  // [64] key << 32 | prim
+  unsigned long long* olo = reinterpret_cast<unsigned long long*>(own + kPairBatch);  // [64] key << 32 | prim
   unsigned long long* ohi = olo + 64;  // [64] (INT_MAX - key) << 32 | prim
   uint8_t* onear = reinterpret_cast<uint8_t*>(ohi + 64);  // [64]
   const int na = qa.count ? *qa.count : 0;
@@ -318,6 +322,19 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
     ++sp;
     tmax = t;
     return nearc;
+  };
+  // t of one (ray, primitive) pair, NaN when Triangle::hit / Sphere::hit reject it
+  // or (triangles) when it cannot beat `screen`, the ray's best at round start
+  auto pair_t = [&](float4 a, float4 b, float2 c, V3 ro, V3 rd, float rt0, float rt1, float screen) -> float {
+    const int prim = __float_as_int(c.y);
+    float th = __int_as_float(0x7fc00000);
+    bool h;
+    if (!SPH || prim >= 0) {
+      h = tri_test(a, b, c.x, ro, rd, rt0, rt1, screen, th);
+    } else {
+      h = sph_hit(S, -prim - 1, ro, rd, rt0, rt1, th);
+    }
+    return h ? th : __int_as_float(0x7fc00000);
   };
   for (;;) {
     // ---- refill idle lanes
@@ -388,7 +405,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
         }
         if (leaf) {
           leaf_first[lane * kLeavesPerRound + nl] = nd.x;
-          leaf_off[lane * kLeavesPerRound + nl] = count;
+          leaf_off[lane * kLeavesPerRound + nl] = static_cast<PairIdx>(count);
           count += static_cast<int>(nd.y >> 2);
           ++nl;
           if (COUNT) {
@@ -414,14 +431,15 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
     const int incl = wave_scan_add(count);
     const int excl = incl - count;
     const int total = __builtin_amdgcn_readlane(incl, 63);
-    seg_start[lane] = excl;
+    for (int i = 0; i < nl; ++i) leaf_off[lane * kLeavesPerRound + i] += static_cast<PairIdx>(excl);
     rbest[lane] = t_best;
-    // ref of this lane's q-th pair of the round (its leaves concatenated in order)
-    auto own_ref = [&](int q) -> uint32_t {
+    // ref of pair k of the round, k in this lane's range [excl, excl + count)
+    auto own_ref = [&](int k) -> uint32_t {
       int i = 0;
-      for (int k = 1; k < nl; ++k)
-        if (q >= leaf_off[lane * kLeavesPerRound + k]) i = k;
-      return leaf_first[lane * kLeavesPerRound + i] + static_cast<uint32_t>(q - leaf_off[lane * kLeavesPerRound + i]);
+      for (int x = 1; x < nl; ++x)
+        if (k >= static_cast<int>(leaf_off[lane * kLeavesPerRound + x])) i = x;
+      return leaf_first[lane * kLeavesPerRound + i] +
+             static_cast<uint32_t>(k - static_cast<int>(leaf_off[lane * kLeavesPerRound + i]));
     };
     for (int base = 0; base < total; base += kPairBatch) {
       const int lim = min(total - base, kPairBatch);
@@ -435,10 +453,10 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       // leaf table: each leaf marks its first slot in the batch, then a max-scan
       // over the batch in slot order (leaf ids increase with the slot)
       if (k0 < k1) {
-        int s0 = leaf_off[lane * kLeavesPerRound];
+        int s0 = static_cast<int>(leaf_off[lane * kLeavesPerRound]);
         for (int i = 0; i < nl; ++i) {
-          const int s1 = i + 1 < nl ? leaf_off[lane * kLeavesPerRound + i + 1] : count;
-          const int a0 = max(excl + s0, base), a1 = min(excl + s1, base + lim);
+          const int s1 = i + 1 < nl ? static_cast<int>(leaf_off[lane * kLeavesPerRound + i + 1]) : excl + count;
+          const int a0 = max(s0, base), a1 = min(s1, base + lim);
           if (a0 < a1) own[a0 - base] = static_cast<uint8_t>(lane * kLeavesPerRound + i);
           s0 = s1;
         }
@@ -454,50 +472,56 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       }
       __syncthreads();
       WR_STAMP(2)
-      // two pairs in flight per lane: pair j and j + 64 of the batch
-      for (int j = lane; j < lim; j += 128) {
-        const int j2 = j + 64;
-        const bool two = j2 < lim;
-        const int id1 = own[j], id2 = own[two ? j2 : j];
-        const int L1 = id1 / kLeavesPerRound, L2 = id2 / kLeavesPerRound;
-        const uint32_t ref1 = leaf_first[id1] + static_cast<uint32_t>(base + j - seg_start[L1] - leaf_off[id1]);
-        const uint32_t ref2 =
-            leaf_first[id2] + static_cast<uint32_t>(base + (two ? j2 : j) - seg_start[L2] - leaf_off[id2]);
-        const float2 cc1 = S.ref_c[ref1], cc2 = S.ref_c[ref2];
-        const float4 a1 = S.ref_a[ref1], a2 = S.ref_a[ref2];
-        const float4 b1 = S.ref_b[ref1], b2 = S.ref_b[ref2];
-        const float4 x1 = ray4[2 * L1], y1 = ray4[2 * L1 + 1], x2 = ray4[2 * L2], y2 = ray4[2 * L2 + 1];
-        const float rb1 = rbest[L1], rb2 = rbest[L2];
+      // kPairsInFlight pairs per lane per trip: j, j + 64, ... of the batch; all
+      // their records are requested before the first test.  A lane keeps the t
+      // of its own pairs (slot (j - lane) / 64) in registers.
+      float tv[kPairBatch / 64];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (u == 1 && !two) break;
-          const float4 x = u ? x2 : x1, y = u ? y2 : y1;
-          const float2 c = u ? cc2 : cc1;
-          const V3 ro = v3(x.x, x.y, x.z), rd = v3(x.w, y.x, y.y);
-          const int prim = __float_as_int(c.y);
-          float t = __int_as_float(0x7fc00000);  // NaN: no hit
-          float th;
-          bool h;
-          if (!SPH || prim >= 0) {
-            h = tri_test(u ? a2 : a1, u ? b2 : b1, c.x, ro, rd, y.z, y.w, u ? rb2 : rb1, th);
-          } else {
-            h = sph_hit(S, -prim - 1, ro, rd, y.z, y.w, th);
-          }
-          if (h) {  // t > EPS > 0: the order key is the float's bits
-            t = th;
+      for (int k = 0; k < kPairBatch / 64; ++k) tv[k] = __int_as_float(0x7fc00000);  // NaN: no hit
+#pragma unroll
+      for (int tr = 0; tr < kPairBatch / (64 * kPairsInFlight); ++tr) {
+        const int j0 = lane + 64 * kPairsInFlight * tr;
+        if (j0 >= lim) break;
+        uint32_t ref[kPairsInFlight];
+        int owner[kPairsInFlight];
+#pragma unroll
+        for (int u = 0; u < kPairsInFlight; ++u) {
+          const int j = min(j0 + 64 * u, lim - 1);
+          const int id = own[j];
+          owner[u] = id / kLeavesPerRound;
+          ref[u] = leaf_first[id] + static_cast<uint32_t>(base + j - static_cast<int>(leaf_off[id]));
+        }
+        float2 rc[kPairsInFlight];
+        float4 ra[kPairsInFlight], rb[kPairsInFlight];
+#pragma unroll
+        for (int u = 0; u < kPairsInFlight; ++u) {
+          rc[u] = S.ref_c[ref[u]];
+          ra[u] = S.ref_a[ref[u]];
+          rb[u] = S.ref_b[ref[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < kPairsInFlight; ++u) {
+          if (j0 + 64 * u >= lim) break;
+          const int L = owner[u];
+          const float4 x = ray4[2 * L], y = ray4[2 * L + 1];
+          const int prim = __float_as_int(rc[u].y);
+          const float t = pair_t(ra[u], rb[u], rc[u], v3(x.x, x.y, x.z), v3(x.w, y.x, y.y), y.z, y.w, rbest[L]);
+          if (t == t) {  // t > EPS > 0: the order key is the float's bits
             const unsigned long long key = static_cast<uint32_t>(__float_as_int(t));
             const unsigned long long pr = static_cast<uint32_t>((!SPH || prim >= 0) ? prim : -prim - 1);
-            atomicMin(olo + (u ? L2 : L1), (key << 32) | pr);
-            atomicMax(ohi + (u ? L2 : L1), ((0x7fffffffull - key) << 32) | pr);
+            atomicMin(olo + L, (key << 32) | pr);
+            atomicMax(ohi + L, ((0x7fffffffull - key) << 32) | pr);
           }
-          res[u ? j2 : j] = t;
+          tv[tr * kPairsInFlight + u] = t;
         }
       }
       __syncthreads();
       // flag owners with a hit in (min, min + 2 EPS]
-      for (int j = lane; j < lim; j += 64) {
-        const float t = res[j];
-        if (t == t) {
+#pragma unroll
+      for (int k = 0; k < kPairBatch / 64; ++k) {
+        const int j = lane + 64 * k;
+        const float t = tv[k];
+        if (j < lim && t == t) {
           const int L = own[j] / kLeavesPerRound;
           const float m = __int_as_float(static_cast<int>(olo[L] >> 32));
           if (t != m && t - m <= 2.f * WR_EPS) onear[L] = 1;
@@ -505,33 +529,36 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       }
       __syncthreads();
       WR_STAMP(3)
-      // first-found-wins (cmp(t - best) < 0, in leaf order).  The sequential rule
-      // keeps best within EPS of the minimum m once m is seen, and a repeat of a
-      // value already seen is never taken.  So when every hit within 2 EPS of m
-      // is exactly m on one primitive (a triangle met again in a later leaf of
-      // the round) and the incoming best is 2 EPS away from m either way, m
-      // decides the outcome; otherwise this owner replays its pairs in order.
+      // first-found-wins (cmp(t - best) < 0, in leaf order, :367).  With m the
+      // round's smallest hit (every hit t >= m, float rounding is monotone):
+      //  * cmp(m - best) >= 0: no hit of the round can be taken -- no change;
+      //  * else, if every other hit is more than 2 EPS above m and m is a single
+      //    primitive (repeats of a triangle met in two leaves give the same t),
+      //    m is taken when reached and nothing after it can replace it;
+      //  * otherwise (a near-tie between different primitives) this owner
+      //    replays its pairs in order, re-testing them (same inputs and screen
+      //    => the same t as above).
       if (act && k0 < k1) {
         const unsigned long long lo = olo[lane];
-        if (lo != ~0ull) {  // at least one hit
-          const float m = __int_as_float(static_cast<int>(lo >> 32));
+        const float m = __int_as_float(static_cast<int>(lo >> 32));
+        if (lo != ~0ull && cmpf(m - t_best) < 0) {
           const int pmin = static_cast<int>(lo & 0xffffffffull);
-          bool decided = onear[lane] == 0 && pmin == static_cast<int>(ohi[lane] & 0xffffffffull);
+          const bool decided = onear[lane] == 0 && pmin == static_cast<int>(ohi[lane] & 0xffffffffull);
           if (decided) {
-            if (t_best - m > 2.f * WR_EPS) {
-              t_best = m;
-              best = pmin;
-            } else if (!(m - t_best > 2.f * WR_EPS)) {
-              decided = false;
-            }
+            t_best = m;
+            best = pmin;
           }
           if (!decided) {
+            const float screen = rbest[lane];
+            const float rtmin = ray4[2 * lane + 1].z;
             for (int k = k0; k < k1; ++k) {
-              const float t = res[k - base];
+              const uint32_t ref = own_ref(k);
+              const float2 c = S.ref_c[ref];
+              const float t = pair_t(S.ref_a[ref], S.ref_b[ref], c, o, d, rtmin, rtmax, screen);
               if (t == t && cmpf(t - t_best) < 0) {
                 t_best = t;
-                const int c = __float_as_int(S.ref_c[own_ref(k - excl)].y);
-                best = (!SPH || c >= 0) ? c : -c - 1;
+                const int cp = __float_as_int(c.y);
+                best = (!SPH || cp >= 0) ? cp : -cp - 1;
               }
             }
           }
