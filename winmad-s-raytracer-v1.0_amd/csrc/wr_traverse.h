@@ -191,7 +191,11 @@ constexpr int kPairBatch = 256;
 #define WR_PAIRS_IN_FLIGHT 2
 #endif
 constexpr int kPairsInFlight = WR_PAIRS_IN_FLIGHT;     // (ray, triangle) records requested per lane per trip
-constexpr int kLeavesPerRound = WR_LEAVES_PER_ROUND;  // leaves a lane may collect per round
+constexpr int kLeavesPerRound = WR_LEAVES_PER_ROUND;
+#ifndef WR_RAY_GRAB
+#define WR_RAY_GRAB 64
+#endif
+constexpr int kRayGrab = WR_RAY_GRAB;  // queue indices a wave reserves per atomic (>= 64)  // leaves a lane may collect per round
 constexpr int kLeavesWait = WR_LEAVES_WAIT;           // the walk runs until every lane has this many
 __host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
   return size_t(depth) * 64 * (narrow ? 6 : 8) +
@@ -298,6 +302,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
   bool inb = false;      // the lane's ray comes from qb
   int r = -1;            // ray held by this lane (-1: none)
   bool pool = true;      // wave-uniform: queue not yet exhausted
+  int pb = 0, pe = 0;    // wave-uniform: reserved queue indices [pb, pe)
   bool more = false;     // the lane's ray has nodes left to visit
   V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
   float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmax = WR_INF, root_tmax = 0.f;
@@ -342,11 +347,22 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
       const bool idle = r < 0;
       const unsigned long long m = __ballot(idle);
       if (m) {
-        const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(fetch, __popcll(m));
-        base = __builtin_amdgcn_readlane(base, leader);
-        const int idx = base + __popcll(m & ((1ull << lane) - 1ull));
+        // queue indices come from the wave's reservation [pb, pe), topped up
+        // kRayGrab at a time (one global atomic per kRayGrab rays, not per refill)
+        const int need = __popcll(m);
+        const int rank = __popcll(m & ((1ull << lane) - 1ull));
+        int idx = pb + rank;
+        if (pe - pb < need) {
+          int got = 0;
+          if (lane == 0) got = atomicAdd(fetch, kRayGrab);
+          got = __builtin_amdgcn_readlane(got, 0);
+          const int rem = pe - pb;
+          if (rank >= rem) idx = got + (rank - rem);
+          pb = got + (need - rem);
+          pe = got + kRayGrab;
+        } else {
+          pb += need;
+        }
         if (idle && idx < n) {
           inb = idx >= na;
           const RayQueue& q = inb ? qb : qa;
