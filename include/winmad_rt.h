@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define WR_API_VERSION 1
+#define WR_API_VERSION 2
 
 enum {
   WR_OK = 0,
@@ -104,6 +104,8 @@ typedef struct {
   double seconds;            /* host wall time of the call (stream synced)  */
   double kernel_ms[WR_K_NUM];      /* time_kernels only: summed launch durations */
   int64_t kernel_launches[WR_K_NUM];
+  double trace_wall_ms;      /* time_kernels only: union of the traversal launch
+                                intervals over all pipelines (launches overlap) */
 } wr_stats;
 
 /* ---- scene (Scene::init, scene/scene.cpp:469-489 + loadScene :259-467) ---- */
@@ -117,6 +119,11 @@ void wr_scene_free(wr_scene* scene);
 int wr_device_count(void);
 int wr_create(const wr_scene* scene, int hip_device, wr_context** out);
 void wr_destroy(wr_context* ctx);
+/* Concurrent render pipelines (HIP streams, each with its own work buffers):
+ * iterations / samples are dealt round-robin to them so that one stream's
+ * late-bounce traversal tail overlaps another's full launches.  1..4, default
+ * 3 (env WR_PIPES).  GPU-specific scheduling; no reference counterpart. */
+int wr_set_pipelines(wr_context* ctx, int n);
 
 /* ---- traversal ---- */
 /* Scene::intersect (scene/scene.cpp:21-43) -> KDtreeAccel::traverse

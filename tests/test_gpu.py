@@ -204,3 +204,26 @@ def test_trace_1m_triangle_scene_matches_oracle(tmp_path):
     rays = np.zeros((n, 9), np.float32)
     rays[:, 0:3], rays[:, 3:6] = o, d
     assert _check_trace_vs_oracle(c, _oracle.Scene(path), rays) > n // 4
+
+
+@pytest.mark.parametrize("pipes", [1, 3, 4])
+def test_pipeline_count_does_not_change_the_render(pipes):
+    """Iterations / samples dealt to 1..4 concurrent streams: same rays, same film
+    up to the order of float atomics."""
+    path = _scenes.torus(96, 64)
+    s = native.Scene(path)
+    c = native.Context(s, 0)
+    c.set_pipelines(2)
+    ref, rs = c.render_bdpt(96, 64, iterations=5, seed=21)
+    c.set_pipelines(pipes)
+    got, gs = c.render_bdpt(96, 64, iterations=5, seed=21)
+    assert gs.closest_rays == rs.closest_rays and gs.shadow_rays == rs.shadow_rays
+    assert np.allclose(got, ref, rtol=1e-4, atol=1e-6)
+    cb = native.Context(native.Scene(_scenes.cbox(64, 48)), 0)
+    cb.set_pipelines(1)
+    pref, _ = cb.render_path(64, 48, spp=9, seed=4)
+    cb.set_pipelines(pipes)
+    pgot, _ = cb.render_path(64, 48, spp=9, seed=4)
+    assert np.allclose(pgot, pref, rtol=1e-4, atol=1e-6)
+    with pytest.raises(native.WrError):
+        c.set_pipelines(0)

@@ -980,29 +980,46 @@ size_t measure(Fn fn) {  // bytes an arena layout needs
 }
 }  // namespace
 
-struct wr_context {
-  int device = 0;
+// One render pipeline: a HIP stream with its own work buffers and queue
+// counters.  Iterations (BDPT) / samples (PT) are dealt round-robin to the
+// context's pipelines, so the long tail of one stream's late-bounce traversal
+// launches (a launch lasts as long as its slowest ray) overlaps the full
+// launches of another.  The film is a sum, so the result does not depend on the
+// pipeline count (up to the order of float atomics).
+constexpr int kMaxPipes = 4;
+struct Pipe {
   hipStream_t stream = nullptr;
-  DevScene ds{};
-  Arena scene_mem;
-  int64_t scene_bytes = 0;
+  DevCounters* ctr = nullptr;
   Arena work;
   size_t work_key = 0;  // P for which `work` is laid out
   int work_kind = 0;    // 1 bdpt, 2 pt
   BdptBuf bb{};
   PtBuf pb{};
-  DevCounters* ctr = nullptr;
+  std::vector<hipEvent_t> events;  // Timer marks (time_kernels)
+  std::vector<int> ev_cat;
+  size_t ev_used = 0;
+  hipEvent_t done = nullptr;
+};
+
+struct wr_context {
+  int device = 0;
+  hipStream_t stream = nullptr;  // API traversal, film set-up / return, joins the pipelines
+  Pipe pipes[kMaxPipes];
+  int npipes = 3;  // measured on MI355X, torus 1080p BDPT: 1 -> 350, 2 -> 522, 3 -> 575, 4 -> 506 Mrays/s
+  hipEvent_t t_ref = nullptr;  // start of the current render (pipelines wait on it)
+  DevScene ds{};
+  Arena scene_mem;
+  int64_t scene_bytes = 0;
+  DevCounters* ctr = nullptr;  // API traversal
   float* film_tmp = nullptr;
   size_t film_tmp_n = 0;
   int grid = 2048;
   int cus = 256;
   bool spheres = false;
   bool narrow = false;  // <= 65536 nodes, leaves <= 255 refs: 16-bit stack / pair offsets
+  bool trace_log = false;  // WR_TRACE_LOG=1: per-launch ray counts and durations
   bool stamps = false;  // WR_TRACE_STAMPS=1: diagnostic traversal with phase stamps
   int trace_blocks = 4096;  // resident one-wave workgroups of the traversal
-  std::vector<hipEvent_t> events;
-  size_t ev_used = 0;
-  int ev_cat[4096];
   bool timing = false;
 };
 
@@ -1097,32 +1114,35 @@ void layout_pt(Arena& a, PtBuf& T, int P) {
   T.s_prim = a.take<int>(sP);
 }
 
-int ensure_work(wr_context* c, int kind, int P) {
-  if (c->work_kind == kind && c->work_key == static_cast<size_t>(P)) return WR_OK;
+int ensure_work(Pipe& p, int kind, int P) {
+  if (p.work_kind == kind && p.work_key == static_cast<size_t>(P)) return WR_OK;
+  p.work_kind = 0;
   size_t bytes = kind == 1 ? measure([&](Arena& a) { BdptBuf b; layout_bdpt(a, b, P); })
                            : measure([&](Arena& a) { PtBuf t; layout_pt(a, t, P); });
-  int rc = c->work.reserve(bytes);
+  int rc = p.work.reserve(bytes);
   if (rc) return rc;
-  if (kind == 1) layout_bdpt(c->work, c->bb, P);
-  else layout_pt(c->work, c->pb, P);
-  c->work_kind = kind;
-  c->work_key = P;
+  if (kind == 1) layout_bdpt(p.work, p.bb, P);
+  else layout_pt(p.work, p.pb, P);
+  p.work_kind = kind;
+  p.work_key = P;
   return WR_OK;
 }
 
-// ---- launch helpers with optional per-launch HIP events (context stream)
+// ---- launch helpers with optional per-launch HIP events (on the pipeline's stream)
 struct Timer {
   wr_context* c;
-  explicit Timer(wr_context* cc) : c(cc) {}
+  Pipe* p;
+  Timer(wr_context* cc, Pipe* pp) : c(cc), p(pp) {}
   void mark(int cat) {
-    if (!c->timing) return;
-    if (c->ev_used >= c->events.size()) {
+    if (!c->timing || !p) return;
+    if (p->ev_used >= p->events.size()) {
       hipEvent_t e;
       (void)hipEventCreate(&e);
-      c->events.push_back(e);
+      p->events.push_back(e);
+      p->ev_cat.push_back(0);
     }
-    if (c->ev_used < 4096) c->ev_cat[c->ev_used] = cat;
-    (void)hipEventRecord(c->events[c->ev_used++], c->stream);
+    p->ev_cat[p->ev_used] = cat;
+    (void)hipEventRecord(p->events[p->ev_used++], p->stream);
   }
 };
 
@@ -1144,58 +1164,124 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps) {
 }
 
 // One persistent traversal launch over qa then qb (max_rays bounds the grid).
-int trace_launch(wr_context* c, Timer& tm, bool count, const RayQueue& qa, const RayQueue& qb, int max_rays) {
+int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, Timer& tm, bool count, const RayQueue& qa,
+                 const RayQueue& qb, int max_rays) {
   const size_t lds = trace_lds_bytes(c->ds.max_stack, c->narrow);
   const int grid = std::max(1, std::min(c->trace_blocks, (max_rays + kTraceBlock - 1) / kTraceBlock));
-  (void)hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream);
+  (void)hipMemsetAsync(&ctr->fetch, 0, sizeof(int), stream);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->trace_log) {  // diagnostic (WR_TRACE_LOG=1): rays and duration of every launch
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, stream);
+  }
   hipLaunchKernelGGL(trace_kernel(count, c->spheres, c->narrow, c->stamps), dim3(grid), dim3(kTraceBlock), lds,
-                     c->stream, c->ds, qa, qb, c->ctr);
+                     stream, c->ds, qa, qb, ctr);
   tm.mark(WR_K_TRACE);
+  if (c->trace_log) {
+    (void)hipEventRecord(e1, stream);
+    (void)hipEventSynchronize(e1);
+    int na = 0, nb = 0;
+    if (qa.count) (void)hipMemcpy(&na, qa.count, sizeof(int), hipMemcpyDeviceToHost);
+    if (qb.count) (void)hipMemcpy(&nb, qb.count, sizeof(int), hipMemcpyDeviceToHost);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    std::fprintf(stderr, "[wr trace] rays %d + %d  %.1f us  grid %d\n", na, nb, ms * 1e3f, grid);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
   return WR_OK;
 }
 
 int shade_grid(wr_context* c, int n) { return std::max(1, std::min(c->grid, (n + kShadeBlock - 1) / kShadeBlock)); }
 
-void begin_stats(wr_context* c, const int time_kernels) {
-  c->timing = time_kernels != 0;
-  c->ev_used = 0;
+double host_now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int finish_stats(wr_context* c, wr_stats* st, double t0_host) {
+// Start a render on `n` pipelines: they wait for the context stream's set-up
+// (film clear) and clear their counters.
+void begin_render(wr_context* c, int n, const int time_kernels) {
+  c->timing = time_kernels != 0;
+  (void)hipEventRecord(c->t_ref, c->stream);
+  for (int i = 0; i < n; ++i) {
+    Pipe& p = c->pipes[i];
+    p.ev_used = 0;
+    (void)hipStreamWaitEvent(p.stream, c->t_ref, 0);
+    (void)hipMemsetAsync(p.ctr, 0, sizeof(DevCounters), p.stream);
+    Timer(c, &p).mark(WR_K_OTHER);
+  }
+}
+
+// Join the pipelines into the context stream, wait, and add up the work
+// counters and (time_kernels) the per-launch durations of every pipeline.
+// stats->trace_wall_ms is the union of all traversal launch intervals.
+int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
+  for (int i = 0; i < n; ++i) {
+    (void)hipEventRecord(c->pipes[i].done, c->pipes[i].stream);
+    (void)hipStreamWaitEvent(c->stream, c->pipes[i].done, 0);
+  }
   HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipGetLastError());
   if (!st) return WR_OK;
-  DevCounters h;
-  HIPCHK(hipMemcpy(&h, c->ctr, sizeof h, hipMemcpyDeviceToHost));
-  st->closest_rays += static_cast<int64_t>(h.closest);
-  st->shadow_rays += static_cast<int64_t>(h.shadow);
-  st->inner_visits += static_cast<int64_t>(h.inner);
-  st->leaf_visits += static_cast<int64_t>(h.leaves);
-  st->prim_refs += static_cast<int64_t>(h.refs);
+  DevCounters sum{};
+  for (int i = 0; i < n; ++i) {
+    DevCounters h;
+    HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
+    sum.closest += h.closest;
+    sum.shadow += h.shadow;
+    sum.inner += h.inner;
+    sum.leaves += h.leaves;
+    sum.refs += h.refs;
+    for (int k = 0; k < 8; ++k) sum.stamps[k] += h.stamps[k];
+  }
+  st->closest_rays += static_cast<int64_t>(sum.closest);
+  st->shadow_rays += static_cast<int64_t>(sum.shadow);
+  st->inner_visits += static_cast<int64_t>(sum.inner);
+  st->leaf_visits += static_cast<int64_t>(sum.leaves);
+  st->prim_refs += static_cast<int64_t>(sum.refs);
   if (c->stamps) {
-    static const char* names[6] = {"refill", "descend", "leaf-setup", "pair-tests", "owner-scan", "pop"};
+    static const char* names[6] = {"refill", "walk", "leaf-setup", "pair-tests", "decision", "write"};
     double tot = 0;
-    for (int k = 0; k < 6; ++k) tot += static_cast<double>(h.stamps[k]);
+    for (int k = 0; k < 6; ++k) tot += static_cast<double>(sum.stamps[k]);
     std::fprintf(stderr, "[wr stamps]");
-    for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %s=%.1f%%", names[k], 100.0 * h.stamps[k] / std::max(1.0, tot));
+    for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %s=%.1f%%", names[k], 100.0 * sum.stamps[k] / std::max(1.0, tot));
     std::fprintf(stderr, " (wave-cycles %.3g)\n", tot);
   }
-  const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-  st->seconds += t1 - t0_host;
+  st->seconds += host_now() - t0_host;
   if (c->timing) {
-    for (size_t i = 1; i < c->ev_used; ++i) {
-      float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, c->events[i - 1], c->events[i]);
-      const int cat = i < 4096 ? c->ev_cat[i] : WR_K_OTHER;
-      st->kernel_ms[cat] += ms;
-      st->kernel_launches[cat] += 1;
+    std::vector<std::pair<float, float>> spans;  // traversal launches, ms from t_ref
+    for (int i = 0; i < n; ++i) {
+      const Pipe& p = c->pipes[i];
+      float prev = 0.f;
+      (void)hipEventElapsedTime(&prev, c->t_ref, p.events[0]);
+      for (size_t k = 1; k < p.ev_used; ++k) {
+        float at = 0.f;
+        (void)hipEventElapsedTime(&at, c->t_ref, p.events[k]);
+        const int cat = p.ev_cat[k];
+        st->kernel_ms[cat] += at - prev;
+        st->kernel_launches[cat] += 1;
+        if (cat == WR_K_TRACE) spans.emplace_back(prev, at);
+        prev = at;
+      }
     }
+    std::sort(spans.begin(), spans.end());
+    double wall = 0.0, lo = 0.0, hi = -1.0;
+    for (const auto& sp : spans) {
+      if (sp.first > hi) {
+        if (hi > lo) wall += hi - lo;
+        lo = sp.first;
+        hi = sp.second;
+      } else {
+        hi = std::max<double>(hi, sp.second);
+      }
+    }
+    if (hi > lo) wall += hi - lo;
+    st->trace_wall_ms += wall;
   }
   return WR_OK;
 }
 
-double host_now() {
-  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 int check_device() {
   int n = 0;
@@ -1274,10 +1360,20 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   HIPCHK(hipSetDevice(device));
   auto* c = new wr_context();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->t_ref, hipEventDefault) != hipSuccess) {
+    wr_destroy(c);
     return fail(WR_E_HIP, "hipStreamCreate failed");
   }
+  for (Pipe& pp : c->pipes) {
+    if (hipStreamCreateWithFlags(&pp.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&pp.done, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&pp.ctr, sizeof(DevCounters)) != hipSuccess) {
+      wr_destroy(c);
+      return fail(WR_E_HIP, "pipeline stream / counters");
+    }
+  }
+  if (const char* e = std::getenv("WR_PIPES")) c->npipes = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->grid = std::max(256, prop.multiProcessorCount * 8);
 
@@ -1419,6 +1515,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   c->scene_bytes = static_cast<int64_t>(A.used);
   for (const auto& p : s.prims) c->spheres |= p.type != wr::kTri;
   if (const char* e = std::getenv("WR_TRACE_STAMPS")) c->stamps = std::atoi(e) != 0 && !c->spheres;
+  if (const char* e = std::getenv("WR_TRACE_LOG")) c->trace_log = std::atoi(e) != 0;
   {
     // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
     // and registers); more would only queue behind the first wave of blocks
@@ -1443,13 +1540,26 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   return WR_OK;
 }
 
+int wr_set_pipelines(wr_context* c, int n) {
+  if (!c || n < 1 || n > kMaxPipes) return fail(WR_E_ARG, "pipelines must be in 1..4");
+  c->npipes = n;
+  return WR_OK;
+}
+
 void wr_destroy(wr_context* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+  for (Pipe& p : c->pipes) {
+    if (p.stream) (void)hipStreamSynchronize(p.stream);
+    for (hipEvent_t e : p.events) (void)hipEventDestroy(e);
+    if (p.done) (void)hipEventDestroy(p.done);
+    if (p.ctr) (void)hipFree(p.ctr);
+    p.work.release();
+    if (p.stream) (void)hipStreamDestroy(p.stream);
+  }
+  if (c->t_ref) (void)hipEventDestroy(c->t_ref);
   if (c->film_tmp) (void)hipFree(c->film_tmp);
-  c->work.release();
   c->scene_mem.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1486,8 +1596,8 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   const int g = std::max(1, std::min(c->grid, (n + 255) / 256));
   hipLaunchKernelGGL(k_api_prep, dim3(g), dim3(256), 0, c->stream, dr, n, occ ? 1 : 0, o3, d3, tmn, tmx);
   c->timing = false;
-  Timer tm(c);
-  trace_launch(c, tm, false, rq(o3, d3, n, cnt, tt, pr, tmn, tmx), kNoQueue, n);
+  Timer tm(c, nullptr);
+  trace_launch(c, c->stream, c->ctr, tm, false, rq(o3, d3, n, cnt, tt, pr, tmn, tmx), kNoQueue, n);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
   HIPCHK(hipGetLastError());
@@ -1545,18 +1655,15 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
   HIPCHK(hipSetDevice(c->device));
   const double t0 = host_now();
   const int P = prm->width * prm->height;
-  if (int rc = ensure_work(c, 1, P)) return rc;
+  const int np = std::max(1, std::min(c->npipes, prm->iterations));
+  for (int i = 0; i < np; ++i)
+    if (int rc = ensure_work(c->pipes[i], 1, P)) return rc;
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
-  HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(DevCounters), c->stream));
-  begin_stats(c, prm->time_kernels);
-  Timer tm(c);
-  tm.mark(WR_K_OTHER);
+  begin_render(c, np, prm->time_kernels);
   BdptArgs A;
   A.S = c->ds;
-  A.B = c->bb;
-  A.ctr = c->ctr;
   A.film = dfilm;
   A.W = prm->width;
   A.H = prm->height;
@@ -1566,50 +1673,57 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
   A.maxlen = prm->max_path_length > 0 ? prm->max_path_length : 10;
   A.faithful = prm->faithful;
   const bool count = prm->count_work != 0;
-  const BdptBuf& B = c->bb;
-  int* ext_cnt = &c->ctr->ext_count[0];
-  int* sq_cnt = &c->ctr->sq_count;
   const int g = shade_grid(c, P);
-  const RayQueue sq = rq(B.s_o, B.s_d, B.cap_sq, sq_cnt, B.s_t, B.s_prim);
-  auto ext = [&](int q) { return rq(B.q_o[q], B.q_d[q], P, ext_cnt + q, B.q_t[q], B.q_prim[q]); };
-  const int sq_max = B.cap_sq;
   for (int it = 0; it < prm->iterations; ++it) {
+    Pipe& pp = c->pipes[it % np];
+    const hipStream_t sm = pp.stream;
+    Timer tm(c, &pp);
+    const BdptBuf& B = pp.bb;
+    A.B = pp.bb;
+    A.ctr = pp.ctr;
     A.iter = static_cast<uint32_t>(prm->iter_begin + it);
+    int* ext_cnt = &pp.ctr->ext_count[0];
+    int* sq_cnt = &pp.ctr->sq_count;
+    const RayQueue sq = rq(B.s_o, B.s_d, B.cap_sq, sq_cnt, B.s_t, B.s_prim);
+    auto ext = [&](int q) { return rq(B.q_o[q], B.q_d[q], P, ext_cnt + q, B.q_t[q], B.q_prim[q]); };
+    const int sq_max = B.cap_sq;
     // ---------------- light pass (:67-131)
-    HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), c->stream));
-    hipLaunchKernelGGL(k_light_gen, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+    HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), sm));
+    HIPCHK(hipMemsetAsync(ext_cnt, 0, sizeof(int), sm));
+    hipLaunchKernelGGL(k_light_gen, dim3(g), dim3(kShadeBlock), 0, sm, A);
     tm.mark(WR_K_GEN);
     int cur = 0;
     for (int b = 0; b < A.maxlen - 1; ++b) {
-      trace_launch(c, tm, count, ext(cur), kNoQueue, P);
-      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), c->stream));
-      hipLaunchKernelGGL(k_light_shade, dim3(g), dim3(kShadeBlock), 0, c->stream, A, cur);
+      trace_launch(c, sm, pp.ctr, tm, count, ext(cur), kNoQueue, P);
+      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), sm));
+      hipLaunchKernelGGL(k_light_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, cur);
       tm.mark(WR_K_SHADE);
       cur ^= 1;
     }
     // ---------------- camera pass (:133-264).  The light pass's splat rays
     // (connectToCamera) ride along with the primary rays; afterwards each
     // bounce's shadow / aux rays ride along with the next bounce's extension rays.
-    hipLaunchKernelGGL(k_camera_gen, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+    HIPCHK(hipMemsetAsync(ext_cnt, 0, sizeof(int), sm));
+    hipLaunchKernelGGL(k_camera_gen, dim3(g), dim3(kShadeBlock), 0, sm, A);
     tm.mark(WR_K_GEN);
     cur = 0;
     for (int b = 0; b <= A.maxlen; ++b) {
       const bool more = b < A.maxlen;  // extension rays of bounce b exist
-      trace_launch(c, tm, count, sq, more ? ext(cur) : kNoQueue, (more ? P : 0) + sq_max);
-      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max)), dim3(kShadeBlock), 0, c->stream, A);
-      if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+      trace_launch(c, sm, pp.ctr, tm, count, sq, more ? ext(cur) : kNoQueue, (more ? P : 0) + sq_max);
+      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max)), dim3(kShadeBlock), 0, sm, A);
+      if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, sm, A);
       tm.mark(WR_K_RESOLVE);
       if (!more) break;
-      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), c->stream));  // next extension queue
-      HIPCHK(hipMemsetAsync(sq_cnt, 0, 2 * sizeof(int), c->stream));           // sq_count, di_count
-      hipLaunchKernelGGL(k_camera_shade, dim3(g), dim3(kShadeBlock), 0, c->stream, A, cur);
+      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), sm));  // next extension queue
+      HIPCHK(hipMemsetAsync(sq_cnt, 0, 2 * sizeof(int), sm));           // sq_count, di_count
+      hipLaunchKernelGGL(k_camera_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, cur);
       tm.mark(WR_K_SHADE);
       cur ^= 1;
     }
   }
   HIPCHK(hipGetLastError());
-  if (int rc = film_return(c, film, film_on_device, nf)) return rc;
-  return finish_stats(c, st, t0);
+  if (int rc = finish_render(c, np, st, t0)) return rc;
+  return film_return(c, film, film_on_device, nf);
 }
 
 int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int film_on_device, wr_stats* st) {
@@ -1619,18 +1733,17 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
   HIPCHK(hipSetDevice(c->device));
   const double t0 = host_now();
   const int P = prm->width * prm->height;
-  if (int rc = ensure_work(c, 2, P)) return rc;
+  const int k0 = prm->sample_begin;
+  const int k1 = prm->sample_count > 0 ? k0 + prm->sample_count : prm->spp;
+  const int np = std::max(1, std::min(c->npipes, k1 - k0));
+  for (int i = 0; i < np; ++i)
+    if (int rc = ensure_work(c->pipes[i], 2, P)) return rc;
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
-  HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(DevCounters), c->stream));
-  begin_stats(c, prm->time_kernels);
-  Timer tm(c);
-  tm.mark(WR_K_OTHER);
+  begin_render(c, np, prm->time_kernels);
   PtArgs A;
   A.S = c->ds;
-  A.T = c->pb;
-  A.ctr = c->ctr;
   A.film = dfilm;
   A.W = prm->width;
   A.H = prm->height;
@@ -1640,37 +1753,41 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
   A.max_depth = prm->max_depth;
   A.seed = prm->seed;
   const bool count = prm->count_work != 0;
-  const PtBuf& T = c->pb;
-  int* ext_cnt = &c->ctr->ext_count[0];
-  int* sq_cnt = &c->ctr->sq_count;
   const int g = shade_grid(c, P);
-  const int k0 = prm->sample_begin;
-  const int k1 = prm->sample_count > 0 ? k0 + prm->sample_count : prm->spp;
   for (int k = k0; k < k1; ++k) {
+    Pipe& pp = c->pipes[(k - k0) % np];
+    const hipStream_t sm = pp.stream;
+    Timer tm(c, &pp);
+    const PtBuf& T = pp.pb;
+    A.T = pp.pb;
+    A.ctr = pp.ctr;
     A.k = static_cast<uint32_t>(k);
-    hipLaunchKernelGGL(k_pt_gen, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+    int* ext_cnt = &pp.ctr->ext_count[0];
+    int* sq_cnt = &pp.ctr->sq_count;
+    HIPCHK(hipMemsetAsync(ext_cnt, 0, sizeof(int), sm));
+    hipLaunchKernelGGL(k_pt_gen, dim3(g), dim3(kShadeBlock), 0, sm, A);
     tm.mark(WR_K_GEN);
     int cur = 0;
-    HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), c->stream));
+    HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), sm));
     for (int b = 0; b <= A.max_depth + 1; ++b) {
       // NEE shadow rays of the previous vertex ride along with this bounce's rays
       const bool more = b <= A.max_depth;
-      trace_launch(c, tm, count, rq(T.s_o, T.s_d, P, sq_cnt, T.s_t, T.s_prim),
+      trace_launch(c, sm, pp.ctr, tm, count, rq(T.s_o, T.s_d, P, sq_cnt, T.s_t, T.s_prim),
                    more ? rq(T.q_o[cur], T.q_d[cur], P, ext_cnt + cur, T.q_t[cur], T.q_prim[cur]) : kNoQueue,
                    2 * P);
-      hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, c->stream, A);
+      hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, sm, A);
       tm.mark(WR_K_RESOLVE);
       if (!more) break;
-      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), c->stream));
-      HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), c->stream));
-      hipLaunchKernelGGL(k_pt_shade, dim3(g), dim3(kShadeBlock), 0, c->stream, A, cur);
+      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), sm));
+      HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), sm));
+      hipLaunchKernelGGL(k_pt_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, cur);
       tm.mark(WR_K_SHADE);
       cur ^= 1;
     }
   }
   HIPCHK(hipGetLastError());
-  if (int rc = film_return(c, film, film_on_device, nf)) return rc;
-  return finish_stats(c, st, t0);
+  if (int rc = finish_render(c, np, st, t0)) return rc;
+  return film_return(c, film, film_on_device, nf);
 }
 
 int wr_film_write_ppm(const float* film, int height, int width, float scale, float gamma, int transpose,

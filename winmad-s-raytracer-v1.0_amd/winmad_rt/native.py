@@ -18,7 +18,7 @@ K_TRACE, K_SHADE, K_RESOLVE, K_GEN, K_OTHER = 0, 1, 2, 3, 4
 
 # every entry point declared in include/winmad_rt.h
 EXPORTS = ["wr_scene_load", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free", "wr_device_count",
-           "wr_create", "wr_destroy", "wr_trace_closest", "wr_occluded", "wr_render_bdpt", "wr_render_path",
+           "wr_create", "wr_destroy", "wr_set_pipelines", "wr_trace_closest", "wr_occluded", "wr_render_bdpt", "wr_render_path",
            "wr_film_write_ppm", "wr_last_error", "wr_api_version"]
 
 
@@ -55,7 +55,7 @@ class WrPathParams(C.Structure):
 class WrStats(C.Structure):
     _fields_ = [("closest_rays", C.c_int64), ("shadow_rays", C.c_int64), ("inner_visits", C.c_int64),
                 ("leaf_visits", C.c_int64), ("prim_refs", C.c_int64), ("seconds", C.c_double),
-                ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8)]
+                ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8), ("trace_wall_ms", C.c_double)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
@@ -104,6 +104,7 @@ def lib():
         L.wr_create.argtypes = [P, I, C.POINTER(P)]
         L.wr_destroy.argtypes = [P]
         L.wr_destroy.restype = None
+        L.wr_set_pipelines.argtypes = [P, I]
         L.wr_trace_closest.argtypes = [P, C.POINTER(WrRay), I64, C.POINTER(WrHit)]
         L.wr_occluded.argtypes = [P, C.POINTER(WrRay), C.POINTER(C.c_float), I64, C.POINTER(C.c_uint8)]
         L.wr_render_bdpt.argtypes = [P, C.POINTER(WrBdptParams), P, I, C.POINTER(WrStats)]
@@ -168,6 +169,10 @@ class Context:
         check(lib().wr_create(scene.h, device, C.byref(h)))
         self.h = h
         self.scene = scene
+
+    def set_pipelines(self, n):
+        """Concurrent render pipelines (streams) for render_bdpt / render_path."""
+        check(lib().wr_set_pipelines(self.h, n))
 
     def close(self):
         if getattr(self, "h", None):
