@@ -51,11 +51,19 @@ constexpr int kShadeBlock = 256;
 enum SqKind { SQ_SPLAT = 0, SQ_CONN = 1, SQ_NEE = 2, SQ_DIB = 3 };
 enum DiFlag { DI_NEE = 1, DI_BSDF = 2, DI_EARLY = 4 };
 
+// Queue counters of one iteration / sample, one slot per step, cleared by a
+// single memset at its start (no per-bounce counter resets).  BDPT: light
+// bounce b uses slot b, camera bounce b slot kCamSlot + b; PT bounce b slot b.
+constexpr int kSlots = 64;
+constexpr int kCamSlot = 16;
+struct StepCounters {
+  int ext[kSlots];    // extension rays entering step `slot`
+  int sq[kSlots];     // shadow / aux rays traced at step `slot` (light splats: slot 0 -> camera bounce 0)
+  int di[kSlots];     // DI records finalized at step `slot`
+  int fetch[kSlots];  // persistent-traversal cursor of the step's trace launch
+};
 struct DevCounters {
-  int ext_count[2];
-  int sq_count;
-  int di_count;
-  int fetch;  // persistent-traversal queue cursor (reset before every trace launch)
+  StepCounters step;
   unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
   unsigned long long closest, shadow, inner, leaves, refs;
 };
@@ -105,10 +113,11 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 // =============================================================== trace kernels
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
 template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
-__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, RayQueue qa, RayQueue qb, DevCounters* ctr) {
+__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, RayQueue qa, RayQueue qb, DevCounters* ctr,
+                                                      int* fetch) {
   extern __shared__ uint32_t smem[];
   TraceCounters tc{0, 0, 0};
-  trace_queue<COUNT, SPH, NARROW, STAMP>(S, qa, qb, &ctr->fetch, smem, tc, ctr->stamps);
+  trace_queue<COUNT, SPH, NARROW, STAMP>(S, qa, qb, fetch, smem, tc, ctr->stamps);
   if (COUNT) {
     unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs);
     if (lane_id() == 0) {
@@ -239,7 +248,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_light_gen(BdptArgs A) {
     st3(B.q_d[0], P, p, normalize(dir));
     B.q_path[0][p] = p;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->ext_count[0] = P;
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->step.ext[0] = P;
 }
 
 // sampleScattering (:370-416).  Returns false when the subpath ends.
@@ -271,11 +280,11 @@ __device__ __forceinline__ bool sample_scatter(const DevScene& S, Rng& rng, cons
 }
 
 // One light-subpath vertex (:77-128)
-__global__ void __launch_bounds__(kShadeBlock) k_light_shade(BdptArgs A, int cur) {
+__global__ void __launch_bounds__(kShadeBlock) k_light_shade(BdptArgs A, int slot) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
-  const int P = A.P, nxt = cur ^ 1;
-  const int n = A.ctr->ext_count[cur];
+  const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
+  const int n = A.ctr->step.ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;  // whole waves reach the appends
@@ -370,13 +379,13 @@ __global__ void __launch_bounds__(kShadeBlock) k_light_shade(BdptArgs A, int cur
         }
       }
     }
-    const int ei = wave_append(&A.ctr->ext_count[nxt], ext);
+    const int ei = wave_append(&A.ctr->step.ext[slot + 1], ext);
     if (ext) {
       st3(B.q_o[nxt], P, ei, e_o);
       st3(B.q_d[nxt], P, ei, e_d);
       B.q_path[nxt][ei] = p;
     }
-    const int si = wave_append(&A.ctr->sq_count, splat);
+    const int si = wave_append(&A.ctr->step.sq[kCamSlot], splat);  // traced with the camera primaries
     if (splat) {
       st3(B.s_o, B.cap_sq, si, s_o);
       st3(B.s_d, B.cap_sq, si, s_d);
@@ -429,16 +438,16 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptArgs A) {
     st3(B.q_d[0], P, s, normalize(d));
     B.q_path[0][s] = p;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->ext_count[0] = P;
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->step.ext[kCamSlot] = P;
 }
 
 // One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
 // connections (shadow rays queued), scattering.
-__global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int cur) {
+__global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int slot) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
-  const int P = A.P, nxt = cur ^ 1, cap = B.cap_sq;
-  const int n = A.ctr->ext_count[cur];
+  const int P = A.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;
+  const int n = A.ctr->step.ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
@@ -579,9 +588,9 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int cu
     }
     // DI queue entries
     {
-      const int di_i = wave_append(&A.ctr->di_count, di);
+      const int di_i = wave_append(&A.ctr->step.di[slot + 1], di);
       if (di) B.di_list[di_i] = p;
-      const int ni = wave_append(&A.ctr->sq_count, nee);
+      const int ni = wave_append(&A.ctr->step.sq[slot + 1], nee);
       if (nee) {
         st3(B.s_o, cap, ni, hp);
         st3(B.s_d, cap, ni, nee_d);
@@ -589,7 +598,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int cu
         B.s_meta[ni] = (SQ_NEE << 30) | p;
         B.s_pix[ni] = pix;
       }
-      const int bi = wave_append(&A.ctr->sq_count, dib);
+      const int bi = wave_append(&A.ctr->step.sq[slot + 1], dib);
       if (dib) {
         st3(B.s_o, cap, bi, dib_o);
         st3(B.s_d, cap, bi, dib_d);
@@ -658,7 +667,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int cu
             }
           }
         }
-        const int si = wave_append(&A.ctr->sq_count, shoot);
+        const int si = wave_append(&A.ctr->step.sq[slot + 1], shoot);
         if (shoot) {
           st3(B.s_o, cap, si, hp);
           st3(B.s_d, cap, si, sdir);
@@ -678,7 +687,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int cu
         B.c_len[p] = len + 1;
       }
     }
-    const int ei = wave_append(&A.ctr->ext_count[nxt], ext);
+    const int ei = wave_append(&A.ctr->step.ext[slot + 1], ext);
     if (ext) {
       st3(B.q_o[nxt], P, ei, e_o);
       st3(B.q_d[nxt], P, ei, e_d);
@@ -688,10 +697,10 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int cu
 }
 
 // Light-tracing splats and camera-pass shadow / aux rays after traversal.
-__global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptArgs A) {
+__global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptArgs A, int slot) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
-  const int n = A.ctr->sq_count, cap = B.cap_sq;
+  const int n = A.ctr->step.sq[slot], cap = B.cap_sq;
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
@@ -729,9 +738,9 @@ __global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptArgs A) {
 }
 
 // getDirectIllumination's final combination (:533-607)
-__global__ void __launch_bounds__(kShadeBlock) k_di_finalize(BdptArgs A) {
+__global__ void __launch_bounds__(kShadeBlock) k_di_finalize(BdptArgs A, int slot) {
   const BdptBuf& B = A.B;
-  const int n = A.ctr->di_count, P = A.P;
+  const int n = A.ctr->step.di[slot], P = A.P;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
     const int p = B.di_list[j];
     const int flags = B.di_flags[p];
@@ -798,15 +807,15 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_gen(PtArgs A) {
     st3(T.q_d[0], P, p, d);
     T.q_path[0][p] = p;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->ext_count[0] = P;
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->step.ext[0] = P;
 }
 
 // One PathIntegrator::raytracing iteration (pathIntegrator.cpp:43-146)
-__global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int cur) {
+__global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int slot) {
   const PtBuf& T = A.T;
   const DevScene& S = A.S;
-  const int P = A.P, nxt = cur ^ 1;
-  const int n = A.ctr->ext_count[cur];
+  const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
+  const int n = A.ctr->step.ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
@@ -894,13 +903,13 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int cur) {
         }
       }
     }
-    const int ei = wave_append(&A.ctr->ext_count[nxt], ext);
+    const int ei = wave_append(&A.ctr->step.ext[slot + 1], ext);
     if (ext) {
       st3(T.q_o[nxt], P, ei, e_o);
       st3(T.q_d[nxt], P, ei, e_d);
       T.q_path[nxt][ei] = p;
     }
-    const int si = wave_append(&A.ctr->sq_count, shadow);
+    const int si = wave_append(&A.ctr->step.sq[slot + 1], shadow);
     if (shadow) {
       st3(T.s_o, P, si, s_o);
       st3(T.s_d, P, si, s_d);
@@ -911,9 +920,9 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int cur) {
   }
 }
 
-__global__ void __launch_bounds__(kShadeBlock) k_pt_resolve(PtArgs A) {
+__global__ void __launch_bounds__(kShadeBlock) k_pt_resolve(PtArgs A, int slot) {
   const PtBuf& T = A.T;
-  const int n = A.ctr->sq_count, P = A.P;
+  const int n = A.ctr->step.sq[slot], P = A.P;
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
@@ -1152,7 +1161,7 @@ RayQueue rq(const float* o3, const float* d3, int cap, const int* cnt, float* t,
 }
 const RayQueue kNoQueue{nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
 
-using TraceKernel = void (*)(DevScene, RayQueue, RayQueue, DevCounters*);
+using TraceKernel = void (*)(DevScene, RayQueue, RayQueue, DevCounters*, int*);
 TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps) {
   if (stamps) return narrow ? k_trace<false, false, true, true> : k_trace<false, false, false, true>;
   if (count) {
@@ -1164,11 +1173,11 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps) {
 }
 
 // One persistent traversal launch over qa then qb (max_rays bounds the grid).
-int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, Timer& tm, bool count, const RayQueue& qa,
-                 const RayQueue& qb, int max_rays) {
+// `fetch` must be zero (the iteration's counter memset, or the caller).
+int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, int* fetch, Timer& tm, bool count,
+                 const RayQueue& qa, const RayQueue& qb, int max_rays) {
   const size_t lds = trace_lds_bytes(c->ds.max_stack, c->narrow);
   const int grid = std::max(1, std::min(c->trace_blocks, (max_rays + kTraceBlock - 1) / kTraceBlock));
-  (void)hipMemsetAsync(&ctr->fetch, 0, sizeof(int), stream);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->trace_log) {  // diagnostic (WR_TRACE_LOG=1): rays and duration of every launch
     (void)hipEventCreate(&e0);
@@ -1176,7 +1185,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, Timer& tm,
     (void)hipEventRecord(e0, stream);
   }
   hipLaunchKernelGGL(trace_kernel(count, c->spheres, c->narrow, c->stamps), dim3(grid), dim3(kTraceBlock), lds,
-                     stream, c->ds, qa, qb, ctr);
+                     stream, c->ds, qa, qb, ctr, fetch);
   tm.mark(WR_K_TRACE);
   if (c->trace_log) {
     (void)hipEventRecord(e1, stream);
@@ -1597,7 +1606,9 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   hipLaunchKernelGGL(k_api_prep, dim3(g), dim3(256), 0, c->stream, dr, n, occ ? 1 : 0, o3, d3, tmn, tmx);
   c->timing = false;
   Timer tm(c, nullptr);
-  trace_launch(c, c->stream, c->ctr, tm, false, rq(o3, d3, n, cnt, tt, pr, tmn, tmx), kNoQueue, n);
+  HIPCHK(hipMemsetAsync(&c->ctr->step.fetch[0], 0, sizeof(int), c->stream));
+  trace_launch(c, c->stream, c->ctr, &c->ctr->step.fetch[0], tm, false, rq(o3, d3, n, cnt, tt, pr, tmn, tmx),
+               kNoQueue, n);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
   HIPCHK(hipGetLastError());
@@ -1682,43 +1693,38 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
     A.B = pp.bb;
     A.ctr = pp.ctr;
     A.iter = static_cast<uint32_t>(prm->iter_begin + it);
-    int* ext_cnt = &pp.ctr->ext_count[0];
-    int* sq_cnt = &pp.ctr->sq_count;
-    const RayQueue sq = rq(B.s_o, B.s_d, B.cap_sq, sq_cnt, B.s_t, B.s_prim);
-    auto ext = [&](int q) { return rq(B.q_o[q], B.q_d[q], P, ext_cnt + q, B.q_t[q], B.q_prim[q]); };
+    StepCounters* sc = &pp.ctr->step;
+    auto sq = [&](int slot) { return rq(B.s_o, B.s_d, B.cap_sq, &sc->sq[slot], B.s_t, B.s_prim); };
+    auto ext = [&](int slot) {
+      const int q = slot & 1;
+      return rq(B.q_o[q], B.q_d[q], P, &sc->ext[slot], B.q_t[q], B.q_prim[q]);
+    };
     const int sq_max = B.cap_sq;
+    HIPCHK(hipMemsetAsync(sc, 0, sizeof(StepCounters), sm));
     // ---------------- light pass (:67-131)
-    HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), sm));
-    HIPCHK(hipMemsetAsync(ext_cnt, 0, sizeof(int), sm));
     hipLaunchKernelGGL(k_light_gen, dim3(g), dim3(kShadeBlock), 0, sm, A);
     tm.mark(WR_K_GEN);
-    int cur = 0;
     for (int b = 0; b < A.maxlen - 1; ++b) {
-      trace_launch(c, sm, pp.ctr, tm, count, ext(cur), kNoQueue, P);
-      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), sm));
-      hipLaunchKernelGGL(k_light_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, cur);
+      trace_launch(c, sm, pp.ctr, &sc->fetch[b], tm, count, ext(b), kNoQueue, P);
+      hipLaunchKernelGGL(k_light_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, b);
       tm.mark(WR_K_SHADE);
-      cur ^= 1;
     }
     // ---------------- camera pass (:133-264).  The light pass's splat rays
     // (connectToCamera) ride along with the primary rays; afterwards each
     // bounce's shadow / aux rays ride along with the next bounce's extension rays.
-    HIPCHK(hipMemsetAsync(ext_cnt, 0, sizeof(int), sm));
     hipLaunchKernelGGL(k_camera_gen, dim3(g), dim3(kShadeBlock), 0, sm, A);
     tm.mark(WR_K_GEN);
-    cur = 0;
     for (int b = 0; b <= A.maxlen; ++b) {
+      const int slot = kCamSlot + b;
       const bool more = b < A.maxlen;  // extension rays of bounce b exist
-      trace_launch(c, sm, pp.ctr, tm, count, sq, more ? ext(cur) : kNoQueue, (more ? P : 0) + sq_max);
-      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max)), dim3(kShadeBlock), 0, sm, A);
-      if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, sm, A);
+      trace_launch(c, sm, pp.ctr, &sc->fetch[slot], tm, count, sq(slot), more ? ext(slot) : kNoQueue,
+                   (more ? P : 0) + sq_max);
+      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max)), dim3(kShadeBlock), 0, sm, A, slot);
+      if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, sm, A, slot);
       tm.mark(WR_K_RESOLVE);
       if (!more) break;
-      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), sm));  // next extension queue
-      HIPCHK(hipMemsetAsync(sq_cnt, 0, 2 * sizeof(int), sm));           // sq_count, di_count
-      hipLaunchKernelGGL(k_camera_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, cur);
+      hipLaunchKernelGGL(k_camera_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, slot);
       tm.mark(WR_K_SHADE);
-      cur ^= 1;
     }
   }
   HIPCHK(hipGetLastError());
@@ -1729,6 +1735,7 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
 int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int film_on_device, wr_stats* st) {
   if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
   if (prm->width <= 0 || prm->height <= 0 || prm->spp <= 0) return fail(WR_E_ARG, "bad film size / spp");
+  if (prm->max_depth < 0 || prm->max_depth > kSlots - 3) return fail(WR_E_ARG, "max_depth must be in 0..61");
   if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "path tracing needs at least one area light");
   HIPCHK(hipSetDevice(c->device));
   const double t0 = host_now();
@@ -1762,27 +1769,21 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
     A.T = pp.pb;
     A.ctr = pp.ctr;
     A.k = static_cast<uint32_t>(k);
-    int* ext_cnt = &pp.ctr->ext_count[0];
-    int* sq_cnt = &pp.ctr->sq_count;
-    HIPCHK(hipMemsetAsync(ext_cnt, 0, sizeof(int), sm));
+    StepCounters* sc = &pp.ctr->step;
+    HIPCHK(hipMemsetAsync(sc, 0, sizeof(StepCounters), sm));
     hipLaunchKernelGGL(k_pt_gen, dim3(g), dim3(kShadeBlock), 0, sm, A);
     tm.mark(WR_K_GEN);
-    int cur = 0;
-    HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), sm));
     for (int b = 0; b <= A.max_depth + 1; ++b) {
       // NEE shadow rays of the previous vertex ride along with this bounce's rays
       const bool more = b <= A.max_depth;
-      trace_launch(c, sm, pp.ctr, tm, count, rq(T.s_o, T.s_d, P, sq_cnt, T.s_t, T.s_prim),
-                   more ? rq(T.q_o[cur], T.q_d[cur], P, ext_cnt + cur, T.q_t[cur], T.q_prim[cur]) : kNoQueue,
-                   2 * P);
-      hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, sm, A);
+      const int q = b & 1;
+      trace_launch(c, sm, pp.ctr, &sc->fetch[b], tm, count, rq(T.s_o, T.s_d, P, &sc->sq[b], T.s_t, T.s_prim),
+                   more ? rq(T.q_o[q], T.q_d[q], P, &sc->ext[b], T.q_t[q], T.q_prim[q]) : kNoQueue, 2 * P);
+      hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, sm, A, b);
       tm.mark(WR_K_RESOLVE);
       if (!more) break;
-      HIPCHK(hipMemsetAsync(ext_cnt + (cur ^ 1), 0, sizeof(int), sm));
-      HIPCHK(hipMemsetAsync(sq_cnt, 0, sizeof(int), sm));
-      hipLaunchKernelGGL(k_pt_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, cur);
+      hipLaunchKernelGGL(k_pt_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, b);
       tm.mark(WR_K_SHADE);
-      cur ^= 1;
     }
   }
   HIPCHK(hipGetLastError());
