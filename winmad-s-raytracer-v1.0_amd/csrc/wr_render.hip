@@ -63,7 +63,7 @@ struct StepCounters {
   int fetch[kSlots];  // persistent-traversal cursor of the step's trace launch
 };
 struct DevCounters {
-  StepCounters step;
+  int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
   unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
   unsigned long long closest, shadow, inner, leaves, refs;
 };
@@ -113,11 +113,10 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 // =============================================================== trace kernels
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
 template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
-__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, RayQueue qa, RayQueue qb, DevCounters* ctr,
-                                                      int* fetch) {
+__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
   extern __shared__ uint32_t smem[];
   TraceCounters tc{0, 0, 0};
-  trace_queue<COUNT, SPH, NARROW, STAMP>(S, qa, qb, fetch, smem, tc, ctr->stamps);
+  trace_queue<COUNT, SPH, NARROW, STAMP>(S, Q, fetch, smem, tc, ctr->stamps);
   if (COUNT) {
     unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs);
     if (lane_id() == 0) {
@@ -203,6 +202,7 @@ struct BdptArgs {
   DevScene S;
   BdptBuf B;
   DevCounters* ctr;
+  StepCounters* sc;  // this iteration's queue counters
   float* film;
   int W, H, P;
   uint32_t seed, iter;
@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_light_gen(BdptArgs A) {
     st3(B.q_d[0], P, p, normalize(dir));
     B.q_path[0][p] = p;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->step.ext[0] = P;
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = P;
 }
 
 // sampleScattering (:370-416).  Returns false when the subpath ends.
@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_light_shade(BdptArgs A, int slo
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
-  const int n = A.ctr->step.ext[slot];
+  const int n = A.sc->ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;  // whole waves reach the appends
@@ -379,13 +379,13 @@ __global__ void __launch_bounds__(kShadeBlock) k_light_shade(BdptArgs A, int slo
         }
       }
     }
-    const int ei = wave_append(&A.ctr->step.ext[slot + 1], ext);
+    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
     if (ext) {
       st3(B.q_o[nxt], P, ei, e_o);
       st3(B.q_d[nxt], P, ei, e_d);
       B.q_path[nxt][ei] = p;
     }
-    const int si = wave_append(&A.ctr->step.sq[kCamSlot], splat);  // traced with the camera primaries
+    const int si = wave_append(&A.sc->sq[kCamSlot], splat);  // traced with the camera primaries
     if (splat) {
       st3(B.s_o, B.cap_sq, si, s_o);
       st3(B.s_d, B.cap_sq, si, s_d);
@@ -438,7 +438,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptArgs A) {
     st3(B.q_d[0], P, s, normalize(d));
     B.q_path[0][s] = p;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->step.ext[kCamSlot] = P;
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[kCamSlot] = P;
 }
 
 // One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
@@ -447,7 +447,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int sl
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;
-  const int n = A.ctr->step.ext[slot];
+  const int n = A.sc->ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
@@ -588,9 +588,9 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int sl
     }
     // DI queue entries
     {
-      const int di_i = wave_append(&A.ctr->step.di[slot + 1], di);
+      const int di_i = wave_append(&A.sc->di[slot + 1], di);
       if (di) B.di_list[di_i] = p;
-      const int ni = wave_append(&A.ctr->step.sq[slot + 1], nee);
+      const int ni = wave_append(&A.sc->sq[slot + 1], nee);
       if (nee) {
         st3(B.s_o, cap, ni, hp);
         st3(B.s_d, cap, ni, nee_d);
@@ -598,7 +598,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int sl
         B.s_meta[ni] = (SQ_NEE << 30) | p;
         B.s_pix[ni] = pix;
       }
-      const int bi = wave_append(&A.ctr->step.sq[slot + 1], dib);
+      const int bi = wave_append(&A.sc->sq[slot + 1], dib);
       if (dib) {
         st3(B.s_o, cap, bi, dib_o);
         st3(B.s_d, cap, bi, dib_d);
@@ -667,7 +667,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int sl
             }
           }
         }
-        const int si = wave_append(&A.ctr->step.sq[slot + 1], shoot);
+        const int si = wave_append(&A.sc->sq[slot + 1], shoot);
         if (shoot) {
           st3(B.s_o, cap, si, hp);
           st3(B.s_d, cap, si, sdir);
@@ -687,7 +687,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int sl
         B.c_len[p] = len + 1;
       }
     }
-    const int ei = wave_append(&A.ctr->step.ext[slot + 1], ext);
+    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
     if (ext) {
       st3(B.q_o[nxt], P, ei, e_o);
       st3(B.q_d[nxt], P, ei, e_d);
@@ -700,7 +700,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int sl
 __global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptArgs A, int slot) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
-  const int n = A.ctr->step.sq[slot], cap = B.cap_sq;
+  const int n = A.sc->sq[slot], cap = B.cap_sq;
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
@@ -740,7 +740,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptArgs A, int slot
 // getDirectIllumination's final combination (:533-607)
 __global__ void __launch_bounds__(kShadeBlock) k_di_finalize(BdptArgs A, int slot) {
   const BdptBuf& B = A.B;
-  const int n = A.ctr->step.di[slot], P = A.P;
+  const int n = A.sc->di[slot], P = A.P;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
     const int p = B.di_list[j];
     const int flags = B.di_flags[p];
@@ -776,6 +776,7 @@ struct PtArgs {
   DevScene S;
   PtBuf T;
   DevCounters* ctr;
+  StepCounters* sc;  // this sample's queue counters
   float* film;
   int W, H, P, spp, grid_len, max_depth;
   uint32_t seed, k;
@@ -807,7 +808,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_gen(PtArgs A) {
     st3(T.q_d[0], P, p, d);
     T.q_path[0][p] = p;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.ctr->step.ext[0] = P;
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = P;
 }
 
 // One PathIntegrator::raytracing iteration (pathIntegrator.cpp:43-146)
@@ -815,7 +816,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int slot) {
   const PtBuf& T = A.T;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
-  const int n = A.ctr->step.ext[slot];
+  const int n = A.sc->ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
@@ -903,13 +904,13 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int slot) {
         }
       }
     }
-    const int ei = wave_append(&A.ctr->step.ext[slot + 1], ext);
+    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
     if (ext) {
       st3(T.q_o[nxt], P, ei, e_o);
       st3(T.q_d[nxt], P, ei, e_d);
       T.q_path[nxt][ei] = p;
     }
-    const int si = wave_append(&A.ctr->step.sq[slot + 1], shadow);
+    const int si = wave_append(&A.sc->sq[slot + 1], shadow);
     if (shadow) {
       st3(T.s_o, P, si, s_o);
       st3(T.s_d, P, si, s_d);
@@ -922,7 +923,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int slot) {
 
 __global__ void __launch_bounds__(kShadeBlock) k_pt_resolve(PtArgs A, int slot) {
   const PtBuf& T = A.T;
-  const int n = A.ctr->step.sq[slot], P = A.P;
+  const int n = A.sc->sq[slot], P = A.P;
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
@@ -996,14 +997,20 @@ size_t measure(Fn fn) {  // bytes an arena layout needs
 // launches of another.  The film is a sum, so the result does not depend on the
 // pipeline count (up to the order of float atomics).
 constexpr int kMaxPipes = 4;
+// Each pipeline advances a group of up to kGroup iterations / samples in
+// lockstep: every traversal launch takes the queues of all of them, so the
+// launch tail (its slowest ray) is paid once per group.
+constexpr int kGroup = 2;
 struct Pipe {
   hipStream_t stream = nullptr;
   DevCounters* ctr = nullptr;
+  StepCounters* sc = nullptr;  // [kGroup]
   Arena work;
   size_t work_key = 0;  // P for which `work` is laid out
   int work_kind = 0;    // 1 bdpt, 2 pt
-  BdptBuf bb{};
-  PtBuf pb{};
+  int work_sets = 0;    // buffer sets laid out
+  BdptBuf bb[kGroup]{};
+  PtBuf pb[kGroup]{};
   std::vector<hipEvent_t> events;  // Timer marks (time_kernels)
   std::vector<int> ev_cat;
   size_t ev_used = 0;
@@ -1123,17 +1130,23 @@ void layout_pt(Arena& a, PtBuf& T, int P) {
   T.s_prim = a.take<int>(sP);
 }
 
-int ensure_work(Pipe& p, int kind, int P) {
-  if (p.work_kind == kind && p.work_key == static_cast<size_t>(P)) return WR_OK;
+int ensure_work(Pipe& p, int kind, int P, int sets) {
+  if (p.work_kind == kind && p.work_key == static_cast<size_t>(P) && p.work_sets >= sets) return WR_OK;
   p.work_kind = 0;
-  size_t bytes = kind == 1 ? measure([&](Arena& a) { BdptBuf b; layout_bdpt(a, b, P); })
-                           : measure([&](Arena& a) { PtBuf t; layout_pt(a, t, P); });
-  int rc = p.work.reserve(bytes);
+  auto lay = [&](Arena& a, Pipe* dst) {
+    for (int g = 0; g < sets; ++g) {
+      BdptBuf b;
+      PtBuf t;
+      if (kind == 1) layout_bdpt(a, dst ? dst->bb[g] : b, P);
+      else layout_pt(a, dst ? dst->pb[g] : t, P);
+    }
+  };
+  int rc = p.work.reserve(measure([&](Arena& a) { lay(a, nullptr); }));
   if (rc) return rc;
-  if (kind == 1) layout_bdpt(p.work, p.bb, P);
-  else layout_pt(p.work, p.pb, P);
+  lay(p.work, &p);
   p.work_kind = kind;
   p.work_key = P;
+  p.work_sets = sets;
   return WR_OK;
 }
 
@@ -1159,9 +1172,17 @@ RayQueue rq(const float* o3, const float* d3, int cap, const int* cnt, float* t,
             const float* tmin = nullptr, const float* tmax = nullptr) {
   return RayQueue{o3, d3, cap, cnt, tmin, tmax, t, prim};
 }
-const RayQueue kNoQueue{nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+// queues of one launch (empty `count` pointers are skipped)
+struct QueueList {
+  TraceQueues Q{};
+  int max_rays = 0;
+  void add(const RayQueue& q, int cap) {
+    Q.q[Q.n++] = q;
+    max_rays += cap;
+  }
+};
 
-using TraceKernel = void (*)(DevScene, RayQueue, RayQueue, DevCounters*, int*);
+using TraceKernel = void (*)(DevScene, TraceQueues, DevCounters*, int*);
 TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps) {
   if (stamps) return narrow ? k_trace<false, false, true, true> : k_trace<false, false, false, true>;
   if (count) {
@@ -1175,7 +1196,7 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps) {
 // One persistent traversal launch over qa then qb (max_rays bounds the grid).
 // `fetch` must be zero (the iteration's counter memset, or the caller).
 int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, int* fetch, Timer& tm, bool count,
-                 const RayQueue& qa, const RayQueue& qb, int max_rays) {
+                 const TraceQueues& Q, int max_rays) {
   const size_t lds = trace_lds_bytes(c->ds.max_stack, c->narrow);
   const int grid = std::max(1, std::min(c->trace_blocks, (max_rays + kTraceBlock - 1) / kTraceBlock));
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1185,17 +1206,20 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, int* fetch
     (void)hipEventRecord(e0, stream);
   }
   hipLaunchKernelGGL(trace_kernel(count, c->spheres, c->narrow, c->stamps), dim3(grid), dim3(kTraceBlock), lds,
-                     stream, c->ds, qa, qb, ctr, fetch);
+                     stream, c->ds, Q, ctr, fetch);
   tm.mark(WR_K_TRACE);
   if (c->trace_log) {
     (void)hipEventRecord(e1, stream);
     (void)hipEventSynchronize(e1);
-    int na = 0, nb = 0;
-    if (qa.count) (void)hipMemcpy(&na, qa.count, sizeof(int), hipMemcpyDeviceToHost);
-    if (qb.count) (void)hipMemcpy(&nb, qb.count, sizeof(int), hipMemcpyDeviceToHost);
+    int tot = 0;
+    for (int i = 0; i < Q.n; ++i) {
+      int k = 0;
+      if (Q.q[i].count) (void)hipMemcpy(&k, Q.q[i].count, sizeof(int), hipMemcpyDeviceToHost);
+      tot += k;
+    }
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, e0, e1);
-    std::fprintf(stderr, "[wr trace] rays %d + %d  %.1f us  grid %d\n", na, nb, ms * 1e3f, grid);
+    std::fprintf(stderr, "[wr trace] %d queues, %d rays  %.1f us  grid %d\n", Q.n, tot, ms * 1e3f, grid);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
   }
@@ -1377,7 +1401,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   for (Pipe& pp : c->pipes) {
     if (hipStreamCreateWithFlags(&pp.stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&pp.done, hipEventDisableTiming) != hipSuccess ||
-        hipMalloc(&pp.ctr, sizeof(DevCounters)) != hipSuccess) {
+        hipMalloc(&pp.ctr, sizeof(DevCounters)) != hipSuccess ||
+        hipMalloc(&pp.sc, kGroup * sizeof(StepCounters)) != hipSuccess) {
       wr_destroy(c);
       return fail(WR_E_HIP, "pipeline stream / counters");
     }
@@ -1564,6 +1589,7 @@ void wr_destroy(wr_context* c) {
     for (hipEvent_t e : p.events) (void)hipEventDestroy(e);
     if (p.done) (void)hipEventDestroy(p.done);
     if (p.ctr) (void)hipFree(p.ctr);
+    if (p.sc) (void)hipFree(p.sc);
     p.work.release();
     if (p.stream) (void)hipStreamDestroy(p.stream);
   }
@@ -1606,9 +1632,10 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   hipLaunchKernelGGL(k_api_prep, dim3(g), dim3(256), 0, c->stream, dr, n, occ ? 1 : 0, o3, d3, tmn, tmx);
   c->timing = false;
   Timer tm(c, nullptr);
-  HIPCHK(hipMemsetAsync(&c->ctr->step.fetch[0], 0, sizeof(int), c->stream));
-  trace_launch(c, c->stream, c->ctr, &c->ctr->step.fetch[0], tm, false, rq(o3, d3, n, cnt, tt, pr, tmn, tmx),
-               kNoQueue, n);
+  HIPCHK(hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream));
+  QueueList ql;
+  ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx), n);
+  trace_launch(c, c->stream, c->ctr, &c->ctr->fetch, tm, false, ql.Q, ql.max_rays);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
   HIPCHK(hipGetLastError());
@@ -1666,64 +1693,83 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
   HIPCHK(hipSetDevice(c->device));
   const double t0 = host_now();
   const int P = prm->width * prm->height;
-  const int np = std::max(1, std::min(c->npipes, prm->iterations));
+  const int ngroups = (prm->iterations + kGroup - 1) / kGroup;
+  const int np = std::max(1, std::min(c->npipes, ngroups));
+  const int sets = std::max(1, std::min(kGroup, prm->iterations));
   for (int i = 0; i < np; ++i)
-    if (int rc = ensure_work(c->pipes[i], 1, P)) return rc;
+    if (int rc = ensure_work(c->pipes[i], 1, P, sets)) return rc;
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
   begin_render(c, np, prm->time_kernels);
-  BdptArgs A;
-  A.S = c->ds;
-  A.film = dfilm;
-  A.W = prm->width;
-  A.H = prm->height;
-  A.P = P;
-  A.seed = prm->seed;
-  A.ctl = prm->control_length;
-  A.maxlen = prm->max_path_length > 0 ? prm->max_path_length : 10;
-  A.faithful = prm->faithful;
+  BdptArgs A0;
+  A0.S = c->ds;
+  A0.film = dfilm;
+  A0.W = prm->width;
+  A0.H = prm->height;
+  A0.P = P;
+  A0.seed = prm->seed;
+  A0.ctl = prm->control_length;
+  A0.maxlen = prm->max_path_length > 0 ? prm->max_path_length : 10;
+  A0.faithful = prm->faithful;
+  const int maxlen = A0.maxlen;
   const bool count = prm->count_work != 0;
   const int g = shade_grid(c, P);
-  for (int it = 0; it < prm->iterations; ++it) {
-    Pipe& pp = c->pipes[it % np];
+  for (int gi = 0; gi < ngroups; ++gi) {
+    // a group of gn iterations in lockstep on pipeline gi % np
+    Pipe& pp = c->pipes[gi % np];
     const hipStream_t sm = pp.stream;
     Timer tm(c, &pp);
-    const BdptBuf& B = pp.bb;
-    A.B = pp.bb;
-    A.ctr = pp.ctr;
-    A.iter = static_cast<uint32_t>(prm->iter_begin + it);
-    StepCounters* sc = &pp.ctr->step;
-    auto sq = [&](int slot) { return rq(B.s_o, B.s_d, B.cap_sq, &sc->sq[slot], B.s_t, B.s_prim); };
-    auto ext = [&](int slot) {
-      const int q = slot & 1;
-      return rq(B.q_o[q], B.q_d[q], P, &sc->ext[slot], B.q_t[q], B.q_prim[q]);
+    const int it0 = gi * kGroup, gn = std::min(kGroup, prm->iterations - it0);
+    BdptArgs A[kGroup];
+    for (int m = 0; m < gn; ++m) {
+      A[m] = A0;
+      A[m].B = pp.bb[m];
+      A[m].ctr = pp.ctr;
+      A[m].sc = pp.sc + m;
+      A[m].iter = static_cast<uint32_t>(prm->iter_begin + it0 + m);
+    }
+    auto sq = [&](int m, int slot) {
+      const BdptBuf& B = pp.bb[m];
+      return rq(B.s_o, B.s_d, B.cap_sq, &pp.sc[m].sq[slot], B.s_t, B.s_prim);
     };
-    const int sq_max = B.cap_sq;
-    HIPCHK(hipMemsetAsync(sc, 0, sizeof(StepCounters), sm));
+    auto ext = [&](int m, int slot) {
+      const BdptBuf& B = pp.bb[m];
+      const int q = slot & 1;
+      return rq(B.q_o[q], B.q_d[q], P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
+    };
+    const int sq_max = pp.bb[0].cap_sq;
+    HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
     // ---------------- light pass (:67-131)
-    hipLaunchKernelGGL(k_light_gen, dim3(g), dim3(kShadeBlock), 0, sm, A);
+    for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_light_gen, dim3(g), dim3(kShadeBlock), 0, sm, A[m]);
     tm.mark(WR_K_GEN);
-    for (int b = 0; b < A.maxlen - 1; ++b) {
-      trace_launch(c, sm, pp.ctr, &sc->fetch[b], tm, count, ext(b), kNoQueue, P);
-      hipLaunchKernelGGL(k_light_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, b);
+    for (int b = 0; b < maxlen - 1; ++b) {
+      QueueList ql;
+      for (int m = 0; m < gn; ++m) ql.add(ext(m, b), P);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays);
+      for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_light_shade, dim3(g), dim3(kShadeBlock), 0, sm, A[m], b);
       tm.mark(WR_K_SHADE);
     }
     // ---------------- camera pass (:133-264).  The light pass's splat rays
     // (connectToCamera) ride along with the primary rays; afterwards each
     // bounce's shadow / aux rays ride along with the next bounce's extension rays.
-    hipLaunchKernelGGL(k_camera_gen, dim3(g), dim3(kShadeBlock), 0, sm, A);
+    for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_camera_gen, dim3(g), dim3(kShadeBlock), 0, sm, A[m]);
     tm.mark(WR_K_GEN);
-    for (int b = 0; b <= A.maxlen; ++b) {
+    for (int b = 0; b <= maxlen; ++b) {
       const int slot = kCamSlot + b;
-      const bool more = b < A.maxlen;  // extension rays of bounce b exist
-      trace_launch(c, sm, pp.ctr, &sc->fetch[slot], tm, count, sq(slot), more ? ext(slot) : kNoQueue,
-                   (more ? P : 0) + sq_max);
-      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max)), dim3(kShadeBlock), 0, sm, A, slot);
-      if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, sm, A, slot);
+      const bool more = b < maxlen;  // extension rays of bounce b exist
+      QueueList ql;
+      for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), sq_max);
+      if (more)
+        for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays);
+      for (int m = 0; m < gn; ++m) {
+        hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max)), dim3(kShadeBlock), 0, sm, A[m], slot);
+        if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, sm, A[m], slot);
+      }
       tm.mark(WR_K_RESOLVE);
       if (!more) break;
-      hipLaunchKernelGGL(k_camera_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, slot);
+      for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_camera_shade, dim3(g), dim3(kShadeBlock), 0, sm, A[m], slot);
       tm.mark(WR_K_SHADE);
     }
   }
@@ -1742,47 +1788,64 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
   const int P = prm->width * prm->height;
   const int k0 = prm->sample_begin;
   const int k1 = prm->sample_count > 0 ? k0 + prm->sample_count : prm->spp;
-  const int np = std::max(1, std::min(c->npipes, k1 - k0));
+  const int nk = std::max(0, k1 - k0);
+  const int ngroups = (nk + kGroup - 1) / kGroup;
+  const int np = std::max(1, std::min(c->npipes, ngroups));
+  const int sets = std::max(1, std::min(kGroup, nk));
   for (int i = 0; i < np; ++i)
-    if (int rc = ensure_work(c->pipes[i], 2, P)) return rc;
+    if (int rc = ensure_work(c->pipes[i], 2, P, sets)) return rc;
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
   begin_render(c, np, prm->time_kernels);
-  PtArgs A;
-  A.S = c->ds;
-  A.film = dfilm;
-  A.W = prm->width;
-  A.H = prm->height;
-  A.P = P;
-  A.spp = prm->spp;
-  A.grid_len = static_cast<int>(std::sqrt(static_cast<double>(prm->spp)));
-  A.max_depth = prm->max_depth;
-  A.seed = prm->seed;
+  PtArgs A0;
+  A0.S = c->ds;
+  A0.film = dfilm;
+  A0.W = prm->width;
+  A0.H = prm->height;
+  A0.P = P;
+  A0.spp = prm->spp;
+  A0.grid_len = static_cast<int>(std::sqrt(static_cast<double>(prm->spp)));
+  A0.max_depth = prm->max_depth;
+  A0.seed = prm->seed;
   const bool count = prm->count_work != 0;
   const int g = shade_grid(c, P);
-  for (int k = k0; k < k1; ++k) {
-    Pipe& pp = c->pipes[(k - k0) % np];
+  for (int gi = 0; gi < ngroups; ++gi) {
+    // a group of gn samples in lockstep on pipeline gi % np
+    Pipe& pp = c->pipes[gi % np];
     const hipStream_t sm = pp.stream;
     Timer tm(c, &pp);
-    const PtBuf& T = pp.pb;
-    A.T = pp.pb;
-    A.ctr = pp.ctr;
-    A.k = static_cast<uint32_t>(k);
-    StepCounters* sc = &pp.ctr->step;
-    HIPCHK(hipMemsetAsync(sc, 0, sizeof(StepCounters), sm));
-    hipLaunchKernelGGL(k_pt_gen, dim3(g), dim3(kShadeBlock), 0, sm, A);
+    const int gk = k0 + gi * kGroup, gn = std::min(kGroup, k1 - gk);
+    PtArgs A[kGroup];
+    for (int m = 0; m < gn; ++m) {
+      A[m] = A0;
+      A[m].T = pp.pb[m];
+      A[m].ctr = pp.ctr;
+      A[m].sc = pp.sc + m;
+      A[m].k = static_cast<uint32_t>(gk + m);
+    }
+    HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
+    for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_pt_gen, dim3(g), dim3(kShadeBlock), 0, sm, A[m]);
     tm.mark(WR_K_GEN);
-    for (int b = 0; b <= A.max_depth + 1; ++b) {
+    for (int b = 0; b <= A0.max_depth + 1; ++b) {
       // NEE shadow rays of the previous vertex ride along with this bounce's rays
-      const bool more = b <= A.max_depth;
+      const bool more = b <= A0.max_depth;
       const int q = b & 1;
-      trace_launch(c, sm, pp.ctr, &sc->fetch[b], tm, count, rq(T.s_o, T.s_d, P, &sc->sq[b], T.s_t, T.s_prim),
-                   more ? rq(T.q_o[q], T.q_d[q], P, &sc->ext[b], T.q_t[q], T.q_prim[q]) : kNoQueue, 2 * P);
-      hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, sm, A, b);
+      QueueList ql;
+      for (int m = 0; m < gn; ++m) {
+        const PtBuf& T = pp.pb[m];
+        ql.add(rq(T.s_o, T.s_d, P, &pp.sc[m].sq[b], T.s_t, T.s_prim), P);
+      }
+      if (more)
+        for (int m = 0; m < gn; ++m) {
+          const PtBuf& T = pp.pb[m];
+          ql.add(rq(T.q_o[q], T.q_d[q], P, &pp.sc[m].ext[b], T.q_t[q], T.q_prim[q]), P);
+        }
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays);
+      for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, sm, A[m], b);
       tm.mark(WR_K_RESOLVE);
       if (!more) break;
-      hipLaunchKernelGGL(k_pt_shade, dim3(g), dim3(kShadeBlock), 0, sm, A, b);
+      for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_pt_shade, dim3(g), dim3(kShadeBlock), 0, sm, A[m], b);
       tm.mark(WR_K_SHADE);
     }
   }

@@ -171,6 +171,15 @@ struct RayQueue {
   int* out_prim;
 };
 
+// The queues of one traversal launch, fetched in order (the shadow / aux queue
+// of an iteration first: its long rays start early and overlap the extension
+// rays instead of forming a tail of their own).
+constexpr int kMaxQueues = 4;
+struct TraceQueues {
+  RayQueue q[kMaxQueues];
+  int n;
+};
+
 // Per-wave LDS scratch of the traversal (one wave per workgroup, 64 lanes):
 //   stack  [depth][64] tmin (float) + [depth][64] node (u16 when the tree has
 //          <= 65536 nodes, NARROW; u32 otherwise)
@@ -203,9 +212,8 @@ __host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
                       4 * 64 + 16);
 }
 
-// Persistent closest-hit traversal over up to two ray queues (one wave per
-// workgroup); queue `qa` is fetched first (the long shadow rays start early and
-// overlap the extension rays of `qb` instead of forming a tail of their own).
+// Persistent closest-hit traversal over the ray queues of one launch (one wave
+// per workgroup), fetched in queue order.
 //
 // KDtreeAccel::traverse semantics per ray; the SIMT structure is GPU-specific:
 //   * the reference never stops early (it walks to the far end of the root box
@@ -266,7 +274,7 @@ __device__ __forceinline__ uint64_t stamp_now() {
 }
 
 template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
-__device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& qa, const RayQueue& qb, int* fetch,
+__device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues& Q, int* fetch,
                                             uint32_t* lds, TraceCounters& ctr,
                                             unsigned long long* stamps = nullptr) {
   uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
@@ -297,9 +305,25 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
   unsigned long long* olo = reinterpret_cast<unsigned long long*>(own + kPairBatch);  // [64] key << 32 | prim
   unsigned long long* ohi = olo + 64;  // [64] (INT_MAX - key) << 32 | prim
   uint8_t* onear = reinterpret_cast<uint8_t*>(ohi + 64);  // [64]
-  const int na = qa.count ? *qa.count : 0;
-  const int n = na + (qb.count ? *qb.count : 0);
-  bool inb = false;      // the lane's ray comes from qb
+  int qend[kMaxQueues];  // queue i holds launch indices [qend[i-1], qend[i])
+  {
+    int acc = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxQueues; ++i) {
+      if (i < Q.n && Q.q[i].count) acc += *Q.q[i].count;
+      qend[i] = acc;
+    }
+  }
+  const int n = qend[kMaxQueues - 1];
+  int qi = 0;            // queue of the lane's ray
+  // field of queue qi (selects, no dynamic indexing of the kernel argument)
+  auto sel = [&](auto field) {
+    auto v = field(Q.q[0]);
+#pragma unroll
+    for (int i = 1; i < kMaxQueues; ++i)
+      if (qi == i) v = field(Q.q[i]);
+    return v;
+  };
   int r = -1;            // ray held by this lane (-1: none)
   bool pool = true;      // wave-uniform: queue not yet exhausted
   int pb = 0, pe = 0;    // wave-uniform: reserved queue indices [pb, pe)
@@ -364,13 +388,24 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
           pb += need;
         }
         if (idle && idx < n) {
-          inb = idx >= na;
-          const RayQueue& q = inb ? qb : qa;
-          r = inb ? idx - na : idx;
-          o = v3(q.o3[r], q.o3[q.cap + r], q.o3[2 * q.cap + r]);
-          d = v3(q.d3[r], q.d3[q.cap + r], q.d3[2 * q.cap + r]);
-          const float rtmin = q.tmin ? q.tmin[r] : 0.f;
-          rtmax = q.tmax ? q.tmax[r] : WR_INF;
+          qi = 0;
+          int q0 = 0;
+#pragma unroll
+          for (int i = 0; i < kMaxQueues - 1; ++i)
+            if (idx >= qend[i]) {
+              qi = i + 1;
+              q0 = qend[i];
+            }
+          r = idx - q0;
+          const float* o3 = sel([](const RayQueue& x) { return x.o3; });
+          const float* d3 = sel([](const RayQueue& x) { return x.d3; });
+          const int cap = sel([](const RayQueue& x) { return x.cap; });
+          const float* tmn = sel([](const RayQueue& x) { return x.tmin; });
+          const float* tmx = sel([](const RayQueue& x) { return x.tmax; });
+          o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
+          d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+          const float rtmin = tmn ? tmn[r] : 0.f;
+          rtmax = tmx ? tmx[r] : WR_INF;
           t_best = WR_INF;
           best = -1;
           sp = 0;
@@ -379,8 +414,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
           root_tmax = tmax;
           more = true;
           if (!boxed || rtmax < tmin) {  // :312-313, and the :323 check before the root
-            q.out_t[r] = WR_INF;
-            q.out_prim[r] = -1;
+            sel([](const RayQueue& x) { return x.out_t; })[r] = WR_INF;
+            sel([](const RayQueue& x) { return x.out_prim; })[r] = -1;
             r = -1;
             more = false;
           } else {
@@ -584,8 +619,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const RayQueue& q
     }
     if (act) {
       if (!more) {
-        (inb ? qb : qa).out_t[r] = t_best;
-        (inb ? qb : qa).out_prim[r] = best;
+        sel([](const RayQueue& x) { return x.out_t; })[r] = t_best;
+        sel([](const RayQueue& x) { return x.out_prim; })[r] = best;
         r = -1;
       }
     }
