@@ -1000,7 +1000,10 @@ constexpr int kMaxPipes = 4;
 // Each pipeline advances a group of up to kGroup iterations / samples in
 // lockstep: every traversal launch takes the queues of all of them, so the
 // launch tail (its slowest ray) is paid once per group.
-constexpr int kGroup = 2;
+#ifndef WR_GROUP
+#define WR_GROUP 2
+#endif
+constexpr int kGroup = WR_GROUP;
 struct Pipe {
   hipStream_t stream = nullptr;
   DevCounters* ctr = nullptr;

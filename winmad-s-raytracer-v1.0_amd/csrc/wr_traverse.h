@@ -174,7 +174,10 @@ struct RayQueue {
 // The queues of one traversal launch, fetched in order (the shadow / aux queue
 // of an iteration first: its long rays start early and overlap the extension
 // rays instead of forming a tail of their own).
-constexpr int kMaxQueues = 4;
+#ifndef WR_MAX_QUEUES
+#define WR_MAX_QUEUES 4
+#endif
+constexpr int kMaxQueues = WR_MAX_QUEUES;
 struct TraceQueues {
   RayQueue q[kMaxQueues];
   int n;
