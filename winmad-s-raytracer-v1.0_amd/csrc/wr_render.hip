@@ -1571,6 +1571,9 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
         per_cu <= 0)
       per_cu = 8;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    // diagnostic: WR_TRACE_WAVES_PER_CU caps the resident traversal waves (leaving
+    // room for the other pipelines' shading kernels)
+    if (const char* e = std::getenv("WR_TRACE_WAVES_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
     c->trace_blocks = c->cus * per_cu;
   }
   *out = c;
