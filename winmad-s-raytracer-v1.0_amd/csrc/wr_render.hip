@@ -47,6 +47,13 @@ namespace {
 constexpr int kVMax = 9;       // light vertices per subpath (pathLength 1..9, :77-124)
 constexpr int kTraceBlock = 64;  // one wave per workgroup: persistent traversal
 constexpr int kShadeBlock = 256;
+// The vertex kernels at <= 128 VGPRs (4 waves/SIMD, a few dwords spilled) run
+// beside the other pipelines' traversal far better than at 132-146 VGPRs:
+// measured 638 -> 693 Mrays/s (torus 1080p BDPT, 3 pipelines).
+#ifndef WR_SHADE_WAVES
+#define WR_SHADE_WAVES 4
+#endif
+#define WR_SHADE_OCC __attribute__((amdgpu_waves_per_eu(WR_SHADE_WAVES, 8)))
 
 enum SqKind { SQ_SPLAT = 0, SQ_CONN = 1, SQ_NEE = 2, SQ_DIB = 3 };
 enum DiFlag { DI_NEE = 1, DI_BSDF = 2, DI_EARLY = 4 };
@@ -280,7 +287,7 @@ __device__ __forceinline__ bool sample_scatter(const DevScene& S, Rng& rng, cons
 }
 
 // One light-subpath vertex (:77-128)
-__global__ void __launch_bounds__(kShadeBlock) k_light_shade(BdptArgs A, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptArgs A, int slot) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
@@ -443,7 +450,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptArgs A) {
 
 // One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
 // connections (shadow rays queued), scattering.
-__global__ void __launch_bounds__(kShadeBlock) k_camera_shade(BdptArgs A, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptArgs A, int slot) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;
