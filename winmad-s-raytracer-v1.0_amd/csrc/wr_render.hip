@@ -54,6 +54,12 @@ constexpr int kShadeBlock = 256;
 #define WR_SHADE_WAVES 4
 #endif
 #define WR_SHADE_OCC __attribute__((amdgpu_waves_per_eu(WR_SHADE_WAVES, 8)))
+// Iterations / samples a pipeline advances in lockstep (see struct Pipe).  The
+// per-vertex kernels take the whole group (member = blockIdx.y).
+#ifndef WR_GROUP
+#define WR_GROUP 2
+#endif
+constexpr int kGroup = WR_GROUP;
 
 enum SqKind { SQ_SPLAT = 0, SQ_CONN = 1, SQ_NEE = 2, SQ_DIB = 3 };
 enum DiFlag { DI_NEE = 1, DI_BSDF = 2, DI_EARLY = 4 };
@@ -215,11 +221,15 @@ struct BdptArgs {
   uint32_t seed, iter;
   int ctl, maxlen, faithful;
 };
+struct BdptGroup {
+  BdptArgs a[kGroup];
+};
 
 __device__ __forceinline__ bool len_ok(int ctl, int L) { return ctl <= 0 || L == ctl; }
 
 // generateLightSample (:267-311) + the first extension ray
-__global__ void __launch_bounds__(kShadeBlock) k_light_gen(BdptArgs A) {
+__global__ void __launch_bounds__(kShadeBlock) k_light_gen(BdptGroup G_) {
+  const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
   const int P = A.P;
   const float lpp = 1.f / static_cast<float>(A.S.nlights);
@@ -287,7 +297,8 @@ __device__ __forceinline__ bool sample_scatter(const DevScene& S, Rng& rng, cons
 }
 
 // One light-subpath vertex (:77-128)
-__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptArgs A, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGroup G_, int slot) {
+  const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
@@ -405,7 +416,8 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptAr
 }
 
 // generateCameraSample (:418-452) + first extension ray
-__global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptArgs A) {
+__global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptGroup G_) {
+  const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
   const DCam& cam = A.S.cam;
   const int P = A.P;
@@ -450,7 +462,8 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptArgs A) {
 
 // One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
 // connections (shadow rays queued), scattering.
-__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptArgs A, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptGroup G_, int slot) {
+  const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;
@@ -704,7 +717,8 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptA
 }
 
 // Light-tracing splats and camera-pass shadow / aux rays after traversal.
-__global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptArgs A, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptGroup G_, int slot) {
+  const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   const int n = A.sc->sq[slot], cap = B.cap_sq;
@@ -745,7 +759,8 @@ __global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptArgs A, int slot
 }
 
 // getDirectIllumination's final combination (:533-607)
-__global__ void __launch_bounds__(kShadeBlock) k_di_finalize(BdptArgs A, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) k_di_finalize(BdptGroup G_, int slot) {
+  const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
   const int n = A.sc->di[slot], P = A.P;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
@@ -788,9 +803,13 @@ struct PtArgs {
   int W, H, P, spp, grid_len, max_depth;
   uint32_t seed, k;
 };
+struct PtGroup {
+  PtArgs a[kGroup];
+};
 
 // SurfaceIntegrator::render per-sample setup (surfaceIntegrator.cpp:26-34)
-__global__ void __launch_bounds__(kShadeBlock) k_pt_gen(PtArgs A) {
+__global__ void __launch_bounds__(kShadeBlock) k_pt_gen(PtGroup G_) {
+  const PtArgs& A = G_.a[blockIdx.y];
   const PtBuf& T = A.T;
   const DCam& cam = A.S.cam;
   const int P = A.P;
@@ -819,7 +838,8 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_gen(PtArgs A) {
 }
 
 // One PathIntegrator::raytracing iteration (pathIntegrator.cpp:43-146)
-__global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtGroup G_, int slot) {
+  const PtArgs& A = G_.a[blockIdx.y];
   const PtBuf& T = A.T;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
@@ -928,7 +948,8 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtArgs A, int slot) {
   }
 }
 
-__global__ void __launch_bounds__(kShadeBlock) k_pt_resolve(PtArgs A, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) k_pt_resolve(PtGroup G_, int slot) {
+  const PtArgs& A = G_.a[blockIdx.y];
   const PtBuf& T = A.T;
   const int n = A.sc->sq[slot], P = A.P;
   const int gstride = gridDim.x * blockDim.x;
@@ -1007,10 +1028,6 @@ constexpr int kMaxPipes = 4;
 // Each pipeline advances a group of up to kGroup iterations / samples in
 // lockstep: every traversal launch takes the queues of all of them, so the
 // launch tail (its slowest ray) is paid once per group.
-#ifndef WR_GROUP
-#define WR_GROUP 2
-#endif
-constexpr int kGroup = WR_GROUP;
 struct Pipe {
   hipStream_t stream = nullptr;
   DevCounters* ctr = nullptr;
@@ -1734,7 +1751,8 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
     const hipStream_t sm = pp.stream;
     Timer tm(c, &pp);
     const int it0 = gi * kGroup, gn = std::min(kGroup, prm->iterations - it0);
-    BdptArgs A[kGroup];
+    BdptGroup GA;
+    BdptArgs* A = GA.a;
     for (int m = 0; m < gn; ++m) {
       A[m] = A0;
       A[m].B = pp.bb[m];
@@ -1754,19 +1772,19 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
     const int sq_max = pp.bb[0].cap_sq;
     HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
     // ---------------- light pass (:67-131)
-    for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_light_gen, dim3(g), dim3(kShadeBlock), 0, sm, A[m]);
+    hipLaunchKernelGGL(k_light_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
     tm.mark(WR_K_GEN);
     for (int b = 0; b < maxlen - 1; ++b) {
       QueueList ql;
       for (int m = 0; m < gn; ++m) ql.add(ext(m, b), P);
       trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays);
-      for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_light_shade, dim3(g), dim3(kShadeBlock), 0, sm, A[m], b);
+      hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
       tm.mark(WR_K_SHADE);
     }
     // ---------------- camera pass (:133-264).  The light pass's splat rays
     // (connectToCamera) ride along with the primary rays; afterwards each
     // bounce's shadow / aux rays ride along with the next bounce's extension rays.
-    for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_camera_gen, dim3(g), dim3(kShadeBlock), 0, sm, A[m]);
+    hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
     tm.mark(WR_K_GEN);
     for (int b = 0; b <= maxlen; ++b) {
       const int slot = kCamSlot + b;
@@ -1776,13 +1794,11 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
       if (more)
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
       trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays);
-      for (int m = 0; m < gn; ++m) {
-        hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max)), dim3(kShadeBlock), 0, sm, A[m], slot);
-        if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g), dim3(kShadeBlock), 0, sm, A[m], slot);
-      }
+      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max), gn), dim3(kShadeBlock), 0, sm, GA, slot);
+      if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, slot);
       tm.mark(WR_K_RESOLVE);
       if (!more) break;
-      for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_camera_shade, dim3(g), dim3(kShadeBlock), 0, sm, A[m], slot);
+      hipLaunchKernelGGL(k_camera_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, slot);
       tm.mark(WR_K_SHADE);
     }
   }
@@ -1829,7 +1845,8 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
     const hipStream_t sm = pp.stream;
     Timer tm(c, &pp);
     const int gk = k0 + gi * kGroup, gn = std::min(kGroup, k1 - gk);
-    PtArgs A[kGroup];
+    PtGroup GA;
+    PtArgs* A = GA.a;
     for (int m = 0; m < gn; ++m) {
       A[m] = A0;
       A[m].T = pp.pb[m];
@@ -1838,7 +1855,7 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
       A[m].k = static_cast<uint32_t>(gk + m);
     }
     HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
-    for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_pt_gen, dim3(g), dim3(kShadeBlock), 0, sm, A[m]);
+    hipLaunchKernelGGL(k_pt_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
     tm.mark(WR_K_GEN);
     for (int b = 0; b <= A0.max_depth + 1; ++b) {
       // NEE shadow rays of the previous vertex ride along with this bounce's rays
@@ -1855,10 +1872,10 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
           ql.add(rq(T.q_o[q], T.q_d[q], P, &pp.sc[m].ext[b], T.q_t[q], T.q_prim[q]), P);
         }
       trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays);
-      for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_pt_resolve, dim3(g), dim3(kShadeBlock), 0, sm, A[m], b);
+      hipLaunchKernelGGL(k_pt_resolve, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
       tm.mark(WR_K_RESOLVE);
       if (!more) break;
-      for (int m = 0; m < gn; ++m) hipLaunchKernelGGL(k_pt_shade, dim3(g), dim3(kShadeBlock), 0, sm, A[m], b);
+      hipLaunchKernelGGL(k_pt_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
       tm.mark(WR_K_SHADE);
     }
   }
