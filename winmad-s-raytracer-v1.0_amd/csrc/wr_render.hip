@@ -63,6 +63,8 @@ constexpr int kGroup = WR_GROUP;
 
 enum SqKind { SQ_SPLAT = 0, SQ_CONN = 1, SQ_NEE = 2, SQ_DIB = 3 };
 enum DiFlag { DI_NEE = 1, DI_BSDF = 2, DI_EARLY = 4 };
+// DI record state word: rays still to resolve (low byte) | results
+enum DiState { DI_COUNT = 0xff, DI_VIS = 0x100, DI_SAME = 0x200 };
 
 // Queue counters of one iteration / sample, one slot per step, cleared by a
 // single memset at its start (no per-bounce counter resets).  BDPT: light
@@ -204,11 +206,19 @@ struct BdptBuf {
   float *q_o[2], *q_d[2], *q_t[2];
   int *q_path[2], *q_prim[2];
   // shadow + aux closest-hit queue (splat / connection / NEE / DI-BSDF)
-  float *s_o, *s_d, *s_tgt, *s_val, *s_t;
-  int *s_meta, *s_pix, *s_prim;
+  // shadow / aux queue and DI records, two each: the ones of step `slot` are
+  // [slot & 1], so a step's resolve and the next step's vertex shading (which
+  // writes [(slot + 1) & 1]) can run in one launch
+  struct Sq {
+    float *o, *d, *tgt, *val, *t;
+    int *meta, *pix, *prim;
+  } sq[2];
+  struct Di {
+    float *nee, *neew, *bsdf, *thr, *wlen;
+    int *flags, *light, *pix;
+    int* state;  // rays still to resolve | DI_VIS | DI_SAME (one atomic per resolved ray)
+  } di[2];
   // direct-illumination records (getDirectIllumination, :484-608)
-  float *di_nee, *di_neew, *di_bsdf, *di_thr, *di_wlen;
-  int *di_flags, *di_light, *di_pix, *di_vis, *di_same, *di_list;
 };
 
 struct BdptArgs {
@@ -405,12 +415,13 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
     }
     const int si = wave_append(&A.sc->sq[kCamSlot], splat);  // traced with the camera primaries
     if (splat) {
-      st3(B.s_o, B.cap_sq, si, s_o);
-      st3(B.s_d, B.cap_sq, si, s_d);
-      st3(B.s_tgt, B.cap_sq, si, S.cam.pos);
-      st3(B.s_val, B.cap_sq, si, s_val);
-      B.s_meta[si] = SQ_SPLAT << 30;
-      B.s_pix[si] = s_pix;
+      const BdptBuf::Sq& Q = B.sq[kCamSlot & 1];
+      st3(Q.o, B.cap_sq, si, s_o);
+      st3(Q.d, B.cap_sq, si, s_d);
+      st3(Q.tgt, B.cap_sq, si, S.cam.pos);
+      st3(Q.val, B.cap_sq, si, s_val);
+      Q.meta[si] = SQ_SPLAT << 30;
+      Q.pix[si] = s_pix;
     }
   }
 }
@@ -462,18 +473,19 @@ __global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptGroup G_) {
 
 // One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
 // connections (shadow rays queued), scattering.
-__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptGroup G_, int slot) {
-  const BdptArgs& A = G_.a[blockIdx.y];
+__device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, int bid, int nblk) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;
   const int n = A.sc->ext[slot];
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
-  const int gstride = gridDim.x * blockDim.x;
+  if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
+  const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
   const float lpp = 1.f / static_cast<float>(S.nlights);
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
-    bool live = false, ext = false, conn_phase = false, nee = false, dib = false, di = false;
+  const BdptBuf::Sq& Q = B.sq[(slot + 1) & 1];  // rays traced at the next step
+  const BdptBuf::Di& D = B.di[(slot + 1) & 1];
+  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    bool live = false, ext = false, conn_phase = false, nee = false, dib = false;
     int p = -1, pix = -1, nv = 0, len = 0, nspec = 0, cnspec = 0;
     V3 hp{}, thr{}, cthr{}, e_o{}, e_d{}, nee_tgt{}, nee_d{}, dib_o{}, dib_d{};
     float dvcm = 0.f, dvc = 0.f, cdvcm = 0.f, cdvc = 0.f;
@@ -523,7 +535,6 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptG
             live = true;
             Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), B.c_ctr[p]};
             if (!b.delta && len_ok(A.ctl, len + 1)) {  // getDirectIllumination (:205-217, :484-608)
-              di = true;
               const float wlen = 1.f / (static_cast<float>(len) + 1.f - static_cast<float>(nspec));
               const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
               const DLight L = S.lights[lid];
@@ -576,16 +587,20 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptG
                   if (!black(illu2)) bsdf_val = div_plain(mul(illu2, bf2) * cos_s, dpdf2) * w;
                 }
               }
-              B.di_flags[p] = flags;
-              st3(B.di_nee, P, p, nee_val);
-              B.di_neew[p] = nee_w;
-              st3(B.di_bsdf, P, p, bsdf_val);
-              st3(B.di_thr, P, p, thr);
-              B.di_wlen[p] = wlen;
-              B.di_light[p] = lid;
-              B.di_pix[p] = pix;
-              B.di_vis[p] = 0;
-              B.di_same[p] = 0;
+              // a record only when a ray will be resolved: with neither the NEE
+              // nor the BSDF ray the contribution is exactly zero (:533-607)
+              const int nrays = (nee ? 1 : 0) + (dib ? 1 : 0);
+              if (nrays > 0) {
+                D.flags[p] = flags;
+                st3(D.nee, P, p, nee_val);
+                D.neew[p] = nee_w;
+                st3(D.bsdf, P, p, bsdf_val);
+                st3(D.thr, P, p, thr);
+                D.wlen[p] = wlen;
+                D.light[p] = lid;
+                D.pix[p] = pix;
+                D.state[p] = nrays;
+              }
             }
             if (!b.delta) {
               conn_phase = true;
@@ -608,22 +623,20 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptG
     }
     // DI queue entries
     {
-      const int di_i = wave_append(&A.sc->di[slot + 1], di);
-      if (di) B.di_list[di_i] = p;
       const int ni = wave_append(&A.sc->sq[slot + 1], nee);
       if (nee) {
-        st3(B.s_o, cap, ni, hp);
-        st3(B.s_d, cap, ni, nee_d);
-        st3(B.s_tgt, cap, ni, nee_tgt);
-        B.s_meta[ni] = (SQ_NEE << 30) | p;
-        B.s_pix[ni] = pix;
+        st3(Q.o, cap, ni, hp);
+        st3(Q.d, cap, ni, nee_d);
+        st3(Q.tgt, cap, ni, nee_tgt);
+        Q.meta[ni] = (SQ_NEE << 30) | p;
+        Q.pix[ni] = pix;
       }
       const int bi = wave_append(&A.sc->sq[slot + 1], dib);
       if (dib) {
-        st3(B.s_o, cap, bi, dib_o);
-        st3(B.s_d, cap, bi, dib_d);
-        B.s_meta[bi] = (SQ_DIB << 30) | p;
-        B.s_pix[bi] = pix;
+        st3(Q.o, cap, bi, dib_o);
+        st3(Q.d, cap, bi, dib_d);
+        Q.meta[bi] = (SQ_DIB << 30) | p;
+        Q.pix[bi] = pix;
       }
     }
     // vertex connections to the paired light subpath (:219-257)
@@ -689,12 +702,12 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptG
         }
         const int si = wave_append(&A.sc->sq[slot + 1], shoot);
         if (shoot) {
-          st3(B.s_o, cap, si, hp);
-          st3(B.s_d, cap, si, sdir);
-          st3(B.s_tgt, cap, si, stgt);
-          st3(B.s_val, cap, si, sval);
-          B.s_meta[si] = (SQ_CONN << 30) | p;
-          B.s_pix[si] = pix;
+          st3(Q.o, cap, si, hp);
+          st3(Q.d, cap, si, sdir);
+          st3(Q.tgt, cap, si, stgt);
+          st3(Q.val, cap, si, sval);
+          Q.meta[si] = (SQ_CONN << 30) | p;
+          Q.pix[si] = pix;
         }
       }
     }
@@ -717,39 +730,65 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_shade(BdptG
 }
 
 // Light-tracing splats and camera-pass shadow / aux rays after traversal.
-__global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptGroup G_, int slot) {
-  const BdptArgs& A = G_.a[blockIdx.y];
+// Light-tracing splats and camera-pass shadow / aux rays of step `slot` after
+// traversal.  A DI record is finalized (getDirectIllumination's combination,
+// :533-607) by whichever of its rays is resolved last: each resolve adds
+// (its result bit - 1) to the record's state word in one atomic.
+__device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int bid, int nblk) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
-  const int n = A.sc->sq[slot], cap = B.cap_sq;
-  const int gstride = gridDim.x * blockDim.x;
+  const BdptBuf::Sq& Q = B.sq[slot & 1];
+  const BdptBuf::Di& D = B.di[slot & 1];
+  const int n = A.sc->sq[slot], cap = B.cap_sq, P = A.P;
+  const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
     bool is_shadow = false, is_closest = false;
     if (j < n) {
-      const int meta = B.s_meta[j];
+      const int meta = Q.meta[j];
       const int kind = (meta >> 30) & 3, p = meta & 0x3fffffff;
-      const int prim = B.s_prim[j];
-      const float t = B.s_t[j];
+      const int prim = Q.prim[j];
+      const float t = Q.t[j];
+      int di_bits = -1;  // >= 0: this ray belongs to DI record p
       if (kind == SQ_DIB) {  // DI BSDF-sampled ray: same light? (:570-596)
         is_closest = true;
-        int same = 0;
+        bool same = false;
         if (prim >= 0) {
           const int m = S.prim_mat[prim];
-          same = (m < 0 && -m - 1 == B.di_light[p]) ? 1 : 0;
+          same = m < 0 && -m - 1 == D.light[p];
         }
-        B.di_same[p] = same;
+        di_bits = same ? DI_SAME : 0;
       } else {  // Scene::occluded: position equality (scene.cpp:55-69)
         is_shadow = true;
         bool unocc = true;
         if (prim >= 0) {
-          const V3 o = ld3(B.s_o, cap, j), d = ld3(B.s_d, cap, j);
-          unocc = near_eq(o + d * t, ld3(B.s_tgt, cap, j));
+          const V3 o = ld3(Q.o, cap, j), d = ld3(Q.d, cap, j);
+          unocc = near_eq(o + d * t, ld3(Q.tgt, cap, j));
         }
         if (kind == SQ_NEE) {
-          B.di_vis[p] = unocc ? 1 : 0;
+          di_bits = unocc ? DI_VIS : 0;
         } else if (unocc) {
-          film_add(A.film, B.s_pix[j], ld3(B.s_val, cap, j));
+          film_add(A.film, Q.pix[j], ld3(Q.val, cap, j));
+        }
+      }
+      if (di_bits >= 0) {
+        const int st = atomicAdd(&D.state[p], di_bits - 1) + di_bits - 1;
+        if ((st & DI_COUNT) == 0) {
+          const int flags = D.flags[p];
+          V3 res = v3(0.f, 0.f, 0.f);
+          float weight = 0.f;
+          if ((flags & DI_NEE) && (st & DI_VIS)) {
+            weight = D.neew[p];
+            res = res + ld3(D.nee, P, p);
+          }
+          V3 di;
+          if (flags & DI_EARLY) {
+            di = res;
+          } else {
+            if ((flags & DI_BSDF) && (st & DI_SAME)) res = res + ld3(D.bsdf, P, p);
+            di = res * weight;
+          }
+          film_add(A.film, D.pix[p], mul(ld3(D.thr, P, p), di) * D.wlen[p]);
         }
       }
     }
@@ -758,30 +797,17 @@ __global__ void __launch_bounds__(kShadeBlock) k_sq_resolve(BdptGroup G_, int sl
   }
 }
 
-// getDirectIllumination's final combination (:533-607)
-__global__ void __launch_bounds__(kShadeBlock) k_di_finalize(BdptGroup G_, int slot) {
+// One camera-pass step after its traversal: resolve the step's shadow / aux
+// rays (blocks [0, nres)) and shade its camera vertices (the rest) -- they touch
+// different queue / DI buffers.  The last step has no vertices (shade = 0).
+__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_step(BdptGroup G_, int slot, int nres,
+                                                                         int shade) {
   const BdptArgs& A = G_.a[blockIdx.y];
-  const BdptBuf& B = A.B;
-  const int n = A.sc->di[slot], P = A.P;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    const int p = B.di_list[j];
-    const int flags = B.di_flags[p];
-    V3 res = v3(0.f, 0.f, 0.f);
-    float weight = 0.f;
-    if ((flags & DI_NEE) && B.di_vis[p]) {
-      weight = B.di_neew[p];
-      res = res + ld3(B.di_nee, P, p);
-    }
-    V3 di;
-    if (flags & DI_EARLY) {
-      di = res;
-    } else {
-      if ((flags & DI_BSDF) && B.di_same[p]) res = res + ld3(B.di_bsdf, P, p);
-      di = res * weight;
-    }
-    film_add(A.film, B.di_pix[p], mul(ld3(B.di_thr, P, p), di) * B.di_wlen[p]);
-  }
+  if (static_cast<int>(blockIdx.x) < nres) sq_resolve_body(A, slot, blockIdx.x, nres);
+  else if (shade) camera_shade_body(A, slot, blockIdx.x - nres, gridDim.x - nres);
 }
+
+// getDirectIllumination's final combination (:533-607)
 
 // =============================================================== PT
 struct PtBuf {
@@ -1109,25 +1135,27 @@ void layout_bdpt(Arena& a, BdptBuf& B, int P) {
     B.q_path[q] = a.take<int>(sP);
     B.q_prim[q] = a.take<int>(sP);
   }
-  B.s_o = a.take<float>(3 * sQ);
-  B.s_d = a.take<float>(3 * sQ);
-  B.s_tgt = a.take<float>(3 * sQ);
-  B.s_val = a.take<float>(3 * sQ);
-  B.s_t = a.take<float>(sQ);
-  B.s_meta = a.take<int>(sQ);
-  B.s_pix = a.take<int>(sQ);
-  B.s_prim = a.take<int>(sQ);
-  B.di_nee = a.take<float>(3 * sP);
-  B.di_neew = a.take<float>(sP);
-  B.di_bsdf = a.take<float>(3 * sP);
-  B.di_thr = a.take<float>(3 * sP);
-  B.di_wlen = a.take<float>(sP);
-  B.di_flags = a.take<int>(sP);
-  B.di_light = a.take<int>(sP);
-  B.di_pix = a.take<int>(sP);
-  B.di_vis = a.take<int>(sP);
-  B.di_same = a.take<int>(sP);
-  B.di_list = a.take<int>(sP);
+  for (int k = 0; k < 2; ++k) {
+    BdptBuf::Sq& q = B.sq[k];
+    q.o = a.take<float>(3 * sQ);
+    q.d = a.take<float>(3 * sQ);
+    q.tgt = a.take<float>(3 * sQ);
+    q.val = a.take<float>(3 * sQ);
+    q.t = a.take<float>(sQ);
+    q.meta = a.take<int>(sQ);
+    q.pix = a.take<int>(sQ);
+    q.prim = a.take<int>(sQ);
+    BdptBuf::Di& d = B.di[k];
+    d.nee = a.take<float>(3 * sP);
+    d.neew = a.take<float>(sP);
+    d.bsdf = a.take<float>(3 * sP);
+    d.thr = a.take<float>(3 * sP);
+    d.wlen = a.take<float>(sP);
+    d.flags = a.take<int>(sP);
+    d.light = a.take<int>(sP);
+    d.pix = a.take<int>(sP);
+    d.state = a.take<int>(sP);
+  }
 }
 
 void layout_pt(Arena& a, PtBuf& T, int P) {
@@ -1761,8 +1789,8 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
       A[m].iter = static_cast<uint32_t>(prm->iter_begin + it0 + m);
     }
     auto sq = [&](int m, int slot) {
-      const BdptBuf& B = pp.bb[m];
-      return rq(B.s_o, B.s_d, B.cap_sq, &pp.sc[m].sq[slot], B.s_t, B.s_prim);
+      const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
+      return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim);
     };
     auto ext = [&](int m, int slot) {
       const BdptBuf& B = pp.bb[m];
@@ -1794,11 +1822,10 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
       if (more)
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
       trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays);
-      hipLaunchKernelGGL(k_sq_resolve, dim3(shade_grid(c, sq_max), gn), dim3(kShadeBlock), 0, sm, GA, slot);
-      if (b > 0) hipLaunchKernelGGL(k_di_finalize, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, slot);
-      tm.mark(WR_K_RESOLVE);
-      if (!more) break;
-      hipLaunchKernelGGL(k_camera_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, slot);
+      // resolve this step's shadow / aux rays and shade its vertices in one launch
+      const int nres = shade_grid(c, sq_max);
+      hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot, nres,
+                         more ? 1 : 0);
       tm.mark(WR_K_SHADE);
     }
   }
