@@ -122,7 +122,7 @@ void wr_destroy(wr_context* ctx);
 /* Concurrent render pipelines (HIP streams, each with its own work buffers):
  * iterations / samples are dealt round-robin to them so that one stream's
  * late-bounce traversal tail overlaps another's full launches.  1..4, default
- * 3 (env WR_PIPES).  GPU-specific scheduling; no reference counterpart. */
+ * 4 (env WR_PIPES).  GPU-specific scheduling; no reference counterpart. */
 int wr_set_pipelines(wr_context* ctx, int n);
 
 /* ---- traversal ---- */
