@@ -128,7 +128,8 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 // =============================================================== trace kernels
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
 template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
-__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
+// 4 waves/SIMD (<= 128 VGPRs) to match the LDS-limited 16 waves/CU
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
   extern __shared__ uint32_t smem[];
   TraceCounters tc{0, 0, 0};
   trace_queue<COUNT, SPH, NARROW, STAMP>(S, Q, fetch, smem, tc, ctr->stamps);
