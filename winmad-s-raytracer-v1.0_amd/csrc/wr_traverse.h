@@ -192,7 +192,11 @@ struct TraceQueues {
 //   own    leaf id of each pair of the batch (bytes)
 //   owner  per ray: (min hit key, smallest prim at it) and (min hit key, largest
 //          prim at it) as 64-bit atomics, + a flag for hits in (min, min + 2 EPS]
-constexpr int kPairBatch = 256;
+#ifndef WR_PAIR_BATCH
+#define WR_PAIR_BATCH 256
+#endif
+constexpr int kPairBatch = WR_PAIR_BATCH;  // multiple of 256
+static_assert(kPairBatch % 256 == 0, "the owner-table scan covers 4 bytes per lane per 256 slots");
 #ifndef WR_LEAVES_PER_ROUND
 #define WR_LEAVES_PER_ROUND 4
 #endif
@@ -499,7 +503,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
       const int lim = min(total - base, kPairBatch);
       const int k0 = max(excl, base), k1 = min(excl + count, base + lim);
       __syncthreads();
-      own32[lane] = 0u;
+#pragma unroll
+      for (int k = 0; k < kPairBatch / 256; ++k) own32[lane * (kPairBatch / 256) + k] = 0u;
       olo[lane] = ~0ull;
       ohi[lane] = 0ull;
       onear[lane] = 0;
@@ -517,12 +522,25 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
       }
       __syncthreads();
       {
-        const uint32_t w = own32[lane];
-        const uint32_t m0 = w & 0xffu, m1 = max(m0, (w >> 8) & 0xffu), m2 = max(m1, (w >> 16) & 0xffu),
-                       m3 = max(m2, w >> 24);
-        const uint32_t run = static_cast<uint32_t>(wave_scan_max(static_cast<int>(m3)));
+        // lane covers slots [lane * kPairBatch / 64, (lane + 1) * kPairBatch / 64)
+        constexpr int kW = kPairBatch / 256;
+        uint32_t m[4 * kW];
+        uint32_t run = 0u;
+#pragma unroll
+        for (int k = 0; k < kW; ++k) {
+          const uint32_t w = own32[lane * kW + k];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            run = max(run, (w >> (8 * b)) & 0xffu);
+            m[4 * k + b] = run;
+          }
+        }
+        run = static_cast<uint32_t>(wave_scan_max(static_cast<int>(run)));
         const uint32_t prev = static_cast<uint32_t>(wave_shr1(static_cast<int>(run)));
-        own32[lane] = max(m0, prev) | (max(m1, prev) << 8) | (max(m2, prev) << 16) | (max(m3, prev) << 24);
+#pragma unroll
+        for (int k = 0; k < kW; ++k)
+          own32[lane * kW + k] = max(m[4 * k], prev) | (max(m[4 * k + 1], prev) << 8) |
+                                 (max(m[4 * k + 2], prev) << 16) | (max(m[4 * k + 3], prev) << 24);
       }
       __syncthreads();
       WR_STAMP(2)
