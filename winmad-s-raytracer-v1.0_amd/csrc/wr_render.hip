@@ -53,7 +53,16 @@ constexpr int kShadeBlock = 256;
 #ifndef WR_SHADE_WAVES
 #define WR_SHADE_WAVES 4
 #endif
-#define WR_SHADE_OCC __attribute__((amdgpu_waves_per_eu(WR_SHADE_WAVES, 8)))
+// Scalar fp32 instead of v_pk_mul/add_f32: the pairing costs more register moves
+// than it saves in this divergent, register-bound code (traversal 736 -> 791
+// Mrays/s).  Results are identical (both are IEEE single-precision).  A gfx950
+// target feature, so it is attached in the device pass only.
+#ifdef __HIP_DEVICE_COMPILE__
+#define WR_NO_PK_FP32 __attribute__((target("no-packed-fp32-ops")))
+#else
+#define WR_NO_PK_FP32
+#endif
+#define WR_SHADE_OCC __attribute__((amdgpu_waves_per_eu(WR_SHADE_WAVES, 8))) WR_NO_PK_FP32
 // Iterations / samples a pipeline advances in lockstep (see struct Pipe).  The
 // per-vertex kernels take the whole group (member = blockIdx.y).
 #ifndef WR_GROUP
@@ -129,7 +138,7 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
 template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
 // 4 waves/SIMD (<= 128 VGPRs) to match the LDS-limited 16 waves/CU
-__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32 k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
   extern __shared__ uint32_t smem[];
   TraceCounters tc{0, 0, 0};
   trace_queue<COUNT, SPH, NARROW, STAMP>(S, Q, fetch, smem, tc, ctr->stamps);
@@ -239,7 +248,7 @@ struct BdptGroup {
 __device__ __forceinline__ bool len_ok(int ctl, int L) { return ctl <= 0 || L == ctl; }
 
 // generateLightSample (:267-311) + the first extension ray
-__global__ void __launch_bounds__(kShadeBlock) k_light_gen(BdptGroup G_) {
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_light_gen(BdptGroup G_) {
   const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
   const int P = A.P;
@@ -428,7 +437,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
 }
 
 // generateCameraSample (:418-452) + first extension ray
-__global__ void __launch_bounds__(kShadeBlock) k_camera_gen(BdptGroup G_) {
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGroup G_) {
   const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
   const DCam& cam = A.S.cam;
@@ -835,7 +844,7 @@ struct PtGroup {
 };
 
 // SurfaceIntegrator::render per-sample setup (surfaceIntegrator.cpp:26-34)
-__global__ void __launch_bounds__(kShadeBlock) k_pt_gen(PtGroup G_) {
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_gen(PtGroup G_) {
   const PtArgs& A = G_.a[blockIdx.y];
   const PtBuf& T = A.T;
   const DCam& cam = A.S.cam;
@@ -865,7 +874,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_gen(PtGroup G_) {
 }
 
 // One PathIntegrator::raytracing iteration (pathIntegrator.cpp:43-146)
-__global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtGroup G_, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_shade(PtGroup G_, int slot) {
   const PtArgs& A = G_.a[blockIdx.y];
   const PtBuf& T = A.T;
   const DevScene& S = A.S;
@@ -975,7 +984,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_pt_shade(PtGroup G_, int slot) 
   }
 }
 
-__global__ void __launch_bounds__(kShadeBlock) k_pt_resolve(PtGroup G_, int slot) {
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_resolve(PtGroup G_, int slot) {
   const PtArgs& A = G_.a[blockIdx.y];
   const PtBuf& T = A.T;
   const int n = A.sc->sq[slot], P = A.P;
