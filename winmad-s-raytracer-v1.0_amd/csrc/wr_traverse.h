@@ -489,13 +489,16 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
     const int incl = wave_scan_add(count);
     const int excl = incl - count;
     const int total = __builtin_amdgcn_readlane(incl, 63);
-    for (int i = 0; i < nl; ++i) leaf_off[lane * kLeavesPerRound + i] += static_cast<PairIdx>(excl);
+#pragma unroll
+    for (int i = 0; i < kLeavesPerRound; ++i)  // nl <= kLeavesPerRound
+      if (i < nl) leaf_off[lane * kLeavesPerRound + i] += static_cast<PairIdx>(excl);
     rbest[lane] = t_best;
     // ref of pair k of the round, k in this lane's range [excl, excl + count)
     auto own_ref = [&](int k) -> uint32_t {
       int i = 0;
-      for (int x = 1; x < nl; ++x)
-        if (k >= static_cast<int>(leaf_off[lane * kLeavesPerRound + x])) i = x;
+#pragma unroll
+      for (int x = 1; x < kLeavesPerRound; ++x)
+        if (x < nl && k >= static_cast<int>(leaf_off[lane * kLeavesPerRound + x])) i = x;
       return leaf_first[lane * kLeavesPerRound + i] +
              static_cast<uint32_t>(k - static_cast<int>(leaf_off[lane * kLeavesPerRound + i]));
     };
@@ -513,11 +516,14 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
       // over the batch in slot order (leaf ids increase with the slot)
       if (k0 < k1) {
         int s0 = static_cast<int>(leaf_off[lane * kLeavesPerRound]);
-        for (int i = 0; i < nl; ++i) {
-          const int s1 = i + 1 < nl ? static_cast<int>(leaf_off[lane * kLeavesPerRound + i + 1]) : excl + count;
-          const int a0 = max(s0, base), a1 = min(s1, base + lim);
-          if (a0 < a1) own[a0 - base] = static_cast<uint8_t>(lane * kLeavesPerRound + i);
-          s0 = s1;
+#pragma unroll
+        for (int i = 0; i < kLeavesPerRound; ++i) {
+          if (i < nl) {
+            const int s1 = i + 1 < nl ? static_cast<int>(leaf_off[lane * kLeavesPerRound + i + 1]) : excl + count;
+            const int a0 = max(s0, base), a1 = min(s1, base + lim);
+            if (a0 < a1) own[a0 - base] = static_cast<uint8_t>(lane * kLeavesPerRound + i);
+            s0 = s1;
+          }
         }
       }
       __syncthreads();
