@@ -348,16 +348,20 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
     const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
     const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
     const float t = (split - oa) * ia;
-    const bool below = (oa < split) || (oa == split && da <= 0);
+    // predicates combined bitwise: one branch (the push) instead of a branch
+    // per short-circuit
+    const bool below = (oa < split) | ((oa == split) & (da <= 0));
     const uint32_t left = at + 1, right = w.y >> 2;
     const uint32_t nearc = below ? left : right, farc = below ? right : left;
-    if (t > tmax || t <= 0) return nearc;
-    if (t < tmin) return farc;
-    stk_node[sp * 64] = static_cast<NodeIdx>(farc);
-    stk_tmin[sp * 64] = t;
-    ++sp;
-    tmax = t;
-    return nearc;
+    const bool go_near = (t > tmax) | (t <= 0);
+    const bool go_far = !go_near & (t < tmin);
+    if (!go_near & !go_far) {
+      stk_node[sp * 64] = static_cast<NodeIdx>(farc);
+      stk_tmin[sp * 64] = t;
+      ++sp;
+      tmax = t;
+    }
+    return go_far ? farc : nearc;
   };
   // t of one (ray, primitive) pair, NaN when Triangle::hit / Sphere::hit reject it
   // or (triangles) when it cannot beat `screen`, the ray's best at round start
