@@ -227,3 +227,22 @@ def test_pipeline_count_does_not_change_the_render(pipes):
     assert np.allclose(pgot, pref, rtol=1e-4, atol=1e-6)
     with pytest.raises(native.WrError):
         c.set_pipelines(0)
+
+
+@pytest.mark.parametrize("mode,W,H", [("-bpt", 64, 64), ("-p", 64, 48)])
+def test_cli_renders_like_the_reference_main(mode, W, H, tmp_path):
+    """wr_tot (the C++ mirror of main.cpp's -bpt / -p branches) end to end on the GPU."""
+    import subprocess
+    scene = _scenes.torus(W, H) if mode == "-bpt" else _scenes.cbox(W, H)
+    para = tmp_path / "p.para"  # parameters.para: depth, spp, light / hemisphere samples, W, H, phong, lights
+    para.write_text(f"#\n7\n#\n4\n8\n4\n{W}\n{H}\n5\n400\n")
+    out = tmp_path / "o.ppm"
+    r = subprocess.run([os.path.join(native.PKG_DIR, "wr_tot"), scene, str(out), mode, "--params", str(para),
+                        "--iterations", "2"], capture_output=True, text=True, cwd=tmp_path, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Mrays/s" in r.stdout
+    data = out.read_bytes()
+    header = f"P6\n{W} {H}\n255\n".encode()
+    assert data.startswith(header) and len(data) == len(header) + W * H * 3
+    assert max(data[len(header):]) > 0
+    assert (tmp_path / "time.txt").exists()
