@@ -26,10 +26,16 @@ import sys
 import tempfile
 import time
 
+# At least 8 hardware queues for this process (HIP's default, and the GPU
+# box's environment, is 4) so that the library runs 8 concurrent render
+# pipelines; must be set before HIP initialises.  DESIGN.md section 4.
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)))
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "winmad-s-raytracer-v1.0_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2, 8 XCDs x 4 MiB, ~34.5 TB/s aggregate
 # HBM bytes per k_trace launch from the PMC passes of the same bench command
 # (scripts/profile_round.sh + scripts/summarize_profile.py; counters cannot be
 # read from inside the timed run)
@@ -194,7 +200,10 @@ def main():
                     "launches": int(trace_launches),
                     "tests_per_ray": round(cst.prim_refs / rays, 2),
                     "nodes_per_ray": round((cst.inner_visits + cst.leaf_visits) / rays, 2),
-                    "trace_share_of_wall": round(st.trace_wall_ms / 1e3 / max(1e-9, elapsed), 3)}
+                    "trace_share_of_wall": round(st.trace_wall_ms / 1e3 / max(1e-9, elapsed), 3),
+                    # a scene that fits L2 / Infinity Cache is read from there, not HBM
+                    # (traffic << algorithmic bytes): the L2 peak is the tighter ceiling
+                    "l2_peak": L2_PEAK_GBS, "l2_frac": round(achieved / L2_PEAK_GBS, 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -215,7 +224,8 @@ def main():
             "config": {"workload": f"{cfg['desc']} {W}x{H}, {K} {unit_name} per GPU"
                                    + ("" if pt else ", controlLength 3, maxPathLength 10"),
                        "scene_config": args.config.upper(), "width": W, "height": H,
-                       "steps_per_gpu": K, "parallelism": f"sample-batch x{world}"},
+                       "steps_per_gpu": K, "parallelism": f"sample-batch x{world}",
+                       "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
             "spp_per_sec": round(W * H * K * world / elapsed, 1),
             "rays_per_step": round(total_rays / (K * world)),
             "roofline": roofline, "cpu_baseline": cpu,

@@ -119,10 +119,12 @@ void wr_scene_free(wr_scene* scene);
 int wr_device_count(void);
 int wr_create(const wr_scene* scene, int hip_device, wr_context** out);
 void wr_destroy(wr_context* ctx);
-/* Concurrent render pipelines (HIP streams, each with its own work buffers):
- * iterations / samples are dealt round-robin to them so that one stream's
- * late-bounce traversal tail overlaps another's full launches.  1..4, default
- * 4 (env WR_PIPES).  GPU-specific scheduling; no reference counterpart. */
+/* Concurrent render pipelines (HIP streams, each with its own work buffers,
+ * ~5 GB per pair of iterations at 1080p): iterations / samples are dealt
+ * round-robin to them so that one stream's late-bounce traversal tail overlaps
+ * another's full launches.  1..16; default = the process's hardware queues
+ * (GPU_MAX_HW_QUEUES, HIP default 4) up to 8, or env WR_PIPES.
+ * GPU-specific scheduling; no reference counterpart. */
 int wr_set_pipelines(wr_context* ctx, int n);
 
 /* ---- traversal ---- */

@@ -1060,7 +1060,7 @@ size_t measure(Fn fn) {  // bytes an arena layout needs
 // launches (a launch lasts as long as its slowest ray) overlaps the full
 // launches of another.  The film is a sum, so the result does not depend on the
 // pipeline count (up to the order of float atomics).
-constexpr int kMaxPipes = 4;
+constexpr int kMaxPipes = 16;
 // Each pipeline advances a group of up to kGroup iterations / samples in
 // lockstep: every traversal launch takes the queues of all of them, so the
 // launch tail (its slowest ray) is paid once per group.
@@ -1084,7 +1084,9 @@ struct wr_context {
   int device = 0;
   hipStream_t stream = nullptr;  // API traversal, film set-up / return, joins the pipelines
   Pipe pipes[kMaxPipes];
-  int npipes = 4;  // torus 1080p BDPT, groups of 2: 3 pipelines 707, 4 -> 734 Mrays/s
+  // torus 1080p BDPT, groups of 2 (Mrays/s): 4 pipelines / 4 queues 832,
+  // 8 / 8 -> 864, 16 / 16 -> 894 (twice the memory of 8: ~5 GB per buffer set)
+  int npipes = 4;
   hipEvent_t t_ref = nullptr;  // start of the current render (pipelines wait on it)
   DevScene ds{};
   Arena scene_mem;
@@ -1485,6 +1487,14 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       return fail(WR_E_HIP, "pipeline stream / counters");
     }
   }
+  // one pipeline per hardware queue of this process (HIP's GPU_MAX_HW_QUEUES,
+  // default 4; pipeline 0 shares the context stream), at most 8: streams that
+  // share a hardware queue serialize behind each other
+  {
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
+    c->npipes = std::max(1, std::min(8, hwq));
+  }
   if (const char* e = std::getenv("WR_PIPES")) c->npipes = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->grid = std::max(256, prop.multiProcessorCount * 8);
@@ -1656,7 +1666,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
 }
 
 int wr_set_pipelines(wr_context* c, int n) {
-  if (!c || n < 1 || n > kMaxPipes) return fail(WR_E_ARG, "pipelines must be in 1..4");
+  if (!c || n < 1 || n > kMaxPipes) return fail(WR_E_ARG, "pipelines must be in 1..8");
   c->npipes = n;
   return WR_OK;
 }
