@@ -1217,6 +1217,39 @@ int ensure_work(Pipe& p, int kind, int P, int sets) {
   return WR_OK;
 }
 
+// Work buffers for up to `want` pipelines, each with `sets` buffer sets (~2.5 KB
+// per path for BDPT), kept within 3/4 of the device memory free now plus what
+// the pipelines already hold: big films degrade to fewer pipelines instead of
+// failing.  Every render lays out full groups on all pipelines that fit, so a
+// short render (a warm-up) leaves the buffers of a long one in place.
+int pipelines_that_fit(wr_context* c, int kind, int P, int sets, int want) {
+  const size_t per = kind == 1 ? measure([&](Arena& a) {
+    for (int g = 0; g < sets; ++g) {
+      BdptBuf b;
+      layout_bdpt(a, b, P);
+    }
+  })
+                               : measure([&](Arena& a) {
+                                   for (int g = 0; g < sets; ++g) {
+                                     PtBuf t;
+                                     layout_pt(a, t, P);
+                                   }
+                                 });
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return want;
+  size_t held = 0;
+  for (int i = 0; i < kMaxPipes; ++i) held += c->pipes[i].work.cap;
+  const size_t budget = (free_b + held) / 4 * 3;
+  const int fit = static_cast<int>(std::min<size_t>(static_cast<size_t>(want), std::max<size_t>(1, budget / per)));
+  for (int i = fit; i < kMaxPipes; ++i) {  // memory-limited: free the rest
+    c->pipes[i].work.release();
+    c->pipes[i].work_kind = 0;
+  }
+  for (int i = 0; i < fit; ++i)
+    if (ensure_work(c->pipes[i], kind, P, sets) != WR_OK) return 0;
+  return fit;
+}
+
 // ---- launch helpers with optional per-launch HIP events (on the pipeline's stream)
 struct Timer {
   wr_context* c;
@@ -1785,10 +1818,9 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
   const double t0 = host_now();
   const int P = prm->width * prm->height;
   const int ngroups = (prm->iterations + kGroup - 1) / kGroup;
-  const int np = std::max(1, std::min(c->npipes, ngroups));
-  const int sets = std::max(1, std::min(kGroup, prm->iterations));
-  for (int i = 0; i < np; ++i)
-    if (int rc = ensure_work(c->pipes[i], 1, P, sets)) return rc;
+  const int fit = pipelines_that_fit(c, 1, P, kGroup, c->npipes);
+  if (fit < 1) return WR_E_HIP;  // message set by the allocation
+  const int np = std::max(1, std::min(fit, ngroups));
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
@@ -1879,10 +1911,9 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
   const int k1 = prm->sample_count > 0 ? k0 + prm->sample_count : prm->spp;
   const int nk = std::max(0, k1 - k0);
   const int ngroups = (nk + kGroup - 1) / kGroup;
-  const int np = std::max(1, std::min(c->npipes, ngroups));
-  const int sets = std::max(1, std::min(kGroup, nk));
-  for (int i = 0; i < np; ++i)
-    if (int rc = ensure_work(c->pipes[i], 2, P, sets)) return rc;
+  const int fit = pipelines_that_fit(c, 2, P, kGroup, c->npipes);
+  if (fit < 1) return WR_E_HIP;  // message set by the allocation
+  const int np = std::max(1, std::min(fit, ngroups));
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
