@@ -20,3 +20,7 @@ def torus(W, H, mode="bdpt"):
 
 def cbox(W, H, mode="pt"):
     return path(f"cbox_{W}x{H}_{mode}.scene", scenes.cbox_scene(W, H, mode))
+
+
+def spheres(W, H, mode="bdpt"):
+    return path(f"spheres_{W}x{H}_{mode}.scene", scenes.spheres_scene(W, H, mode))

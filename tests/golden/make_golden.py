@@ -76,6 +76,7 @@ def main():
         "torus64": (scenes.torus_scene(64, 64), scenes.params_text(64, 64)),
         "torus256": (scenes.torus_scene(256, 256), scenes.params_text(256, 256)),
         "cbox64x48": (scenes.cbox_scene(64, 48), scenes.params_text(64, 48, 7, 16)),
+        "spheres64": (scenes.spheres_scene(64, 64), scenes.params_text(64, 64, 7, 4)),
     }
     for name, (sc, pa) in cases.items():
         sp = scenes.write(os.path.join(tmp, name + ".scene"), sc)
@@ -93,6 +94,10 @@ def main():
         if name == "torus256":
             continue
         corpus = ray_corpus(dump, 2048 if name == "torus64" else 1024, 99)
+        if name == "spheres64":  # aim half of the random rays at the spheres
+            c = np.array([[-0.5, 0.3, -0.82], [0.55, 0.6, -0.86], [0.05, -0.45, -1.0]], np.float32)
+            k = np.arange(512, 1024, 2)
+            corpus[k, 3:6] = c[k % 3] - corpus[k, 0:3]
         cp = os.path.join(HERE, f"rays_{name}.f32")
         corpus.tofile(cp)
         # second pass: every other hitting ray gets its own hit point as the
@@ -124,6 +129,10 @@ def main():
     }
     sp, pp = os.path.join(tmp, "cbox64x48.scene"), os.path.join(tmp, "cbox64x48.para")
     refdrv("pt", sp, pp, 5489, os.path.join(HERE, "pt_cbox64x48_spp16_s5489.f32"), cwd=tmp)
+    # spheres: Sphere::hit and the specular (glass / mirror) BSDF branches
+    sp, pp = os.path.join(tmp, "spheres64.scene"), os.path.join(tmp, "spheres64.para")
+    refdrv("bdpt", sp, pp, 2, 5489, os.path.join(HERE, "bdpt_spheres64_i2_s5489.f32"), cwd=tmp)
+    refdrv("pt", sp, pp, 5489, os.path.join(HERE, "pt_spheres64_spp4_s5489.f32"), cwd=tmp)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print(json.dumps({k: v for k, v in meta.items() if "block32_mean" not in v}, indent=1))

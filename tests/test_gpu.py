@@ -41,7 +41,8 @@ def normalize_f32(d):
 
 
 @pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),
-                                        ("cbox64x48", lambda: _scenes.cbox(64, 48))])
+                                        ("cbox64x48", lambda: _scenes.cbox(64, 48)),
+                                        ("spheres64", lambda: _scenes.spheres(64, 64))])
 def test_trace_closest_bit_exact_vs_reference(name, maker):
     c = ctx(maker())
     rays = np.fromfile(os.path.join(GOLD, f"rays_{name}.f32"), np.float32).reshape(-1, 9)
@@ -246,3 +247,19 @@ def test_cli_renders_like_the_reference_main(mode, W, H, tmp_path):
     assert data.startswith(header) and len(data) == len(header) + W * H * 3
     assert max(data[len(header):]) > 0
     assert (tmp_path / "time.txt").exists()
+
+
+def test_spheres_bdpt_and_pt_match_oracle_counter_rng():
+    """The SPH traversal variant, Sphere::hit and the glass / mirror BSDF branches."""
+    path = _scenes.spheres(64, 64)
+    film, st = ctx(path).render_bdpt(64, 64, iterations=4, seed=5489)
+    ref, rst = _oracle.Scene(path).bdpt(64, 64, 4, 5489, mode=1)
+    rmse, rms, ch = film_err(film, ref)
+    assert rmse / rms < 1e-2, (rmse, rms)
+    assert np.all(ch < 1e-3), ch
+    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+    film, st = ctx(path).render_path(64, 64, spp=16, max_depth=7, seed=5489)
+    ref, rst = _oracle.Scene(path).pt(64, 64, 16, 7, 5489, mode=1)
+    rmse, rms, _ = film_err(film * np.float32(1.0 / 16), ref)
+    assert rmse / rms < 1e-2, (rmse, rms)
+    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays

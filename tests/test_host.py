@@ -30,7 +30,8 @@ def test_library_exports_every_declared_symbol():
 
 @pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),
                                         ("torus256", lambda: _scenes.torus(256, 256)),
-                                        ("cbox64x48", lambda: _scenes.cbox(64, 48))])
+                                        ("cbox64x48", lambda: _scenes.cbox(64, 48)),
+                                        ("spheres64", lambda: _scenes.spheres(64, 64))])
 def test_product_loader_and_kdtree_match_reference(name, maker, tmp_path):
     """wr_scene_load == Scene::init of the reference (scene.cpp:259-489,
     KDtreeAccel.cpp:12-307): identical triangles, lights, camera matrices and tree."""

@@ -32,7 +32,8 @@ def test_mt19937_matches_reference(seed):
 
 @pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),
                                         ("torus256", lambda: _scenes.torus(256, 256)),
-                                        ("cbox64x48", lambda: _scenes.cbox(64, 48))])
+                                        ("cbox64x48", lambda: _scenes.cbox(64, 48)),
+                                        ("spheres64", lambda: _scenes.spheres(64, 64))])
 def test_scene_and_kdtree_dump_bit_exact(name, maker, tmp_path):
     """Loader (scene.cpp:259-467 + tinyobj), camera matrices (camera.cpp:3-29) and
     the whole KD tree incl. leaf order (KDtreeAccel.cpp:12-307) hash-equal."""
@@ -60,7 +61,8 @@ def parse_rays(path):
 
 
 @pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),
-                                        ("cbox64x48", lambda: _scenes.cbox(64, 48))])
+                                        ("cbox64x48", lambda: _scenes.cbox(64, 48)),
+                                        ("spheres64", lambda: _scenes.spheres(64, 64))])
 def test_trace_corpus_bit_exact(name, maker):
     """Scene::intersect + Scene::occluded on the golden ray corpus."""
     s = _oracle.Scene(maker())
@@ -114,7 +116,8 @@ def test_kat_samplers():
 
 
 @pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),
-                                        ("cbox64x48", lambda: _scenes.cbox(64, 48))])
+                                        ("cbox64x48", lambda: _scenes.cbox(64, 48)),
+                                        ("spheres64", lambda: _scenes.spheres(64, 64))])
 def test_kat_bsdf_lights_camera(name, maker):
     """BSDF init/f/pdf/sample (bsdf.h:66-89, bsdf.cpp), AreaLight (light.cpp:4-100)
     and Camera (camera.cpp:31-42) known answers per material / light."""
@@ -187,6 +190,18 @@ def test_pt_film_mt_serial_bit_exact():
     s = _oracle.Scene(_scenes.cbox(64, 48))
     film, _ = s.pt(64, 48, 16, 7, 5489, mode=0)
     ref = np.fromfile(os.path.join(GOLD, "pt_cbox64x48_spp16_s5489.f32"), np.float32).reshape(48, 64, 3)
+    assert np.array_equal(film, ref)
+
+
+def test_spheres_bdpt_and_pt_films_mt_serial_bit_exact():
+    """Sphere::hit (sphere.cpp:17-78) and the glass / mirror BSDF branches, whole
+    renders against the reference's own films."""
+    s = _oracle.Scene(_scenes.spheres(64, 64))
+    film, _ = s.bdpt(64, 64, 2, 5489, mode=0)
+    ref = np.fromfile(os.path.join(GOLD, "bdpt_spheres64_i2_s5489.f32"), np.float32).reshape(64, 64, 3)
+    assert np.array_equal(film, ref)
+    film, _ = s.pt(64, 64, 4, 7, 5489, mode=0)
+    ref = np.fromfile(os.path.join(GOLD, "pt_spheres64_spp4_s5489.f32"), np.float32).reshape(64, 64, 3)
     assert np.array_equal(film, ref)
 
 

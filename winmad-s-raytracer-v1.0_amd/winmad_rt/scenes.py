@@ -102,6 +102,41 @@ def cbox_scene(width, height, mode="pt", assets=ASSETS):
     return out
 
 
+def _sphere(c, r, matid):
+    """<sphere> element (scene.cpp:375-396): origin, radius, material id."""
+    return (f"\t<sphere>\n\t\t<origin x=\"{c[0]}\" y=\"{c[1]}\" z=\"{c[2]}\"/>\n"
+            f"\t\t<radius radius=\"{r}\"/>\n\t\t<matid matid=\"{matid}\"/>\n\t</sphere>\n")
+
+
+def spheres_scene(width, height, mode="bdpt", assets=ASSETS):
+    """Cornell-box walls and luminaire with three spheres -- glass (IOR 1.5),
+    mirror and diffuse -- for the Sphere::hit path and the specular BSDF
+    branches (the reference's configs use triangles only)."""
+    xres, yres = (width, height) if mode == "pt" else (height, width)
+    a = lambda f: os.path.join(assets, f)
+    out = "<scene>\n"
+    out += _camera(("-0.0439815", "-4.12529", "0.222539"),
+                   ("0.00688625", "0.998505", "-0.0542161"),
+                   ("3.73896e-4", "0.0542148", "0.998529"), xres, yres, "45")
+    out += _mat()
+    out += _mat(d=("0.803922", "0.803922", "0.803922"), e=1)
+    out += _mat(d=("0.156863", "0.803922", "0.172549"), e=1)
+    out += _mat(d=("0.803922", "0.152941", "0.152941"), e=1)
+    out += _mat(s=("1", "1", "1"), n="1.5")                   # 4 glass
+    out += _mat(s=("0.95", "0.95", "0.95"))                    # 5 mirror
+    out += _mat(d=("0.2", "0.3", "0.7"), g=("0.3", "0.3", "0.3"), e=20)  # 6 glossy blue
+    for f in ("cbox_floor.obj", "cbox_back.obj", "cbox_ceiling.obj"):
+        out += _obj(a(f), 1)
+    out += _obj(a("cbox_greenwall.obj"), 2)
+    out += _obj(a("cbox_redwall.obj"), 3)
+    out += _sphere(("-0.5", "0.3", "-0.82"), "0.45", 4)
+    out += _sphere(("0.55", "0.6", "-0.86"), "0.42", 5)
+    out += _sphere(("0.05", "-0.45", "-1.0"), "0.28", 6)
+    out += _area(a("cbox_luminaire.obj"), "25.03329895614464")
+    out += "</scene>\n"
+    return out
+
+
 def synth_torus_obj(path, U=1000, V=500, R=150.0, r=45.0, center=(17.0, 102.0, -15.0)):
     """The C4/C5 synthetic torus: U x V quad grid in the xy-plane, each quad
     (a b c d) written as `f a b c` / `f a c d` => 2*U*V = 1,000,000 triangles."""
