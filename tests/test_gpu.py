@@ -263,3 +263,50 @@ def test_spheres_bdpt_and_pt_match_oracle_counter_rng():
     rmse, rms, _ = film_err(film * np.float32(1.0 / 16), ref)
     assert rmse / rms < 1e-2, (rmse, rms)
     assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+
+
+def test_render_argument_and_scene_errors(tmp_path):
+    """Failures are WR_E_* codes with a message, never a crash (the reference
+    would index an empty light list or overrun its buffers)."""
+    from winmad_rt import scenes
+    text = scenes.torus_scene(16, 16)
+    nolight = "\n".join(l for l in text.splitlines() if "area_light" not in l and "torus_light" not in l
+                        and "intensity" not in l)
+    s = native.Scene(scenes.write(str(tmp_path / "nolight.scene"), nolight))
+    c = native.Context(s, 0)
+    with pytest.raises(native.WrError) as e:
+        c.render_bdpt(16, 16, iterations=1)
+    assert e.value.code == native.WR_E_SCENE
+    with pytest.raises(native.WrError) as e:
+        c.render_path(16, 16, spp=1)
+    assert e.value.code == native.WR_E_SCENE
+    c2 = ctx(_scenes.torus(16, 16))
+    for kw in ({"max_path_length": 11}, {"iterations": -1}):
+        with pytest.raises(native.WrError) as e:
+            c2.render_bdpt(16, 16, **kw)
+        assert e.value.code == native.WR_E_ARG
+    with pytest.raises(native.WrError):
+        c2.render_bdpt(0, 16)
+    with pytest.raises(native.WrError):
+        c2.render_path(16, 16, spp=4, max_depth=62)
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (7, 5), (3, 130)])
+def test_bdpt_tiny_and_ragged_films_match_oracle(W, H):
+    """Films smaller than a wave / not a multiple of the 8x8 camera tiles."""
+    path = _scenes.torus(W, H)
+    film, st = ctx(path).render_bdpt(W, H, iterations=3, seed=17)
+    ref, rst = _oracle.Scene(path).bdpt(W, H, 3, 17, mode=1)
+    assert st.closest_rays == rst.closest_rays or abs(st.closest_rays - rst.closest_rays) <= 2
+    assert np.allclose(film, ref, rtol=1e-3, atol=1e-5)
+
+
+def test_zero_iterations_and_depth_zero():
+    c = ctx(_scenes.torus(16, 16))
+    film, st = c.render_bdpt(16, 16, iterations=0)
+    assert st.closest_rays == 0 and not film.any()
+    path = _scenes.cbox(16, 12)
+    film, st = ctx(path).render_path(16, 12, spp=4, max_depth=0, seed=2)
+    ref, rst = _oracle.Scene(path).pt(16, 12, 4, 0, 2, mode=1)
+    assert st.closest_rays == rst.closest_rays
+    assert np.allclose(film / 4, ref, rtol=1e-3, atol=1e-6)
