@@ -155,6 +155,12 @@ int wr_render_path(wr_context* ctx, const wr_path_params* p, float* film, int fi
  * first (square films only, as the reference). */
 int wr_film_write_ppm(const float* film, int height, int width, float scale, float gamma, int transpose,
                       const char* path);
+/* The same pipeline into the format the path's extension names, as the
+ * reference's cvSaveImage(filename) does (film.cpp:63): .ppm, .bmp (24-bit),
+ * .png (8-bit RGB); .pfm writes the scaled linear floats (no clamp / gamma).
+ * Other extensions: WR_E_ARG. */
+int wr_film_write_image(const float* film, int height, int width, float scale, float gamma, int transpose,
+                        const char* path);
 
 const char* wr_last_error(void);
 int wr_api_version(void);

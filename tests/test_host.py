@@ -123,3 +123,64 @@ def test_cli_mirrors_reference_main(tmp_path):
     r = subprocess.run([exe, _scenes.torus(64, 64), str(tmp_path / "o.ppm"), "-xyz", "--params", str(para)],
                        capture_output=True, text=True)
     assert "error!" in r.stdout  # unknown mode (main.cpp:88-91)
+
+
+def _expected_8bit(film, scale, gamma):
+    """ImageFilm::outputImage's pipeline in float32 (film.cpp:39-64, color.h:47-75)."""
+    v = film.astype(np.float32) * np.float32(scale)
+    v = np.minimum(np.float32(1), np.where(v < 0, np.float32(0), v))  # clampVal; NaN -> 1 below
+    v = np.where(np.isnan(v), np.float32(1), v)
+    v = np.power(v, np.float32(1) / np.float32(gamma))
+    return (v.astype(np.float64) * 255.0).astype(np.uint8)
+
+
+def test_image_writer_formats(tmp_path):
+    """wr_film_write_image: the reference's 8-bit pipeline into PPM / BMP / PNG
+    (decoded here independently) and linear PFM."""
+    import struct
+    import zlib
+    rng = np.random.default_rng(3)
+    H, W = 5, 7  # odd width: BMP row padding, PNG scanlines
+    film = (rng.random((H, W, 3)) * 1.4 - 0.1).astype(np.float32)
+    film[0, 0, 0] = np.nan
+    exp = _expected_8bit(film, 0.9, 2.2)
+    native.write_image(film, tmp_path / "a.ppm", scale=0.9)
+    data = (tmp_path / "a.ppm").read_bytes()
+    head = f"P6\n{W} {H}\n255\n".encode()
+    assert data.startswith(head)
+    got = np.frombuffer(data[len(head):], np.uint8).reshape(H, W, 3)
+    # libm powf vs numpy float32 power may differ in the last bit before truncation
+    assert np.abs(got.astype(int) - exp).max() <= 1 and (got == exp).mean() > 0.97
+    assert got[0, 0, 0] == 255
+    native.write_image(film, tmp_path / "a.bmp", scale=0.9)
+    b = (tmp_path / "a.bmp").read_bytes()
+    assert b[:2] == b"BM" and struct.unpack("<iiHH", b[18:30]) == (W, H, 1, 24)
+    row = (3 * W + 3) & ~3
+    bgr = np.array([np.frombuffer(b[54 + r * row: 54 + r * row + 3 * W], np.uint8).reshape(W, 3)
+                    for r in range(H)])[::-1][..., ::-1]
+    assert np.array_equal(bgr, got)
+    native.write_image(film, tmp_path / "a.png", scale=0.9)
+    p = (tmp_path / "a.png").read_bytes()
+    assert p[:8] == b"\x89PNG\r\n\x1a\n"
+    chunks, off = {}, 8
+    while off < len(p):
+        n, typ = struct.unpack(">I4s", p[off:off + 8])
+        body = p[off + 8: off + 8 + n]
+        assert struct.unpack(">I", p[off + 8 + n: off + 12 + n])[0] == zlib.crc32(typ + body)
+        chunks.setdefault(typ, b"")
+        chunks[typ] += body
+        off += 12 + n
+    assert struct.unpack(">IIBBBBB", chunks[b"IHDR"]) == (W, H, 8, 2, 0, 0, 0)
+    raw = np.frombuffer(zlib.decompress(chunks[b"IDAT"]), np.uint8).reshape(H, 3 * W + 1)
+    assert not raw[:, 0].any() and np.array_equal(raw[:, 1:].reshape(H, W, 3), got)
+    native.write_image(film, tmp_path / "a.pfm", scale=0.5)
+    f = (tmp_path / "a.pfm").read_bytes()
+    head = f"PF\n{W} {H}\n-1.0\n".encode()
+    assert f.startswith(head)
+    lin = np.frombuffer(f[len(head):], "<f4").reshape(H, W, 3)[::-1]
+    assert np.array_equal(lin, film * np.float32(0.5), equal_nan=True)
+    native.write_image(film[:5, :5], tmp_path / "t.png", transpose=True)  # square transpose
+    with pytest.raises(native.WrError):
+        native.write_image(film, tmp_path / "a.jpg")
+    with pytest.raises(native.WrError):
+        native.write_image(film, tmp_path / "t.ppm", transpose=True)  # non-square

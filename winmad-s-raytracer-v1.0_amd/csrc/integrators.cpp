@@ -61,7 +61,7 @@ void BidirPathTracing::render() {
 void BidirPathTracing::outputImage(const char* filename) {
   // The reference transposes in place assuming height == width (:31-44);
   // only square films are transposed here (non-square reference output is corrupt).
-  ok(wr_film_write_ppm(film.data(), height, width, 1.f / iterations, 2.2f, height == width, filename));
+  ok(wr_film_write_image(film.data(), height, width, 1.f / iterations, 2.2f, height == width, filename));
 }
 
 void PathIntegrator::init(const char* filename, Parameters& para) {
@@ -89,7 +89,7 @@ void PathIntegrator::render() {
 }
 
 void PathIntegrator::outputImage(const char* filename) {
-  ok(wr_film_write_ppm(film.data(), height, width, 1.f, 2.2f, 0, filename));
+  ok(wr_film_write_image(film.data(), height, width, 1.f, 2.2f, 0, filename));
 }
 
 }  // namespace winmad

@@ -30,11 +30,7 @@
 using namespace wrd;
 
 // =============================================================== errors
-static thread_local std::string g_err;
-static int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
+static int fail(int code, const std::string& msg) { return wr::set_error(code, msg); }
 #define HIPCHK(expr)                                                                          \
   do {                                                                                        \
     hipError_t e_ = (expr);                                                                   \
@@ -1427,7 +1423,7 @@ int check_device() {
 // =============================================================== C ABI
 extern "C" {
 
-const char* wr_last_error(void) { return g_err.c_str(); }
+const char* wr_last_error(void) { return wr::last_error(); }
 int wr_api_version(void) { return WR_API_VERSION; }
 
 int wr_scene_load(const char* path, wr_scene** out) {
@@ -1975,28 +1971,5 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
   return film_return(c, film, film_on_device, nf);
 }
 
-int wr_film_write_ppm(const float* film, int height, int width, float scale, float gamma, int transpose,
-                      const char* path) {
-  if (!film || !path || height <= 0 || width <= 0) return fail(WR_E_ARG, "bad argument");
-  if (transpose && height != width) return fail(WR_E_ARG, "transpose needs a square film (bidirPathTracing.cpp:31-44)");
-  std::vector<unsigned char> img(size_t(height) * width * 3);
-  const float inv_gamma = 1.f / gamma;
-  for (int i = 0; i < height; ++i)
-    for (int j = 0; j < width; ++j) {
-      const float* c = transpose ? film + 3 * (size_t(j) * width + i) : film + 3 * (size_t(i) * width + j);
-      for (int ch = 0; ch < 3; ++ch) {
-        float v = c[ch] * scale;                                  // ImageFilm::scale
-        v = std::min(1.0f, std::max(v, 0.0f));                    // Color3::clamp
-        v = std::pow(v, inv_gamma);                               // Color3::gamma
-        img[3 * (size_t(i) * width + j) + ch] = static_cast<unsigned char>(v * 255.0);  // Color3::R()
-      }
-    }
-  FILE* f = std::fopen(path, "wb");
-  if (!f) return fail(WR_E_IO, std::string("cannot write ") + path);
-  std::fprintf(f, "P6\n%d %d\n255\n", width, height);
-  std::fwrite(img.data(), 1, img.size(), f);
-  std::fclose(f);
-  return WR_OK;
-}
 
 }  // extern "C"

@@ -850,4 +850,13 @@ std::string dump_scene(const Scene& s) {
   return o;
 }
 
+namespace {
+thread_local std::string g_err;
+}
+int set_error(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+const char* last_error() { return g_err.c_str(); }
+
 }  // namespace wr

@@ -88,4 +88,8 @@ std::string dump_scene(const Scene& s);
 // Camera::setup (camera.cpp:3-29).
 void setup_camera(Camera& c, F3 pos, F3 fwd, F3 up, float xres, float yres, float fov);
 
+// Error message of the last failing wr_* call on this thread (wr_last_error).
+int set_error(int code, const std::string& msg);
+const char* last_error();
+
 }  // namespace wr

@@ -19,7 +19,7 @@ K_TRACE, K_SHADE, K_RESOLVE, K_GEN, K_OTHER = 0, 1, 2, 3, 4
 # every entry point declared in include/winmad_rt.h
 EXPORTS = ["wr_scene_load", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free", "wr_device_count",
            "wr_create", "wr_destroy", "wr_set_pipelines", "wr_trace_closest", "wr_occluded", "wr_render_bdpt", "wr_render_path",
-           "wr_film_write_ppm", "wr_last_error", "wr_api_version"]
+           "wr_film_write_ppm", "wr_film_write_image", "wr_last_error", "wr_api_version"]
 
 
 class WrRay(C.Structure):
@@ -110,6 +110,7 @@ def lib():
         L.wr_render_bdpt.argtypes = [P, C.POINTER(WrBdptParams), P, I, C.POINTER(WrStats)]
         L.wr_render_path.argtypes = [P, C.POINTER(WrPathParams), P, I, C.POINTER(WrStats)]
         L.wr_film_write_ppm.argtypes = [C.POINTER(C.c_float), I, I, C.c_float, C.c_float, I, C.c_char_p]
+        L.wr_film_write_image.argtypes = [C.POINTER(C.c_float), I, I, C.c_float, C.c_float, I, C.c_char_p]
         L.wr_last_error.restype = C.c_char_p
         _lib = L
     return _lib
@@ -237,3 +238,11 @@ def write_ppm(film, path, scale=1.0, gamma=2.2, transpose=False):
     h, w = film.shape[:2]
     check(lib().wr_film_write_ppm(film.ctypes.data_as(C.POINTER(C.c_float)), h, w, scale, gamma,
                                   1 if transpose else 0, os.fsencode(path)))
+
+
+def write_image(film, path, scale=1.0, gamma=2.2, transpose=False):
+    """ImageFilm::outputImage into .ppm / .bmp / .png, or linear .pfm."""
+    film = np.ascontiguousarray(film, np.float32)
+    h, w = film.shape[:2]
+    check(lib().wr_film_write_image(film.ctypes.data_as(C.POINTER(C.c_float)), h, w, scale, gamma,
+                                    1 if transpose else 0, os.fsencode(path)))
