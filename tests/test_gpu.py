@@ -310,3 +310,16 @@ def test_zero_iterations_and_depth_zero():
     ref, rst = _oracle.Scene(path).pt(16, 12, 4, 0, 2, mode=1)
     assert st.closest_rays == rst.closest_rays
     assert np.allclose(film / 4, ref, rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("spp", [8, 12])
+def test_pt_non_square_spp_stratification_matches_oracle(spp):
+    """len = floor(sqrt(spp)) strata; samples past len^2 overshoot the pixel
+    exactly as SurfaceIntegrator::render does (surfaceIntegrator.cpp:26-32,
+    sampleRectangleStratified sampler.cpp:28-42) -- the C3 config's 512 spp."""
+    path = _scenes.cbox(40, 30)
+    film, st = ctx(path).render_path(40, 30, spp=spp, max_depth=7, seed=31)
+    ref, rst = _oracle.Scene(path).pt(40, 30, spp, 7, 31, mode=1)
+    rmse, rms, _ = film_err(film * np.float32(1.0 / spp), ref)
+    assert rmse / rms < 1e-2, (rmse, rms)
+    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
