@@ -7,7 +7,7 @@ tmp = tempfile.mkdtemp()
 p = scenes.write(os.path.join(tmp, "t.scene"), scenes.torus_scene(W, H))
 c = native.Context(native.Scene(p), 0)
 film = torch.zeros((H, W, 3), device="cuda")
-for pipes in (1, 3):
+for pipes in (1, 4):
     c.set_pipelines(pipes)
     c.render_bdpt(W, H, iterations=2, seed=1, iter_begin=999, film_ptr=film.data_ptr())
     _, st = c.render_bdpt(W, H, iterations=12, seed=1, film_ptr=film.data_ptr(), time_kernels=1)
