@@ -1749,6 +1749,510 @@ int cr_render_bdpt(const cr_scene* s, int W, int H, int iter_begin, int iteratio
 }
 
 /* ------------------------------------------------------------------------- */
+/* VertexCM (vertexcm.h, vertexcm.cpp) + the point KD tree (KDtree.h)         */
+/* ------------------------------------------------------------------------- */
+typedef struct {  /* SubPathState (vertexcm.h:25-37) / PathVertex (:12-23) */
+    v3 origin, dir, pos;
+    c3 thr;
+    bsdf_t bsdf;
+    float dVCM, dVC, dVM;
+    int len;
+} vstate;
+
+typedef struct {  /* KdNode (KDtree.h:8-30): pre-order, left child = node + 1 */
+    float split;
+    int axis;      /* 0..2 inner, -1 leaf */
+    int has_left;
+    int right;     /* -1: none */
+} vkd_node;
+
+typedef struct {
+    const cr_scene* s;
+    int W, H, P, minlen, maxlen;
+    float N;                           /* lightSubPathNum (:49-51) */
+    float radius, vm_norm, mis_vm, mis_vc;
+    float* film;
+    cr_stats* st;
+    vstate* lv; int64_t nlv, cap_lv;
+    int* ends;                         /* pathEnds */
+    vkd_node* nodes; int* node_vert; int64_t nnodes, next_node;
+    int* idx;                          /* build scratch: buildNodes */
+    int cur_axis;
+} vcm_ctx;
+
+/* CompareNode (KDtree.h:74-86): pos[axis], ties by address (= index in data). */
+static inline int vkd_less(const vcm_ctx* c, int a, int b, int axis) {
+    float pa = vget(c->lv[a].pos, axis), pb = vget(c->lv[b].pos, axis);
+    return pa == pb ? a < b : pa < pb;
+}
+
+/* std::nth_element under a strict total order: the element of rank k lands at
+ * k, smaller ones before it, larger after.  The tree depends only on these
+ * sets (KDtree.h:117-138), not on their arrangement, so any selection
+ * algorithm reproduces the reference's tree. */
+static void vkd_select(vcm_ctx* c, int* a, int n, int k, int axis) {
+    int lo = 0, hi = n - 1;
+    while (hi > lo) {
+        int mid = lo + (hi - lo) / 2;
+        /* median of three to a[hi] */
+        if (vkd_less(c, a[mid], a[lo], axis)) { int t = a[mid]; a[mid] = a[lo]; a[lo] = t; }
+        if (vkd_less(c, a[hi], a[lo], axis)) { int t = a[hi]; a[hi] = a[lo]; a[lo] = t; }
+        if (vkd_less(c, a[mid], a[hi], axis)) { int t = a[mid]; a[mid] = a[hi]; a[hi] = t; }
+        int pv = a[hi], st = lo;
+        for (int i = lo; i < hi; i++)
+            if (vkd_less(c, a[i], pv, axis)) { int t = a[i]; a[i] = a[st]; a[st] = t; st++; }
+        a[hi] = a[st]; a[st] = pv;
+        if (st == k) return;
+        if (k < st) hi = st - 1; else lo = st + 1;
+    }
+}
+
+static void vkd_build(vcm_ctx* c, int64_t node, int st, int ed) { /* KdTree::buildTree (KDtree.h:88-139) */
+    vkd_node* nd = &c->nodes[node];
+    if (st + 1 == ed) {
+        nd->axis = -1; nd->has_left = 0; nd->right = -1;
+        c->node_vert[node] = c->idx[st];
+        return;
+    }
+    v3 l = mk(R_INF, R_INF, R_INF), r = mk(-R_INF, -R_INF, -R_INF);
+    for (int i = st; i < ed; i++) {
+        v3 p = c->lv[c->idx[i]].pos;
+        l.x = fmins(l.x, p.x); l.y = fmins(l.y, p.y); l.z = fmins(l.z, p.z);   /* std::min(l, p) */
+        r.x = fmaxs(r.x, p.x); r.y = fmaxs(r.y, p.y); r.z = fmaxs(r.z, p.z);
+    }
+    v3 diag = vsub(r, l);
+    float tmp = -R_INF;
+    int axis = -1;
+    for (int i = 0; i <= 2; i++)
+        if (tmp < vget(diag, i)) { tmp = vget(diag, i); axis = i; }
+    int sp = (st + ed) / 2;
+    vkd_select(c, c->idx + st, ed - st, sp - st, axis);
+    nd = &c->nodes[node];
+    nd->split = vget(c->lv[c->idx[sp]].pos, axis);
+    nd->axis = axis; nd->has_left = 0; nd->right = -1;
+    c->node_vert[node] = c->idx[sp];
+    if (st < sp) {
+        c->nodes[node].has_left = 1;
+        int64_t ch = c->next_node++;
+        vkd_build(c, ch, st, sp);
+    }
+    if (sp + 1 < ed) {
+        int64_t ch = c->next_node++;
+        c->nodes[node].right = (int)ch;
+        vkd_build(c, ch, sp + 1, ed);
+    }
+}
+
+typedef struct {  /* RangeQuery (vertexcm.h:42-97) */
+    const bsdf_t* cb;
+    const vstate* cs;
+    c3 contrib;
+} vquery;
+
+static void vquery_process(vcm_ctx* c, vquery* q, const vstate* lv) { /* vertexcm.h:59-96 */
+    if (lv->len + q->cs->len > c->maxlen || lv->len + q->cs->len < c->minlen) return;
+    v3 ldir = to_world(&lv->bsdf.fr, lv->bsdf.wi);  /* BSDF::wiWorld (bsdf.h:101-104) */
+    float cosC, dp, rp;
+    c3 f = bsdf_f(q->cb, c->s->mats, ldir, &cosC, &dp, &rp);
+    if (cblack(f)) return;
+    if (c->st) c->st->vm_merged++;
+    dp *= q->cb->cont;
+    rp *= lv->bsdf.cont;
+    float wl = lv->dVCM * c->mis_vc + lv->dVM * dp;
+    float wc = q->cs->dVCM * c->mis_vc + q->cs->dVM * rp;
+    float w = 1.f / (wl + 1.f + wc);
+    c3 tmp = cmul(f, lv->thr);
+    q->contrib = cadd(q->contrib, cscale(tmp, w));
+}
+
+static void vkd_search(vcm_ctx* c, int64_t node, v3 pos, float radius, vquery* q) { /* KDtree.h:141-175 */
+    const vkd_node* nd = &c->nodes[node];
+    if (nd->axis >= 0) {
+        float pa = vget(pos, nd->axis);
+        float delta = fabsf(pa - nd->split);
+        if (pa <= nd->split) {
+            if (nd->has_left) vkd_search(c, node + 1, pos, radius, q);
+            if (delta < radius && nd->right >= 0) vkd_search(c, nd->right, pos, radius, q);
+        } else {
+            if (nd->right >= 0) vkd_search(c, nd->right, pos, radius, q);
+            if (delta < radius && nd->has_left) vkd_search(c, node + 1, pos, radius, q);
+        }
+    }
+    const vstate* lv = &c->lv[c->node_vert[node]];
+    v3 d = vsub(pos, lv->pos);
+    float dis = sqrtf(vsqr(d));
+    if (dis < radius) {
+        if (c->st) c->st->vm_found++;
+        vquery_process(c, q, lv);
+    }
+}
+
+/* Known-answer hook: build the point tree over pts[n][3] and, per query, count
+ * the vertices searchInRadius reports and sum their indices; the same two
+ * numbers by brute force (|q - p| < radius, same float expression). */
+typedef struct { int64_t n, isum; } vkd_acc;
+static void vkd_collect(vcm_ctx* c, int64_t node, v3 pos, float radius, vkd_acc* a) {
+    const vkd_node* nd = &c->nodes[node];
+    if (nd->axis >= 0) {
+        float pa = vget(pos, nd->axis), delta = fabsf(pa - nd->split);
+        if (pa <= nd->split) {
+            if (nd->has_left) vkd_collect(c, node + 1, pos, radius, a);
+            if (delta < radius && nd->right >= 0) vkd_collect(c, nd->right, pos, radius, a);
+        } else {
+            if (nd->right >= 0) vkd_collect(c, nd->right, pos, radius, a);
+            if (delta < radius && nd->has_left) vkd_collect(c, node + 1, pos, radius, a);
+        }
+    }
+    int v = c->node_vert[node];
+    if (sqrtf(vsqr(vsub(pos, c->lv[v].pos))) < radius) { a->n++; a->isum += v; }
+}
+void cr_kat_vkd(const float* pts, int n, const float* qs, int nq, float radius, int64_t* out4) {
+    vcm_ctx c;
+    memset(&c, 0, sizeof c);
+    c.lv = (vstate*)calloc((size_t)n, sizeof(vstate));
+    for (int i = 0; i < n; i++) c.lv[i].pos = mk(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
+    c.nlv = n;
+    c.nodes = (vkd_node*)calloc((size_t)n, sizeof(vkd_node));
+    c.node_vert = (int*)calloc((size_t)n, sizeof(int));
+    c.idx = (int*)calloc((size_t)n, sizeof(int));
+    for (int i = 0; i < n; i++) c.idx[i] = i;
+    c.next_node = 1;
+    if (n > 0) vkd_build(&c, 0, 0, n);
+    for (int k = 0; k < nq; k++) {
+        v3 q = mk(qs[3 * k], qs[3 * k + 1], qs[3 * k + 2]);
+        vkd_acc a = {0, 0}, b = {0, 0};
+        if (n > 0) vkd_collect(&c, 0, q, radius, &a);
+        for (int i = 0; i < n; i++)
+            if (sqrtf(vsqr(vsub(q, c.lv[i].pos))) < radius) { b.n++; b.isum += i; }
+        out4[4 * k] = a.n; out4[4 * k + 1] = a.isum; out4[4 * k + 2] = b.n; out4[4 * k + 3] = b.isum;
+    }
+    free(c.lv); free(c.nodes); free(c.node_vert); free(c.idx);
+}
+
+static void vcm_gen_light(vcm_ctx* c, rng_t* rng, vstate* ls) { /* :287-330 */
+    const cr_scene* s = c->s;
+    int nl = s->nlights;
+    float lpp = 1.f / (float)nl;
+    int id = (int)(rng_f(rng) * (float)nl);
+    const light_t* l = &s->lights[id];
+    float epdf, dpdf, cal;
+    c3 rad;
+    for (;;) {
+        v3 pr = rng_v3(rng);  /* argument order as gen_light above */
+        v3 dr = rng_v3(rng);
+        rad = light_emit(l, dr, pr, &ls->origin, &ls->dir, &epdf, &dpdf, &cal);
+        if (epdf > 1e-7f) break;
+    }
+    ls->thr = rad;
+    epdf = fmaxs(epdf, 1e-7f);
+    epdf *= lpp;
+    dpdf *= lpp;
+    ls->thr = cdivs(ls->thr, epdf);
+    ls->len = 1;
+    ls->dVCM = dpdf / epdf;
+    ls->dVC = cal / epdf;     /* AreaLight: finite, not delta -> cosAtLight */
+    ls->dVM = ls->dVC * c->mis_vc;
+}
+
+static int vcm_scatter(vcm_ctx* c, rng_t* rng, const bsdf_t* b, v3 hit, vstate* ps) { /* :386-444 */
+    const mat_t* mats = c->s->mats;
+    float dpdf, cosWo;
+    int type;
+    v3 r3 = rng_v3(rng);
+    c3 f = bsdf_sample(b, mats, r3, &ps->dir, &dpdf, &cosWo, &type);
+    if (cblack(f)) return 0;
+    float rpdf = dpdf;
+    if ((type & T_SPEC) == 0) rpdf = bsdf_pdf(b, mats, ps->dir, 1);
+    float cp = b->cont;
+    if (rng_f(rng) > cp) return 0;
+    dpdf *= cp;
+    rpdf *= cp;
+    if (type & T_SPEC) {
+        ps->dVCM = 0.f;
+        ps->dVC *= cosWo;
+        ps->dVM *= cosWo;
+    } else {
+        ps->dVC = (cosWo / dpdf) * (ps->dVC * rpdf + ps->dVCM + c->mis_vm);
+        ps->dVM = (cosWo / dpdf) * (ps->dVM * rpdf + ps->dVCM * c->mis_vc + 1.f);
+        ps->dVCM = 1.f / dpdf;
+    }
+    ps->origin = hit;
+    ps->thr = cscale(cmul(ps->thr, f), cosWo / dpdf);
+    return 1;
+}
+
+static c3 vcm_connect_camera(vcm_ctx* c, const vstate* ls, v3 hit, const bsdf_t* b) { /* :332-384 */
+    const cr_scene* s = c->s;
+    const camera_t* cam = &s->cam;
+    c3 res = C0;
+    v3 dtc = vsub(cam->pos, hit);
+    if (cmpf(vdot(vneg(dtc), cam->fwd)) <= 0) return res;
+    float d2 = vsqr(dtc);
+    float dist = sqrtf(d2);
+    dtc = vdiv(dtc, dist);
+    float cosTo, dp, rp;
+    c3 f = bsdf_f(b, s->mats, dtc, &cosTo, &dp, &rp);
+    if (cblack(f)) return res;
+    rp *= b->cont;
+    float cosAt = vdot(vneg(dtc), cam->fwd);
+    float ipd = cam->plane_dist / cosAt;
+    float i2sa = (ipd * ipd) / cosAt;
+    float i2s = i2sa * fabsf(cosTo) / d2;
+    float pdfA = i2s;
+    float wl = (pdfA / c->N) * (c->mis_vm + ls->dVCM + ls->dVC * rp);
+    float w = 1.f / (wl + 1.f);
+    float s2i = 1.f / i2s;
+    res = cdivs(cscale(cmul(ls->thr, f), w), c->N * s2i);
+    if (cblack(res)) return res;
+    if (occluded(s, hit, dtc, cam->pos, c->st)) return C0;
+    return res;
+}
+
+static c3 vcm_direct(vcm_ctx* c, rng_t* rng, const vstate* cs, v3 hit, const bsdf_t* b) { /* :516-573 */
+    const cr_scene* s = c->s;
+    c3 res = C0;
+    int nl = s->nlights;
+    float lpp = 1.f / (float)nl;
+    int id = (int)(rng_f(rng) * (float)nl);
+    const light_t* l = &s->lights[id];
+    v3 dtl;
+    float dist, dpdf, epdf, cal;
+    v3 r3 = rng_v3(rng);
+    c3 illu = light_illum(l, hit, r3, &dtl, &dist, &dpdf, &epdf, &cal);
+    if (cblack(illu)) return res;
+    float bdp, brp, cosTo;
+    c3 f = bsdf_f(b, s->mats, dtl, &cosTo, &bdp, &brp);
+    if (cblack(f)) return res;
+    float cp = b->cont;
+    bdp *= cp;  /* AreaLight is not delta */
+    brp *= cp;
+    float wl = bdp / (lpp * dpdf);
+    float wc = (epdf * cosTo / (dpdf * cal)) * (c->mis_vm + cs->dVCM + cs->dVC * brp);
+    float w = 1.f / (wl + 1.f + wc);
+    res = cscale(cmul(illu, f), w * cosTo / (lpp * dpdf));
+    if (cblack(res) || occluded(s, hit, dtl, vadd(hit, vscale(dtl, dist)), c->st)) return C0;
+    return res;
+}
+
+static c3 vcm_connect(vcm_ctx* c, const vstate* ls, const bsdf_t* cb, v3 hit, const vstate* cs) { /* :575-636 */
+    const cr_scene* s = c->s;
+    v3 dir = vsub(ls->pos, hit);
+    float d2 = vsqr(dir);
+    float dist = sqrtf(d2);
+    dir = vdiv(dir, dist);
+    c3 res = C0;
+    float cosC, cdp, crp;
+    c3 cf = bsdf_f(cb, s->mats, dir, &cosC, &cdp, &crp);
+    if (cblack(cf)) return res;
+    float ccp = cb->cont;
+    cdp *= ccp;
+    crp *= ccp;
+    float cosL, ldp, lrp;
+    c3 lf = bsdf_f(&ls->bsdf, s->mats, vneg(dir), &cosL, &ldp, &lrp);
+    if (cblack(lf)) return res;
+    float lcp = ls->bsdf.cont;
+    ldp *= lcp;
+    lrp *= lcp;
+    float G = cosL * cosC / d2;
+    if (cmpf(G) < 0) return res;
+    float cdpa = cdp * fabsf(cosL) / (dist * dist);  /* pdfWtoA (math.cpp:13-16) */
+    float ldpa = ldp * fabsf(cosC) / (dist * dist);
+    float wl = cdpa * (c->mis_vm + ls->dVCM + ls->dVC * lrp);
+    float wc = ldpa * (c->mis_vm + cs->dVCM + cs->dVC * crp);
+    float w = 1.f / (wl + 1.f + wc);
+    res = cscale(cscale(cmul(cf, lf), w), G);
+    if (cblack(res) || occluded(s, hit, dir, vadd(hit, vscale(dir, dist)), c->st)) return C0;
+    return res;
+}
+
+static void vcm_push(vcm_ctx* c, const vstate* v) {
+    if (c->nlv >= c->cap_lv) { c->cap_lv = c->cap_lv ? 2 * c->cap_lv : 4096;
+        c->lv = (vstate*)realloc(c->lv, (size_t)c->cap_lv * sizeof(vstate)); }
+    c->lv[c->nlv++] = *v;
+}
+
+/* VertexCM::runIteration (:47-285) for iteration index `it` (radius schedule)
+ * with the RNG of global iteration `key_iter` (counter mode). */
+static void vcm_iteration(vcm_ctx* c, mt_state* mt, int mode, uint32_t seed, int it, uint32_t key_iter,
+                          float base_radius, float alpha, int64_t pb, int64_t pe) {
+    const cr_scene* s = c->s;
+    const camera_t* cam = &s->cam;
+    float radius = base_radius;
+    radius /= powf((float)(it + 1), 0.5f * (1.f - alpha));
+    radius = fmaxs(radius, R_EPS);
+    float r2 = radius * radius;
+    c->radius = radius;
+    c->vm_norm = 1.f / (r2 * R_PI * c->N);
+    float eta = (R_PI * r2) * c->N;
+    c->mis_vm = eta;
+    c->mis_vc = 1.f / eta;
+    memset(c->ends, 0, sizeof(int) * (size_t)c->P);
+    c->nlv = 0;
+    rng_t rng;
+    bsdf_t stale;
+    memset(&stale, 0, sizeof stale);
+    /* light pass (:74-140) */
+    for (int64_t pi = pb; pi < pe; pi++) {
+        rng_for(&rng, mode, mt, seed, key_iter, 0, (uint32_t)pi);
+        vstate ls;
+        memset(&ls, 0, sizeof ls);
+        vcm_gen_light(c, &rng, &ls);
+        for (;; ls.len++) {
+            ray_t ray = mkray(vadd(ls.origin, vscale(ls.dir, R_EPS)), ls.dir);
+            hit_t h;
+            if (intersect(s, &ray, &h, c->st) < 0) break;
+            v3 hp = h.p;
+            bsdf_t b;
+            bsdf_init(&b, vneg(ray.d), &h, s->mats);
+            if (b.matId == 0) break;
+            if (b.matId < 0) {
+                /* An emitter hit: BSDF::init skips calcComponentProb (bsdf.h:78-83), so
+                 * componentProb / continueProb / fresnelReflect keep whatever the
+                 * stack slot of `BSDF bsdf` (:90) held -- the previous BSDF built in
+                 * this loop, in path order (pinned against refdrv, which matches it
+                 * bit for bit).  isDelta is then computed from those, and a
+                 * non-delta emitter vertex is stored and merged (vertexcm.h:77-78
+                 * reads its continueProb).  Iteration start: a zeroed slot. */
+                b.pd = stale.pd; b.pg = stale.pg; b.pr = stale.pr; b.pt = stale.pt;
+                b.cont = stale.cont; b.fres = stale.fres;
+                b.delta = (cmpf(b.pd) == 0 && cmpf(b.pg) == 0);
+            }
+            stale = b;
+            /* `pathLength > 1 || isFiniteLight == 1` (:94-95): isFiniteLight is a signed
+             * 1-bit field (vertexcm.h:31), so storing true reads back as -1 and only
+             * pathLength > 1 scales -- unlike BDPT, whose flag is a plain int */
+            if (ls.len > 1) ls.dVCM *= (h.t * h.t);
+            ls.dVCM /= fabsf(b.wi.z);
+            ls.dVC /= fabsf(b.wi.z);
+            ls.dVM /= fabsf(b.wi.z);
+            ls.pos = hp;
+            ls.bsdf = b;
+            if (!b.delta) vcm_push(c, &ls);
+            if (!b.delta && ls.len + 1 >= c->minlen) {
+                v3 ip = x_point(&cam->w2r, hp);
+                if (cam_check(cam, ip.x, ip.y)) {
+                    c3 r = vcm_connect_camera(c, &ls, hp, &b);
+                    film_add(c->film, c->H, c->W, (int)ip.x, (int)ip.y, r);
+                }
+            }
+            if (ls.len + 2 > c->maxlen) break;
+            if (!vcm_scatter(c, &rng, &b, hp, &ls)) break;
+        }
+        c->ends[pi] = (int)c->nlv;
+    }
+    /* vertex kd-tree (:152) */
+    c->nnodes = c->nlv;
+    c->next_node = 1;
+    if (c->nlv > 0) {
+        c->nodes = (vkd_node*)realloc(c->nodes, (size_t)c->nlv * sizeof(vkd_node));
+        c->node_vert = (int*)realloc(c->node_vert, (size_t)c->nlv * sizeof(int));
+        c->idx = (int*)realloc(c->idx, (size_t)c->nlv * sizeof(int));
+        for (int64_t i = 0; i < c->nlv; i++) c->idx[i] = (int)i;
+        vkd_build(c, 0, 0, (int)c->nlv);
+    }
+    /* camera pass (:157-283) */
+    for (int64_t pi = pb; pi < pe; pi++) {
+        rng_for(&rng, mode, mt, seed, key_iter, 1, (uint32_t)pi);
+        vstate cs;
+        memset(&cs, 0, sizeof cs);
+        int y = (int)(pi % c->W), x = (int)(pi / c->W);  /* generateCameraSample (:446-479) */
+        v3 jit = rng_v3(&rng);
+        v3 smp = mk((float)x + jit.x, (float)y + jit.y, 0.f);
+        v3 rp = x_point(&cam->r2w, mk(smp.x, smp.y, 0));
+        ray_t cr = mkray(cam->pos, vsub(rp, cam->pos));
+        float cosAt = vdot(cam->fwd, cr.d);
+        float ipd = cam->plane_dist / cosAt;
+        float i2sa = (ipd * ipd) / cosAt;
+        cs.origin = cr.o;
+        cs.dir = cr.d;
+        cs.thr = mkc(1, 1, 1);
+        cs.len = 1;
+        cs.dVCM = c->N / i2sa;
+        cs.dVC = 0.f;
+        cs.dVM = 0.f;
+        c3 color = C0;
+        for (;; cs.len++) {
+            ray_t ray = mkray(vadd(cs.origin, vscale(cs.dir, R_EPS)), cs.dir);
+            hit_t h;
+            if (intersect(s, &ray, &h, c->st) < 0) break;
+            v3 hp = h.p;
+            bsdf_t b;
+            bsdf_init(&b, vneg(ray.d), &h, s->mats);
+            if (b.matId == 0) break;
+            cs.dVCM *= (h.t * h.t);
+            cs.dVCM /= fabsf(b.wi.z);
+            cs.dVC /= fabsf(b.wi.z);
+            cs.dVM /= fabsf(b.wi.z);
+            if (h.matId < 0) {  /* getLightRadiance (:481-514) == BDPT's */
+                const light_t* l = &s->lights[-h.matId - 1];
+                if (cs.len >= c->minlen) {
+                    float lpp = 1.f / (float)s->nlights;
+                    float dpa, ep;
+                    c3 r = light_radiance(l, ray.d, &dpa, &ep);
+                    if (!cblack(r)) {
+                        if (cs.len != 1) {
+                            dpa *= lpp;
+                            ep *= lpp;
+                            float wc = dpa * cs.dVCM + ep * cs.dVC;
+                            r = cscale(r, 1.f / (1.f + wc));
+                        }
+                        color = cadd(color, cmul(cs.thr, r));
+                    }
+                }
+                break;
+            }
+            if (cs.len >= c->maxlen) break;
+            if (!b.delta && cs.len + 1 >= c->minlen)
+                color = cadd(color, cmul(cs.thr, vcm_direct(c, &rng, &cs, hp, &b)));
+            if (!b.delta) {
+                int st0 = pi == 0 ? 0 : c->ends[pi - 1], ed = c->ends[pi];
+                for (int i = st0; i < ed; i++) {
+                    const vstate* lsv = &c->lv[i];
+                    if (lsv->len + 1 + cs.len < c->minlen) continue;
+                    if (lsv->len + 1 + cs.len > c->maxlen) break;
+                    c3 tmp = vcm_connect(c, lsv, &b, hp, &cs);
+                    color = cadd(color, cmul(cmul(cs.thr, lsv->thr), tmp));
+                }
+            }
+            if (!b.delta && c->nlv > 0) {  /* vertex merging (:265-276) */
+                vquery q = {&b, &cs, C0};
+                if (c->st) c->st->vm_queries++;
+                vkd_search(c, 0, hp, radius, &q);
+                color = cadd(color, cscale(cmul(cs.thr, q.contrib), c->vm_norm));
+            }
+            if (!vcm_scatter(c, &rng, &b, hp, &cs)) break;
+        }
+        film_add(c->film, c->H, c->W, (int)smp.x, (int)smp.y, color);
+    }
+}
+
+int cr_render_vcm(const cr_scene* s, int W, int H, int iter_begin, int iterations, uint32_t seed,
+                  int rng_mode, int min_path_length, int max_path_length, float radius_factor,
+                  float radius_alpha, int64_t path_begin, int64_t path_end, float* film, cr_stats* st) {
+    init_consts();
+    if (!s || s->nprims == 0 || s->nlights == 0) { set_err("scene has no geometry or lights", NULL); return -1; }
+    vcm_ctx c;
+    memset(&c, 0, sizeof c);
+    c.s = s; c.W = W; c.H = H; c.P = W * H;
+    c.minlen = min_path_length;
+    c.maxlen = max_path_length;
+    c.N = (float)(H * W);
+    c.film = film; c.st = st;
+    c.ends = (int*)calloc((size_t)c.P, sizeof(int));
+    if (path_end > c.P) path_end = c.P;
+    float base_radius = radius_factor * s->ssph.radius;  /* VertexCM::init (:13) */
+    mt_state mt;
+    mt_seed(&mt, seed);
+    double t0 = now_s();
+    for (int it = 0; it < iterations; it++)
+        vcm_iteration(&c, &mt, rng_mode, seed, iter_begin + it, (uint32_t)(iter_begin + it), base_radius,
+                      radius_alpha, path_begin, path_end);
+    if (st) st->seconds += now_s() - t0;
+    free(c.ends); free(c.lv); free(c.nodes); free(c.node_vert); free(c.idx);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
 /* PathIntegrator (pathIntegrator.cpp:29-148) + SurfaceIntegrator::render      */
 /* ------------------------------------------------------------------------- */
 static c3 pt_trace(const cr_scene* s, rng_t* rng, ray_t r, int max_depth, cr_stats* st) {

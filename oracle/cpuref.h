@@ -34,6 +34,9 @@ typedef struct {
     int64_t tri_tests;     /* Triangle::hit calls inside traverse()   */
     int64_t sph_tests;
     double seconds;
+    int64_t vm_queries;    /* VCM: KdTree::searchInRadius calls (camera vertices) */
+    int64_t vm_found;      /* VCM: light vertices within the radius               */
+    int64_t vm_merged;     /* VCM: RangeQuery::process merges (mergeNum)           */
 } cr_stats;
 
 /* Load a .scene (scene.cpp:259-467) and build the KD tree (scene.cpp:469-489).
@@ -63,6 +66,14 @@ int cr_render_bdpt(const cr_scene* s, int W, int H, int iter_begin, int iteratio
                    uint32_t seed, int rng_mode, int control_length, int64_t path_begin,
                    int64_t path_end, float* film, cr_stats* st);
 
+/* VCM (vertexcm.cpp:47-285, KDtree.h): film[x][y] like BDPT, accumulated.
+ * The reference: min 0, max 10, radius factor 0.003 (x sceneRadius), alpha 0.75,
+ * iterations 1 (vertexcm.cpp:3-21).  The merge radius of iteration i (0-based,
+ * global: iter_begin + k) is base / (i+1)^(0.5(1-alpha)) (:53-56). */
+int cr_render_vcm(const cr_scene* s, int W, int H, int iter_begin, int iterations, uint32_t seed,
+                  int rng_mode, int min_path_length, int max_path_length, float radius_factor,
+                  float radius_alpha, int64_t path_begin, int64_t path_end, float* film, cr_stats* st);
+
 /* PT (pathIntegrator.cpp:29-148 + surfaceIntegrator.cpp:14-46); film scaled by 1/spp. */
 int cr_render_pt(const cr_scene* s, int W, int H, int spp, int max_depth, uint32_t seed,
                  int rng_mode, int64_t pix_begin, int64_t pix_end, float* film, cr_stats* st);
@@ -89,6 +100,9 @@ int cr_kat_bsdf(const cr_scene* s, int matId, const float* n, const float* wi,
  *      | radiance(3) dpa epdf   (30 floats) */
 void cr_kat_light(const cr_scene* s, int li, const float* pos, const float* r3,
                   const float* dr, const float* pr, const float* rd, float* out);
+/* Point KD tree (KDtree.h:88-175) over pts[n][3]: per query, out4 = {found,
+ * sum of found indices} by searchInRadius, then the same by brute force. */
+void cr_kat_vkd(const float* pts, int n, const float* qs, int nq, float radius, int64_t* out4);
 /* out: ray origin(3) dir(3), raster(3), check */
 void cr_kat_camera(const cr_scene* s, float x, float y, const float* w, float* out10);
 

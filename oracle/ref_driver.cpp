@@ -11,9 +11,10 @@
 //   refdrv kat    SCENE PARA N SEED              BSDF / AreaLight / sampler / camera known answers
 //   refdrv bdpt   SCENE PARA ITERS SEED OUT.f32  BidirPathTracing::render, film pre-transpose
 //   refdrv pt     SCENE PARA SEED OUT.f32        PathIntegrator via SurfaceIntegrator::render
+//   refdrv vcm    SCENE PARA ITERS SEED OUT.f32  VertexCM::render (ref_driver_vcm.cpp)
 //
 // Every command chdir()s to $REFDRV_CWD (if set) after static initialisation so the
-// reference's debug file (bidirPathTracing.cpp:3) lands in a scratch directory.
+// reference's debug files (bidirPathTracing.cpp:3, vertexcm.h:10) land in a scratch directory.
 #include "surfaceIntegrator/bidirPathTracing.h"
 #include "surfaceIntegrator/pathIntegrator.h"
 #include "material/fresnel.h"
@@ -23,6 +24,7 @@
 #include <unistd.h>
 
 static std::map<const Geometry*, int> g_index;
+int refdrv_vcm(int argc, char** argv, Parameters& para);  // ref_driver_vcm.cpp
 
 static void hv(FILE* f, float x) { fprintf(f, " %a", (double)x); }
 static void hv3(FILE* f, const Vector3& v) { hv(f, v.x); hv(f, v.y); hv(f, v.z); }
@@ -247,6 +249,7 @@ int main(int argc, char** argv) {
         printf("render_seconds %.6f\n", t1 - t0);
         return 0;
     }
+    if (cmd == "vcm") return refdrv_vcm(argc, argv, para);
     if (cmd == "pt") {
         PathIntegrator* p = new PathIntegrator();
         p->init(argv[2], para);

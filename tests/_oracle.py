@@ -18,7 +18,8 @@ class Stats(C.Structure):
     _fields_ = [("closest_rays", C.c_int64), ("shadow_rays", C.c_int64),
                 ("inner_visits", C.c_int64), ("leaf_visits", C.c_int64),
                 ("prim_refs", C.c_int64), ("tri_tests", C.c_int64),
-                ("sph_tests", C.c_int64), ("seconds", C.c_double)]
+                ("sph_tests", C.c_int64), ("seconds", C.c_double),
+                ("vm_queries", C.c_int64), ("vm_found", C.c_int64), ("vm_merged", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -41,6 +42,8 @@ def lib():
         L.cr_scene_dump.argtypes = [P, C.c_char_p]
         L.cr_trace.argtypes = [P, F, I64, C.POINTER(C.c_int32), F, C.POINTER(C.c_uint8), C.POINTER(Stats)]
         L.cr_render_bdpt.argtypes = [P, I, I, I, I, U32, I, I, I64, I64, F, C.POINTER(Stats)]
+        L.cr_render_vcm.argtypes = [P, I, I, I, I, U32, I, I, I, C.c_float, C.c_float, I64, I64, F,
+                                    C.POINTER(Stats)]
         L.cr_render_pt.argtypes = [P, I, I, I, I, U32, I, I64, I64, F, C.POINTER(Stats)]
         L.cr_stream_key.restype = C.c_uint64
         L.cr_stream_key.argtypes = [U32, U32, U32, U32]
@@ -55,6 +58,7 @@ def lib():
         L.cr_kat_strat.argtypes = [F, I, I, F]
         L.cr_kat_bsdf.argtypes = [P, I, F, F, F, F, F]
         L.cr_kat_light.argtypes = [P, I, F, F, F, F, F, F]
+        L.cr_kat_vkd.argtypes = [F, I, F, I, C.c_float, C.POINTER(C.c_int64)]
         L.cr_kat_camera.argtypes = [P, C.c_float, C.c_float, F, F]
         _lib = L
     return _lib
@@ -107,6 +111,17 @@ class Scene:
         pb, pe = path_range or (0, W * H)
         rc = self.L.cr_render_bdpt(self.h, W, H, iter_begin, iterations, seed, mode, control_length,
                                    pb, pe, fptr(film), C.byref(st))
+        if rc:
+            raise RuntimeError(self.L.cr_last_error().decode())
+        return film, st
+
+    def vcm(self, W, H, iterations, seed, mode=0, iter_begin=0, min_len=0, max_len=10,
+            radius_factor=0.003, alpha=0.75, path_range=None):
+        film = np.zeros((H, W, 3), np.float32)
+        st = Stats()
+        pb, pe = path_range or (0, W * H)
+        rc = self.L.cr_render_vcm(self.h, W, H, iter_begin, iterations, seed, mode, min_len, max_len,
+                                  radius_factor, alpha, pb, pe, fptr(film), C.byref(st))
         if rc:
             raise RuntimeError(self.L.cr_last_error().decode())
         return film, st

@@ -25,6 +25,14 @@ from winmad_rt import scenes  # noqa: E402
 
 REFDRV = os.path.join(REPO, "oracle", "_ref", "refdrv")
 
+# (scene, iterations, seed, radius factor or None = the reference's 0.003)
+VCM_CASES = [("torus64", 1, 5489, None), ("torus64", 3, 3, 0.05), ("spheres64", 2, 11, 0.1),
+             ("cboxb64x48", 3, 3, 0.05)]
+
+
+def vcm_fixture(name, it, seed, rf):
+    return f"vcm_{name}_i{it}_s{seed}" + ("" if rf is None else f"_r{rf}") + ".f32"
+
 
 def refdrv(*args, cwd):
     env = dict(os.environ, REFDRV_CWD=cwd)
@@ -133,6 +141,15 @@ def main():
     sp, pp = os.path.join(tmp, "spheres64.scene"), os.path.join(tmp, "spheres64.para")
     refdrv("bdpt", sp, pp, 2, 5489, os.path.join(HERE, "bdpt_spheres64_i2_s5489.f32"), cwd=tmp)
     refdrv("pt", sp, pp, 5489, os.path.join(HERE, "pt_spheres64_spp4_s5489.f32"), cwd=tmp)
+    # VCM (vertexcm.cpp + KDtree.h): the reference radius on torus, larger radii
+    # (baseRadius set through refdrv's RADIUS_FACTOR) so 64^2 films merge a lot;
+    # cbox in the BDPT orientation (raster x = film row) has emitter light vertices
+    sp = scenes.write(os.path.join(tmp, "cboxb64x48.scene"), scenes.cbox_scene(64, 48, "bdpt"))
+    pp = scenes.write(os.path.join(tmp, "cboxb64x48.para"), scenes.params_text(64, 48))
+    for name, it, seed, rf in VCM_CASES:
+        sp, pp = os.path.join(tmp, name + ".scene"), os.path.join(tmp, name + ".para")
+        extra = [] if rf is None else [rf]
+        refdrv("vcm", sp, pp, it, seed, os.path.join(HERE, vcm_fixture(name, it, seed, rf)), *extra, cwd=tmp)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print(json.dumps({k: v for k, v in meta.items() if "block32_mean" not in v}, indent=1))

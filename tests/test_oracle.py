@@ -205,6 +205,51 @@ def test_spheres_bdpt_and_pt_films_mt_serial_bit_exact():
     assert np.array_equal(film, ref)
 
 
+VCM_SCENES = {"torus64": (lambda: _scenes.torus(64, 64), 64, 64),
+              "spheres64": (lambda: _scenes.spheres(64, 64), 64, 64),
+              "cboxb64x48": (lambda: _scenes.cbox(64, 48, "bdpt"), 64, 48)}
+
+
+@pytest.mark.parametrize("name,it,seed,rf", [("torus64", 1, 5489, None), ("torus64", 3, 3, 0.05),
+                                             ("spheres64", 2, 11, 0.1), ("cboxb64x48", 3, 3, 0.05)])
+def test_vcm_film_mt_serial_bit_exact(name, it, seed, rf):
+    """VertexCM::runIteration (vertexcm.cpp:47-285): light pass with light
+    tracing, the point KD tree (KDtree.h:88-175), camera pass with NEE, vertex
+    connection and merging -- replayed on the MT stream, bit for bit, including
+    the radius schedule over iterations (:53-56) and the emitter light vertices
+    that inherit the previous BSDF's probabilities."""
+    maker, W, H = VCM_SCENES[name]
+    s = _oracle.Scene(maker())
+    film, st = s.vcm(W, H, it, seed, mode=0, radius_factor=0.003 if rf is None else rf)
+    fx = f"vcm_{name}_i{it}_s{seed}" + ("" if rf is None else f"_r{rf}") + ".f32"
+    ref = np.fromfile(os.path.join(GOLD, fx), np.float32).reshape(H, W, 3)
+    assert np.array_equal(film.view(np.uint32), ref.view(np.uint32))
+    assert st.vm_queries > 0 and st.vm_merged > 0 and st.vm_found >= st.vm_merged
+
+
+def test_vcm_kdtree_search_is_the_brute_force_set():
+    """KdTree::searchInRadius prunes with |pos[axis] - split| < radius, which is
+    exact in float: the found set equals every point with |q - p| < radius.  So
+    the GPU may replace the tree by a hash grid; only the summation order of the
+    merge contributions differs.  Point clouds with tied coordinates (the
+    comparator's address tie-break, KDtree.h:74-86) and duplicate points."""
+    import ctypes as C
+    rng = np.random.default_rng(3)
+    for n, grid in ((1, None), (2, None), (7, None), (500, None), (3000, 16), (3000, 4)):
+        p = rng.random((n, 3)).astype(np.float32)
+        if grid:
+            p = (np.floor(p * grid) / grid).astype(np.float32)
+        q = np.concatenate([p[: min(n, 200)] + rng.normal(0, 0.02, (min(n, 200), 3)).astype(np.float32),
+                            rng.random((200, 3)).astype(np.float32)])
+        out = np.zeros((len(q), 4), np.int64)
+        for r in (0.01, 0.07, 0.25):
+            _oracle.lib().cr_kat_vkd(_oracle.fptr(np.ascontiguousarray(p)), n,
+                                     _oracle.fptr(np.ascontiguousarray(q)), len(q), r,
+                                     out.ctypes.data_as(C.POINTER(C.c_int64)))
+            assert np.array_equal(out[:, :2], out[:, 2:]), (n, grid, r)
+        assert out[:, 0].sum() > 0
+
+
 def test_counter_mode_is_statistically_the_reference():
     """Counter-RNG oracle vs the reference's 256^2 x4 statistics: same estimator,
     independent random numbers => agreement to within Monte-Carlo noise."""
