@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define WR_API_VERSION 2
+#define WR_API_VERSION 3
 
 enum {
   WR_OK = 0,
@@ -93,6 +93,22 @@ typedef struct {
   int32_t count_work;
 } wr_path_params;
 
+/* VertexCM knobs (surfaceIntegrator/vertexcm.cpp:3-21, :47-66).  The merge
+ * radius of global iteration i is
+ *   max(radius_factor * sceneRadius / (i + 1)^(0.5 (1 - radius_alpha)), EPS). */
+typedef struct {
+  int32_t width, height;
+  int32_t iterations;        /* hard-coded 1 in the reference (:7)                   */
+  int32_t iter_begin;        /* global index of the first iteration (RNG key, radius) */
+  int32_t min_path_length;   /* 0 in the reference                                    */
+  int32_t max_path_length;   /* 10 in the reference; at most 10                      */
+  float radius_factor;       /* 0.003: baseRadius = factor * sceneSphere.sceneRadius  */
+  float radius_alpha;        /* 0.75                                                  */
+  uint32_t seed;
+  int32_t time_kernels;
+  int32_t count_work;
+} wr_vcm_params;
+
 enum { WR_K_TRACE = 0, WR_K_SHADE = 1, WR_K_RESOLVE = 2, WR_K_GEN = 3, WR_K_OTHER = 4, WR_K_NUM = 8 };
 
 typedef struct {
@@ -106,6 +122,9 @@ typedef struct {
   int64_t kernel_launches[WR_K_NUM];
   double trace_wall_ms;      /* time_kernels only: union of the traversal launch
                                 intervals over all pipelines (launches overlap) */
+  int64_t vm_queries;        /* VCM: range queries (KdTree::searchInRadius calls)  */
+  int64_t vm_found;          /* VCM: light vertices found within the radius       */
+  int64_t vm_merged;         /* VCM: RangeQuery::process merges (non-black BSDF)   */
 } wr_stats;
 
 /* ---- scene (Scene::init, scene/scene.cpp:469-489 + loadScene :259-467) ---- */
@@ -148,6 +167,13 @@ int wr_render_bdpt(wr_context* ctx, const wr_bdpt_params* p, float* film, int fi
  * (pathIntegrator.cpp:29-148).  film[height][width][3] accumulates the per-sample
  * radiance SUM (the reference's final film->scale(1/spp) is left to the caller). */
 int wr_render_path(wr_context* ctx, const wr_path_params* p, float* film, int film_on_device, wr_stats* stats);
+
+/* VertexCM::render (surfaceIntegrator/vertexcm.cpp:23-27, runIteration :47-285):
+ * vertex connection + vertex merging.  The reference's point KD tree over the
+ * light vertices (scene/KDtree.h) is replaced by a hash grid: searchInRadius
+ * reports exactly the vertices with |x - v| < radius, and so does the grid.
+ * film as wr_render_bdpt (pre-transpose, accumulated, not scaled). */
+int wr_render_vcm(wr_context* ctx, const wr_vcm_params* p, float* film, int film_on_device, wr_stats* stats);
 
 /* ---- output (ImageFilm::outputImage, scene/film.cpp:39-64; BDPT transpose
  * bidirPathTracing.cpp:29-46) ---- scale -> clamp [0,1] -> pow(1/gamma) ->

@@ -180,7 +180,7 @@ __device__ __forceinline__ V3 light_illuminance(const DLight& l, V3 pos, V3 r3, 
   return l.le;
 }
 __device__ __forceinline__ V3 light_emit(const DLight& l, V3 dr, V3 pr, V3* pos, V3* dir, float* epdf,
-                                         float* dpa) {  // light.cpp:40-67
+                                         float* dpa, float* cal = nullptr) {  // light.cpp:40-67
   *pos = sample_triangle(pr, l.p0, l.p0 + l.d1, l.p0 + l.d2);
   V3 ld = sample_cos_hemi(dr, epdf);
   *epdf *= l.inv_area;
@@ -188,6 +188,7 @@ __device__ __forceinline__ V3 light_emit(const DLight& l, V3 dr, V3 pr, V3* pos,
   Frame f{l.fx, l.fy, l.fz};
   *dir = to_world(f, ld);
   *dpa = l.inv_area;
+  if (cal) *cal = ld.z;
   return l.le * ld.z;
 }
 __device__ __forceinline__ V3 light_radiance(const DLight& l, V3 rd, float* dpa, float* epdf) {  // light.cpp:69-100

@@ -13,6 +13,7 @@
 // device or launch geometry, so any sharding of iterations over GPUs renders the
 // same film up to float summation order.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -81,11 +82,14 @@ struct StepCounters {
   int sq[kSlots];     // shadow / aux rays traced at step `slot` (light splats: slot 0 -> camera bounce 0)
   int di[kSlots];     // DI records finalized at step `slot`
   int fetch[kSlots];  // persistent-traversal cursor of the step's trace launch
+  int vcm_pending;    // VCM: light paths whose first vertex is an emitter (k_vcm_fixup)
+  int vcm_nverts;     // VCM: light vertices in the merge grid
 };
 struct DevCounters {
   int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
   unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
   unsigned long long closest, shadow, inner, leaves, refs;
+  unsigned long long vm_queries, vm_found, vm_merged;  // VCM range queries / vertices in radius / merges
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -432,9 +436,10 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
   }
 }
 
-// generateCameraSample (:418-452) + first extension ray
-__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGroup G_) {
-  const BdptArgs& A = G_.a[blockIdx.y];
+// generateCameraSample (:418-452) + first extension ray, for queue entry s;
+// returns the path index.  (VertexCM::generateCameraSample, vertexcm.cpp:446-479,
+// is the same plus dVM = 0.)
+__device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
   const BdptBuf& B = A.B;
   const DCam& cam = A.S.cam;
   const int P = A.P;
@@ -442,39 +447,42 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGr
   // path <-> pixel mapping stays the reference's (x = p / W, y = p % W, :422-423)
   const bool tiled = (A.W % 8) == 0 && (A.H % 8) == 0;
   const int tiles_y = A.W / 8;
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < P; s += gridDim.x * blockDim.x) {
-    int x, y;
-    if (tiled) {
-      const int t = s >> 6, w = s & 63;
-      x = (t / tiles_y) * 8 + (w >> 3);
-      y = (t % tiles_y) * 8 + (w & 7);
-    } else {
-      x = s / A.W;
-      y = s % A.W;
-    }
-    const int p = x * A.W + y;
-    Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), 0};
-    const V3 jit = rng.v();
-    const float sx = static_cast<float>(x) + jit.x, sy = static_cast<float>(y) + jit.y;
-    const V3 rp = t_point(cam.r2w, v3(sx, sy, 0.f));
-    const V3 d = normalize(rp - cam.pos);  // Ray(pos, p - pos) (camera.cpp:37-42)
-    const float cos_at = dot(cam.fwd, d);
-    const float ipd = cam.plane_dist / cos_at;
-    const float i2sa = (ipd * ipd) / cos_at;
-    st3(B.c_o, P, p, cam.pos);
-    st3(B.c_d, P, p, d);
-    st3(B.c_thr, P, p, v3(1.f, 1.f, 1.f));
-    B.c_dvcm[p] = static_cast<float>(P) / i2sa;
-    B.c_dvc[p] = 0.f;
-    B.c_len[p] = 1;
-    B.c_nspec[p] = 0;
-    B.c_ctr[p] = rng.ctr;
-    B.c_pix[p] = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
-    st3(B.q_o[0], P, s, cam.pos + d * WR_EPS);
-    st3(B.q_d[0], P, s, normalize(d));
-    B.q_path[0][s] = p;
+  int x, y;
+  if (tiled) {
+    const int t = s >> 6, w = s & 63;
+    x = (t / tiles_y) * 8 + (w >> 3);
+    y = (t % tiles_y) * 8 + (w & 7);
+  } else {
+    x = s / A.W;
+    y = s % A.W;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[kCamSlot] = P;
+  const int p = x * A.W + y;
+  Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), 0};
+  const V3 jit = rng.v();
+  const float sx = static_cast<float>(x) + jit.x, sy = static_cast<float>(y) + jit.y;
+  const V3 rp = t_point(cam.r2w, v3(sx, sy, 0.f));
+  const V3 d = normalize(rp - cam.pos);  // Ray(pos, p - pos) (camera.cpp:37-42)
+  const float cos_at = dot(cam.fwd, d);
+  const float ipd = cam.plane_dist / cos_at;
+  const float i2sa = (ipd * ipd) / cos_at;
+  st3(B.c_o, P, p, cam.pos);
+  st3(B.c_d, P, p, d);
+  st3(B.c_thr, P, p, v3(1.f, 1.f, 1.f));
+  B.c_dvcm[p] = static_cast<float>(P) / i2sa;
+  B.c_dvc[p] = 0.f;
+  B.c_len[p] = 1;
+  B.c_nspec[p] = 0;
+  B.c_ctr[p] = rng.ctr;
+  B.c_pix[p] = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
+  st3(B.q_o[0], P, s, cam.pos + d * WR_EPS);
+  st3(B.q_d[0], P, s, normalize(d));
+  B.q_path[0][s] = p;
+  return p;
+}
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGroup G_) {
+  const BdptArgs& A = G_.a[blockIdx.y];
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < A.P; s += gridDim.x * blockDim.x) camera_gen_one(A, s);
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[kCamSlot] = A.P;
 }
 
 // One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
@@ -813,7 +821,9 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_step(BdptGr
   else if (shade) camera_shade_body(A, slot, blockIdx.x - nres, gridDim.x - nres);
 }
 
-// getDirectIllumination's final combination (:533-607)
+// =============================================================== VCM
+#include "wr_vcm.h"
+static_assert(sizeof(VcmGroup) <= 4000, "kernel argument block too large");
 
 // =============================================================== PT
 struct PtBuf {
@@ -1066,10 +1076,11 @@ struct Pipe {
   StepCounters* sc = nullptr;  // [kGroup]
   Arena work;
   size_t work_key = 0;  // P for which `work` is laid out
-  int work_kind = 0;    // 1 bdpt, 2 pt
+  int work_kind = 0;    // 1 bdpt, 2 pt, 3 vcm (bdpt + vcm buffers)
   int work_sets = 0;    // buffer sets laid out
   BdptBuf bb[kGroup]{};
   PtBuf pb[kGroup]{};
+  VcmBuf vb[kGroup]{};
   std::vector<hipEvent_t> events;  // Timer marks (time_kernels)
   std::vector<int> ev_cat;
   size_t ev_used = 0;
@@ -1092,6 +1103,7 @@ struct wr_context {
   size_t film_tmp_n = 0;
   int grid = 2048;
   int cus = 256;
+  float sph_r = 0.f;  // sceneSphere.sceneRadius (scene.cpp:483-487): VCM base radius
   bool spheres = false;
   bool narrow = false;  // <= 65536 nodes, leaves <= 255 refs: 16-bit stack / pair offsets
   bool trace_log = false;  // WR_TRACE_LOG=1: per-launch ray counts and durations
@@ -1193,16 +1205,55 @@ void layout_pt(Arena& a, PtBuf& T, int P) {
   T.s_prim = a.take<int>(sP);
 }
 
+// VCM merge grid: 2^k buckets, at least twice the paths (light vertices
+// average ~0.5-1 per path in the reference scenes)
+uint32_t vcm_table(int P) {
+  uint32_t t = 1024;
+  while (t < 2u * static_cast<uint32_t>(P)) t <<= 1;
+  return t;
+}
+size_t vcm_scan_bytes(uint32_t T) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, static_cast<const int*>(nullptr), static_cast<int*>(nullptr),
+                                         static_cast<int>(T + 1));
+  return b;
+}
+void layout_vcm(Arena& a, VcmBuf& V, int P) {
+  const size_t sP = P, sV = size_t(kVMax) * P;
+  const uint32_t T = vcm_table(P);
+  V.l_dvm = a.take<float>(sP);
+  V.c_dvm = a.take<float>(sP);
+  V.l_spd = a.take<float>(sP);
+  V.l_spg = a.take<float>(sP);
+  V.l_scont = a.take<float>(sP);
+  V.l_shas = a.take<int>(sP);
+  V.v_dvm = a.take<float>(sV);
+  V.pending = a.take<int>(sP);
+  V.cnt = a.take<int>(size_t(T) + 1);
+  V.start = a.take<int>(size_t(T) + 1);
+  V.rec = a.take<float4>(4 * sV);
+  V.scan_bytes = vcm_scan_bytes(T);
+  V.scan_tmp = a.take<char>(V.scan_bytes);
+}
+
+// one buffer set of `kind` (into dst's set g, or only measured)
+void layout_set(Arena& a, Pipe* dst, int g, int kind, int P) {
+  BdptBuf b;
+  PtBuf t;
+  VcmBuf v;
+  if (kind == 2) {
+    layout_pt(a, dst ? dst->pb[g] : t, P);
+    return;
+  }
+  layout_bdpt(a, dst ? dst->bb[g] : b, P);
+  if (kind == 3) layout_vcm(a, dst ? dst->vb[g] : v, P);
+}
+
 int ensure_work(Pipe& p, int kind, int P, int sets) {
   if (p.work_kind == kind && p.work_key == static_cast<size_t>(P) && p.work_sets >= sets) return WR_OK;
   p.work_kind = 0;
   auto lay = [&](Arena& a, Pipe* dst) {
-    for (int g = 0; g < sets; ++g) {
-      BdptBuf b;
-      PtBuf t;
-      if (kind == 1) layout_bdpt(a, dst ? dst->bb[g] : b, P);
-      else layout_pt(a, dst ? dst->pb[g] : t, P);
-    }
+    for (int g = 0; g < sets; ++g) layout_set(a, dst, g, kind, P);
   };
   int rc = p.work.reserve(measure([&](Arena& a) { lay(a, nullptr); }));
   if (rc) return rc;
@@ -1219,18 +1270,9 @@ int ensure_work(Pipe& p, int kind, int P, int sets) {
 // failing.  Every render lays out full groups on all pipelines that fit, so a
 // short render (a warm-up) leaves the buffers of a long one in place.
 int pipelines_that_fit(wr_context* c, int kind, int P, int sets, int want) {
-  const size_t per = kind == 1 ? measure([&](Arena& a) {
-    for (int g = 0; g < sets; ++g) {
-      BdptBuf b;
-      layout_bdpt(a, b, P);
-    }
-  })
-                               : measure([&](Arena& a) {
-                                   for (int g = 0; g < sets; ++g) {
-                                     PtBuf t;
-                                     layout_pt(a, t, P);
-                                   }
-                                 });
+  const size_t per = measure([&](Arena& a) {
+    for (int g = 0; g < sets; ++g) layout_set(a, nullptr, g, kind, P);
+  });
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return want;
   size_t held = 0;
@@ -1362,6 +1404,9 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
     sum.inner += h.inner;
     sum.leaves += h.leaves;
     sum.refs += h.refs;
+    sum.vm_queries += h.vm_queries;
+    sum.vm_found += h.vm_found;
+    sum.vm_merged += h.vm_merged;
     for (int k = 0; k < 8; ++k) sum.stamps[k] += h.stamps[k];
   }
   st->closest_rays += static_cast<int64_t>(sum.closest);
@@ -1369,6 +1414,9 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
   st->inner_visits += static_cast<int64_t>(sum.inner);
   st->leaf_visits += static_cast<int64_t>(sum.leaves);
   st->prim_refs += static_cast<int64_t>(sum.refs);
+  st->vm_queries += static_cast<int64_t>(sum.vm_queries);
+  st->vm_found += static_cast<int64_t>(sum.vm_found);
+  st->vm_merged += static_cast<int64_t>(sum.vm_merged);
   if (c->stamps) {
     static const char* names[6] = {"refill", "walk", "leaf-setup", "pair-tests", "decision", "write"};
     double tot = 0;
@@ -1653,6 +1701,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   d.root_l = v3(s.root_l.x, s.root_l.y, s.root_l.z);
   d.root_r = v3(s.root_r.x, s.root_r.y, s.root_r.z);
   d.max_stack = std::max(1, s.max_stack);
+  c->sph_r = s.sph_r;
   d.nlights = static_cast<int>(s.lights.size());
   d.lights = dl;
   d.mats = dm;
@@ -1887,6 +1936,129 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
       const int nres = shade_grid(c, sq_max);
       hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot, nres,
                          more ? 1 : 0);
+      tm.mark(WR_K_SHADE);
+    }
+  }
+  HIPCHK(hipGetLastError());
+  if (int rc = finish_render(c, np, st, t0)) return rc;
+  return film_return(c, film, film_on_device, nf);
+}
+
+int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film_on_device, wr_stats* st) {
+  if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
+  if (prm->width <= 0 || prm->height <= 0 || prm->iterations < 0) return fail(WR_E_ARG, "bad film size");
+  if (static_cast<int64_t>(prm->width) * prm->height >= (1 << 30) / (kVMax + 2))
+    return fail(WR_E_ARG, "film too large for one context");
+  if (prm->max_path_length < 1 || prm->max_path_length > kVMax + 1)
+    return fail(WR_E_ARG, "max_path_length must be in 1..10 (light-vertex store sized for the reference's 10)");
+  if (prm->min_path_length < 0 || !(prm->radius_factor > 0.f) || !(prm->radius_alpha <= 1.f))
+    return fail(WR_E_ARG, "bad min_path_length / radius_factor / radius_alpha");
+  if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "VCM needs at least one area light");
+  HIPCHK(hipSetDevice(c->device));
+  const double t0 = host_now();
+  const int P = prm->width * prm->height;
+  const int ngroups = (prm->iterations + kGroup - 1) / kGroup;
+  const int fit = pipelines_that_fit(c, 3, P, kGroup, c->npipes);
+  if (fit < 1) return WR_E_HIP;  // message set by the allocation
+  const int np = std::max(1, std::min(fit, ngroups));
+  float* dfilm = nullptr;
+  const size_t nf = size_t(P) * 3;
+  if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
+  begin_render(c, np, prm->time_kernels);
+  VcmArgs X0;
+  BdptArgs& A0 = X0.a;
+  A0.S = c->ds;
+  A0.film = dfilm;
+  A0.W = prm->width;
+  A0.H = prm->height;
+  A0.P = P;
+  A0.seed = prm->seed;
+  A0.ctl = 0;
+  A0.maxlen = prm->max_path_length;
+  A0.faithful = 1;
+  X0.minlen = prm->min_path_length;
+  X0.N = static_cast<float>(prm->height * prm->width);
+  X0.org = c->ds.root_l;
+  const uint32_t T = vcm_table(P);
+  X0.tmask = T - 1;
+  const float base_radius = prm->radius_factor * c->sph_r;  // VertexCM::init (:13)
+  const int maxlen = A0.maxlen;
+  const bool count = prm->count_work != 0;
+  const int g = shade_grid(c, P);
+  for (int gi = 0; gi < ngroups; ++gi) {
+    Pipe& pp = c->pipes[gi % np];
+    const hipStream_t sm = pp.stream;
+    Timer tm(c, &pp);
+    const int it0 = gi * kGroup, gn = std::min(kGroup, prm->iterations - it0);
+    VcmGroup GA;
+    for (int m = 0; m < gn; ++m) {
+      VcmArgs& X = GA.a[m];
+      X = X0;
+      X.a.B = pp.bb[m];
+      X.V = pp.vb[m];
+      X.a.ctr = pp.ctr;
+      X.a.sc = pp.sc + m;
+      const int it = prm->iter_begin + it0 + m;
+      X.a.iter = static_cast<uint32_t>(it);
+      // runIteration's radius schedule and MIS factors (:50-64), host float
+      float radius = base_radius;
+      radius /= powf(static_cast<float>(it + 1), 0.5f * (1.f - prm->radius_alpha));
+      radius = (radius < WR_EPS) ? WR_EPS : radius;
+      const float r2 = radius * radius;
+      X.radius = radius;
+      X.vm_norm = 1.f / (r2 * WR_PI * X.N);
+      const float eta = (WR_PI * r2) * X.N;
+      X.mis_vm = eta;
+      X.mis_vc = 1.f / eta;
+      X.rq = radius * 1.0009765625f;
+      X.inv_cs = 1.f / (2.f * X.rq * 1.0009765625f);
+    }
+    auto sq = [&](int m, int slot) {
+      const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
+      return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim);
+    };
+    auto ext = [&](int m, int slot) {
+      const BdptBuf& B = pp.bb[m];
+      const int q = slot & 1;
+      return rq(B.q_o[q], B.q_d[q], P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
+    };
+    const int sq_max = pp.bb[0].cap_sq;
+    HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
+    // ---------------- light pass (:67-140)
+    hipLaunchKernelGGL(k_vcm_light_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
+    tm.mark(WR_K_GEN);
+    for (int b = 0; b < maxlen - 1; ++b) {
+      QueueList ql;
+      for (int m = 0; m < gn; ++m) ql.add(ext(m, b), P);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays);
+      hipLaunchKernelGGL(k_vcm_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
+      tm.mark(WR_K_SHADE);
+    }
+    // ---------------- light vertices -> merge grid (replaces the KdTree, :152)
+    hipLaunchKernelGGL(k_vcm_fixup, dim3(64, gn), dim3(kShadeBlock), 0, sm, GA);
+    for (int m = 0; m < gn; ++m) HIPCHK(hipMemsetAsync(pp.vb[m].cnt, 0, (size_t(T) + 1) * sizeof(int), sm));
+    hipLaunchKernelGGL(k_vgrid_count, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
+    for (int m = 0; m < gn; ++m) {
+      size_t bytes = pp.vb[m].scan_bytes;
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(pp.vb[m].scan_tmp, bytes, pp.vb[m].cnt, pp.vb[m].start,
+                                              static_cast<int>(T + 1), sm));
+    }
+    hipLaunchKernelGGL(k_vgrid_scatter, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
+    tm.mark(WR_K_OTHER);
+    // ---------------- camera pass (:157-283)
+    hipLaunchKernelGGL(k_vcm_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
+    tm.mark(WR_K_GEN);
+    for (int b = 0; b <= maxlen; ++b) {
+      const int slot = kCamSlot + b;
+      const bool more = b < maxlen;
+      QueueList ql;
+      for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), sq_max);
+      if (more)
+        for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays);
+      const int nres = shade_grid(c, sq_max);
+      hipLaunchKernelGGL(k_vcm_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot,
+                         nres, more ? 1 : 0);
       tm.mark(WR_K_SHADE);
     }
   }

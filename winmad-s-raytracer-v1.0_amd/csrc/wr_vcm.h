@@ -1,0 +1,631 @@
+// VertexCM (surfaceIntegrator/vertexcm.{h,cpp}) on the BDPT wavefront of
+// wr_render.hip.  Included there, inside its anonymous namespace, after the
+// BDPT kernels (it reuses BdptBuf / BdptArgs, camera_gen_one and
+// sq_resolve_body).
+//
+//   light pass  : gen -> [trace -> shade] x 9                 (:67-140)
+//   fix-up      : emitter-first light vertices (stale BSDF, below)
+//   merge grid  : count -> exclusive scan -> scatter          (replaces :152)
+//   camera pass : gen -> [trace -> resolve + shade] x 11      (:157-283)
+//
+// The reference's point KD tree (scene/KDtree.h:88-175) answers
+// searchInRadius with exactly the vertices v for which
+// sqrtf(|x - v|^2) < radius (its pruning test |x[axis] - split| < radius is
+// exact in float; tests/test_oracle.py checks this).  The GPU finds the same
+// set in a hash grid of cell size >= 2 * radius: the query visits every cell
+// overlapping [x - r', x + r'] per axis with r' = r (1 + 2^-10), which holds
+// every vertex the float test can accept (|fl(x - v)| <= fl-distance < r, and
+// float subtraction, scaling and floor are monotone), then applies the
+// reference's test.  Only the summation order of the merged contributions
+// differs.
+
+struct VcmBuf {
+  float *l_dvm, *c_dvm;  // dVM of the light / camera subpath state (vertexcm.h:36)
+  // Probabilities of the last non-emitter BSDF built on each light path (the
+  // emitter-vertex quirk, k_vcm_light_shade)
+  float *l_spd, *l_spg, *l_scont;
+  int* l_shas;
+  float* v_dvm;    // [kVMax][P] beside BdptBuf's vertex store
+  int* pending;    // light paths whose first vertex is an emitter
+  int* cnt;        // [T + 1] vertices per grid bucket, then 0 after the scatter
+  int* start;      // [T + 1] exclusive scan of cnt
+  float4* rec;     // [kVMax * P][4] merge records, bucket-sorted
+  void* scan_tmp;  // hipcub scan scratch
+  size_t scan_bytes;
+};
+
+struct VcmArgs {
+  BdptArgs a;  // S, B, counters, film, W / H / P, seed, iter, maxlen
+  VcmBuf V;
+  int minlen;
+  float N;                               // lightSubPathNum (:49-51)
+  float radius, vm_norm, mis_vm, mis_vc;  // (:53-64)
+  V3 org;                                // grid origin (root box corner)
+  float inv_cs, rq;                      // 1 / cell size, query half-width r (1 + 2^-10)
+  uint32_t tmask;                        // T - 1
+};
+struct VcmGroup {
+  VcmArgs a[kGroup];
+};
+
+__device__ __forceinline__ int vcm_cell(float x, float org, float inv_cs) {
+  const float c = floorf((x - org) * inv_cs);
+  return static_cast<int>(clampv(c, -1073741824.f, 1073741824.f));
+}
+__device__ __forceinline__ uint32_t vcm_hash(int x, int y, int z, uint32_t mask) {
+  return ((static_cast<uint32_t>(x) * 73856093u) ^ (static_cast<uint32_t>(y) * 19349663u) ^
+          (static_cast<uint32_t>(z) * 83492791u)) &
+         mask;
+}
+__device__ __forceinline__ uint32_t vcm_bucket(const VcmArgs& X, V3 p) {
+  return vcm_hash(vcm_cell(p.x, X.org.x, X.inv_cs), vcm_cell(p.y, X.org.y, X.inv_cs),
+                  vcm_cell(p.z, X.org.z, X.inv_cs), X.tmask);
+}
+
+// generateLightSample (:287-330) + the first extension ray
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_vcm_light_gen(VcmGroup G_) {
+  const VcmArgs& X = G_.a[blockIdx.y];
+  const BdptArgs& A = X.a;
+  const BdptBuf& B = A.B;
+  const VcmBuf& V = X.V;
+  const int P = A.P;
+  const float lpp = 1.f / static_cast<float>(A.S.nlights);
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), 0};
+    const int id = min(static_cast<int>(rng.f() * static_cast<float>(A.S.nlights)), A.S.nlights - 1);
+    const DLight L = A.S.lights[id];
+    V3 pos, dir, rad;
+    float epdf = 0.f, dpdf = 0.f, cal = 0.f;
+    for (int tries = 0; tries < 64; ++tries) {  // posRand3 drawn first
+      V3 pr = rng.v();
+      V3 dr = rng.v();
+      rad = light_emit(L, dr, pr, &pos, &dir, &epdf, &dpdf, &cal);
+      if (epdf > 1e-7f) break;
+    }
+    V3 thr = rad;
+    epdf = smax(epdf, 1e-7f);
+    epdf *= lpp;
+    dpdf *= lpp;
+    thr = div_plain(thr, epdf);
+    const float dvc = cal / epdf;  // AreaLight: finite, not delta -> cosAtLight
+    st3(B.l_o, P, p, pos);
+    st3(B.l_d, P, p, dir);
+    st3(B.l_thr, P, p, thr);
+    B.l_dvcm[p] = dpdf / epdf;
+    B.l_dvc[p] = dvc;
+    V.l_dvm[p] = dvc * X.mis_vc;
+    B.l_len[p] = 1;
+    B.l_ctr[p] = rng.ctr;
+    B.v_count[p] = 0;
+    V.l_shas[p] = 0;
+    st3(B.q_o[0], P, p, pos + dir * WR_EPS);  // Ray(origin + dir * EPS, dir) (:79-80)
+    st3(B.q_d[0], P, p, normalize(dir));
+    B.q_path[0][p] = p;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = P;
+}
+
+// VertexCM::sampleScattering (:386-444)
+__device__ __forceinline__ bool vcm_scatter(const VcmArgs& X, Rng& rng, const Bsdf& b, V3 hit, V3& o, V3& dir,
+                                            V3& thr, float& dvcm, float& dvc, float& dvm) {
+  float dpdf = 0.f, cos_wo = 0.f;
+  int type;
+  V3 wo = dir;
+  const V3 f = bsdf_sample(b, X.a.S.mats, rng.v(), &wo, &dpdf, &cos_wo, &type);
+  if (black(f)) return false;
+  dir = wo;
+  float rpdf = dpdf;
+  if ((type & T_SPEC) == 0) rpdf = bsdf_pdf(b, X.a.S.mats, dir, true);
+  const float cp = b.cont;
+  if (rng.f() > cp) return false;
+  dpdf *= cp;
+  rpdf *= cp;
+  if (type & T_SPEC) {
+    dvcm = 0.f;
+    dvc *= cos_wo;
+    dvm *= cos_wo;
+  } else {
+    dvc = (cos_wo / dpdf) * (dvc * rpdf + dvcm + X.mis_vm);
+    dvm = (cos_wo / dpdf) * (dvm * rpdf + dvcm * X.mis_vc + 1.f);
+    dvcm = 1.f / dpdf;
+  }
+  o = hit;
+  thr = mul(thr, f) * (cos_wo / dpdf);
+  return true;
+}
+
+// One light-subpath vertex (:82-137): light-vertex store, connectToCamera
+// (:332-384, splat ray queued with the camera primaries), scattering.
+//
+// Emitter hits: BSDF::init skips calcComponentProb for matId < 0 (bsdf.h:78-83),
+// so componentProb / continueProb keep what the stack slot held -- the BSDF
+// built before it in the reference's serial loop.  On a path's later vertex
+// that is this path's previous vertex (l_s*); on its first vertex it is the
+// last non-emitter BSDF of an earlier light path, known only after the whole
+// pass: such vertices are stored provisionally and settled by k_vcm_fixup.
+// Emitter vertices never connect (BSDF::f is black for matId < 0) and end the
+// path (BSDF::sample too), but a non-delta one is merged (vertexcm.h:77-78).
+__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(VcmGroup G_, int slot) {
+  const VcmArgs& X = G_.a[blockIdx.y];
+  const BdptArgs& A = X.a;
+  const BdptBuf& B = A.B;
+  const VcmBuf& V = X.V;
+  const DevScene& S = A.S;
+  const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
+  const int n = A.sc->ext[slot];
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
+  const int gstride = gridDim.x * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;  // whole waves reach the appends
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    bool ext = false, splat = false, pend = false;
+    V3 e_o, e_d, s_o, s_d, s_val;
+    int s_pix = -1, p = -1;
+    if (j < n) {
+      p = B.q_path[cur][j];
+      const int prim = B.q_prim[cur][j];
+      if (prim >= 0) {
+        const float t = B.q_t[cur][j];
+        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
+        const Hit h = rebuild_hit(S, prim, t, o, d);
+        Bsdf b;
+        bsdf_init(b, -d, h.n, h.mat, S.mats);
+        if (b.mat != 0) {
+          int len = B.l_len[p];
+          if (b.mat < 0) {
+            if (len > 1) {
+              b.pd = V.l_spd[p];
+              b.pg = V.l_spg[p];
+              b.cont = V.l_scont[p];
+              b.delta = (cmpf(b.pd) == 0 && cmpf(b.pg) == 0);
+            } else {
+              pend = true;  // decided by k_vcm_fixup
+            }
+          } else {
+            V.l_spd[p] = b.pd;
+            V.l_spg[p] = b.pg;
+            V.l_scont[p] = b.cont;
+            V.l_shas[p] = 1;
+          }
+          float dvcm = B.l_dvcm[p], dvc = B.l_dvc[p], dvm = V.l_dvm[p];
+          V3 thr = ld3(B.l_thr, P, p);
+          // `pathLength > 1 || isFiniteLight == 1` (:94-95): isFiniteLight is a
+          // signed 1-bit field (vertexcm.h:31) that reads back -1, so only the
+          // path length counts -- unlike BDPT
+          if (len > 1) dvcm *= (t * t);
+          dvcm /= fabsf(b.wi.z);
+          dvc /= fabsf(b.wi.z);
+          dvm /= fabsf(b.wi.z);
+          if (!b.delta) {  // lightVertices.push_back (:98-113)
+            const int k = B.v_count[p];
+            const int vs = k * P + p;
+            st3(B.v_pos, kVMax * P, vs, h.p);
+            st3(B.v_n, kVMax * P, vs, h.n);
+            st3(B.v_wi, kVMax * P, vs, b.wi);
+            st3(B.v_thr, kVMax * P, vs, thr);
+            B.v_dvcm[vs] = dvcm;
+            B.v_dvc[vs] = dvc;
+            V.v_dvm[vs] = dvm;
+            B.v_cont[vs] = b.cont;
+            B.v_pd[vs] = b.pd;
+            B.v_pg[vs] = b.pg;
+            B.v_len[vs] = len;
+            B.v_mat[vs] = b.mat;
+            B.v_count[p] = k + 1;
+            if (b.mat > 0 && len + 1 >= X.minlen) {  // connectToCamera (:116-127, :332-384)
+              const DCam& cam = S.cam;
+              const V3 ip = t_point(cam.w2r, h.p);
+              if (check_raster(cam, ip.x, ip.y)) {
+                V3 dtc = cam.pos - h.p;
+                if (cmpf(dot(-dtc, cam.fwd)) > 0) {
+                  const float d2 = sqr_len(dtc);
+                  const float dist = sqrtf(d2);
+                  dtc = div_guarded(dtc, dist);
+                  float cos_to = 0.f, dp, rp;
+                  const V3 f = bsdf_f(b, S.mats, dtc, &cos_to, &dp, &rp);
+                  if (!black(f)) {
+                    rp *= b.cont;
+                    const float cos_at = dot(-dtc, cam.fwd);
+                    const float ipd = cam.plane_dist / cos_at;
+                    const float i2sa = (ipd * ipd) / cos_at;
+                    const float i2s = i2sa * fabsf(cos_to) / d2;
+                    const float wl = (i2s / X.N) * (X.mis_vm + dvcm + dvc * rp);
+                    const float w = 1.f / (wl + 1.f);
+                    const float s2i = 1.f / i2s;
+                    const V3 res = div_plain(mul(thr, f) * w, X.N * s2i);
+                    if (!black(res)) {
+                      splat = true;
+                      s_o = h.p;
+                      s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
+                      s_val = res;
+                      s_pix = pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W);
+                    }
+                  }
+                }
+              }
+            }
+          }
+          if (b.mat > 0 && !(len + 2 > A.maxlen)) {  // (:129-133); an emitter's sample is black
+            Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), B.l_ctr[p]};
+            V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
+            if (vcm_scatter(X, rng, b, h.p, lo, ld, thr, dvcm, dvc, dvm)) {
+              ext = true;
+              ++len;
+              e_o = lo + ld * WR_EPS;
+              e_d = normalize(ld);
+              st3(B.l_o, P, p, lo);
+              st3(B.l_d, P, p, ld);
+              st3(B.l_thr, P, p, thr);
+              B.l_dvcm[p] = dvcm;
+              B.l_dvc[p] = dvc;
+              V.l_dvm[p] = dvm;
+              B.l_len[p] = len;
+            }
+            B.l_ctr[p] = rng.ctr;
+          }
+        }
+      }
+    }
+    const int pi = wave_append(&A.sc->vcm_pending, pend);
+    if (pend) V.pending[pi] = p;
+    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
+    if (ext) {
+      st3(B.q_o[nxt], P, ei, e_o);
+      st3(B.q_d[nxt], P, ei, e_d);
+      B.q_path[nxt][ei] = p;
+    }
+    const int si = wave_append(&A.sc->sq[kCamSlot], splat);  // traced with the camera primaries
+    if (splat) {
+      const BdptBuf::Sq& Q = B.sq[kCamSlot & 1];
+      st3(Q.o, B.cap_sq, si, s_o);
+      st3(Q.d, B.cap_sq, si, s_d);
+      st3(Q.tgt, B.cap_sq, si, S.cam.pos);
+      st3(Q.val, B.cap_sq, si, s_val);
+      Q.meta[si] = SQ_SPLAT << 30;
+      Q.pix[si] = s_pix;
+    }
+  }
+}
+
+// Emitter vertices that are their path's first: the probabilities of the last
+// non-emitter BSDF of the nearest earlier light path that built one (zero at
+// the iteration's start), then isDelta from them (bsdf.h:86).  A delta one is
+// dropped from the store.  Rare (a light path leaving one emitter and hitting
+// another first); the backward walk is per entry.
+__global__ void __launch_bounds__(kShadeBlock) k_vcm_fixup(VcmGroup G_) {
+  const VcmArgs& X = G_.a[blockIdx.y];
+  const BdptBuf& B = X.a.B;
+  const VcmBuf& V = X.V;
+  const int n = X.a.sc->vcm_pending;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int p = V.pending[i];
+    int q = p - 1;
+    while (q >= 0 && V.l_shas[q] == 0) --q;
+    float pd = 0.f, pg = 0.f, cont = 0.f;
+    if (q >= 0) {
+      pd = V.l_spd[q];
+      pg = V.l_spg[q];
+      cont = V.l_scont[q];
+    }
+    if (cmpf(pd) == 0 && cmpf(pg) == 0) {
+      B.v_count[p] = 0;  // its only vertex (slot 0)
+    } else {
+      B.v_pd[p] = pd;
+      B.v_pg[p] = pg;
+      B.v_cont[p] = cont;
+    }
+  }
+}
+
+// Merge grid, pass 1: vertices per bucket (and the total, for the stats)
+__global__ void __launch_bounds__(kShadeBlock) k_vgrid_count(VcmGroup G_) {
+  const VcmArgs& X = G_.a[blockIdx.y];
+  const BdptBuf& B = X.a.B;
+  const int P = X.a.P;
+  const int gstride = gridDim.x * blockDim.x;
+  const int nround = (P + gstride - 1) / gstride * gstride;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < nround; p += gstride) {
+    const int nv = p < P ? B.v_count[p] : 0;
+    for (int k = 0; k < nv; ++k) {
+      const V3 pos = ld3(B.v_pos, kVMax * P, k * P + p);
+      atomicAdd(&X.V.cnt[vcm_bucket(X, pos)], 1);
+    }
+    const unsigned long long tot = wave_sum(static_cast<unsigned long long>(nv));
+    if (lane_id() == 0 && tot) atomicAdd(&X.a.sc->vcm_nverts, static_cast<int>(tot));
+  }
+}
+
+// Merge grid, pass 2 (after the exclusive scan cnt -> start): bucket-sorted
+// merge records {pos, pathLength}, {wiWorld, continueProb}, {throughput, dVCM},
+// {dVM} -- what RangeQuery::process reads of a light vertex (vertexcm.h:59-96).
+__global__ void __launch_bounds__(kShadeBlock) k_vgrid_scatter(VcmGroup G_) {
+  const VcmArgs& X = G_.a[blockIdx.y];
+  const BdptBuf& B = X.a.B;
+  const VcmBuf& V = X.V;
+  const int P = X.a.P;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    const int nv = B.v_count[p];
+    for (int k = 0; k < nv; ++k) {
+      const int vs = k * P + p;
+      const V3 pos = ld3(B.v_pos, kVMax * P, vs);
+      const uint32_t h = vcm_bucket(X, pos);
+      const int idx = V.start[h] + atomicSub(&V.cnt[h], 1) - 1;
+      const Frame fr = frame_from_z(ld3(B.v_n, kVMax * P, vs));
+      const V3 ldir = to_world(fr, ld3(B.v_wi, kVMax * P, vs));  // BSDF::wiWorld (bsdf.h:101-104)
+      const V3 thr = ld3(B.v_thr, kVMax * P, vs);
+      float4* r = V.rec + 4 * static_cast<size_t>(idx);
+      r[0] = make_float4(pos.x, pos.y, pos.z, __int_as_float(B.v_len[vs]));
+      r[1] = make_float4(ldir.x, ldir.y, ldir.z, B.v_cont[vs]);
+      r[2] = make_float4(thr.x, thr.y, thr.z, B.v_dvcm[vs]);
+      r[3] = make_float4(V.v_dvm[vs], 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+// Vertex merging at one camera vertex: KdTree::searchInRadius (KDtree.h:141-175)
+// + RangeQuery::process (vertexcm.h:59-96).  Returns the contribution sum.
+__device__ __forceinline__ V3 vcm_merge(const VcmArgs& X, const Bsdf& b, V3 hp, int len, float cdvcm, float cdvm,
+                                        unsigned& found, unsigned& merged) {
+  const VcmBuf& V = X.V;
+  V3 acc = v3(0.f, 0.f, 0.f);
+  const int x0 = vcm_cell(hp.x - X.rq, X.org.x, X.inv_cs), x1 = vcm_cell(hp.x + X.rq, X.org.x, X.inv_cs);
+  const int y0 = vcm_cell(hp.y - X.rq, X.org.y, X.inv_cs), y1 = vcm_cell(hp.y + X.rq, X.org.y, X.inv_cs);
+  const int z0 = vcm_cell(hp.z - X.rq, X.org.z, X.inv_cs), z1 = vcm_cell(hp.z + X.rq, X.org.z, X.inv_cs);
+  const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, ncell = nx * ny * (z1 - z0 + 1);
+  for (int c = 0; c < ncell; ++c) {
+    const int cx = x0 + c % nx, cy = y0 + (c / nx) % ny, cz = z0 + c / (nx * ny);
+    const uint32_t h = vcm_hash(cx, cy, cz, X.tmask);
+    bool dup = false;  // two cells of this query in one bucket: visit it once
+    for (int e = 0; e < c && !dup; ++e)
+      dup = vcm_hash(x0 + e % nx, y0 + (e / nx) % ny, z0 + e / (nx * ny), X.tmask) == h;
+    if (dup) continue;
+    const int i1 = V.start[h + 1];
+    for (int i = V.start[h]; i < i1; ++i) {
+      const float4 r0 = V.rec[4 * static_cast<size_t>(i)];
+      const V3 dd = hp - v3(r0.x, r0.y, r0.z);
+      if (!(sqrtf(sqr_len(dd)) < X.radius)) continue;
+      ++found;
+      const int llen = __float_as_int(r0.w);
+      if (llen + len > X.a.maxlen || llen + len < X.minlen) continue;
+      const float4 r1 = V.rec[4 * static_cast<size_t>(i) + 1];
+      float cos_c = 0.f, dp, rp;
+      const V3 f = bsdf_f(b, X.a.S.mats, v3(r1.x, r1.y, r1.z), &cos_c, &dp, &rp);
+      if (black(f)) continue;
+      ++merged;
+      const float4 r2 = V.rec[4 * static_cast<size_t>(i) + 2];
+      const float ldvm = V.rec[4 * static_cast<size_t>(i) + 3].x;
+      dp *= b.cont;
+      rp *= r1.w;
+      const float wl = r2.w * X.mis_vc + ldvm * dp;
+      const float wc = cdvcm * X.mis_vc + cdvm * rp;
+      const float w = 1.f / (wl + 1.f + wc);
+      acc = acc + mul(f, v3(r2.x, r2.y, r2.z)) * w;
+    }
+  }
+  return acc;
+}
+
+// generateCameraSample (:446-479)
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_vcm_camera_gen(VcmGroup G_) {
+  const VcmArgs& X = G_.a[blockIdx.y];
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < X.a.P; s += gridDim.x * blockDim.x) {
+    const int p = camera_gen_one(X.a, s);
+    X.V.c_dvm[p] = 0.f;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) X.a.sc->ext[kCamSlot] = X.a.P;
+}
+
+// One camera-subpath vertex (:166-281): emitter hit (getLightRadiance
+// :481-514), NEE (getDirectIllumination :516-573, shadow ray queued), vertex
+// connections to the paired light path (:575-636, shadow rays queued), vertex
+// merging (inline), scattering.
+__device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot, int bid, int nblk) {
+  const BdptArgs& A = X.a;
+  const BdptBuf& B = A.B;
+  const VcmBuf& V = X.V;
+  const DevScene& S = A.S;
+  const int P = A.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;
+  const int n = A.sc->ext[slot];
+  if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
+  const bool any_verts = A.sc->vcm_nverts > 0;
+  const int gstride = nblk * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;
+  const float lpp = 1.f / static_cast<float>(S.nlights);
+  const BdptBuf::Sq& Q = B.sq[(slot + 1) & 1];  // rays traced at the next step
+  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    bool ext = false, conn_phase = false, nee = false, query = false;
+    int p = -1, pix = -1, nv = 0, len = 0;
+    unsigned found = 0, merged = 0;
+    V3 hp{}, thr{}, cthr{}, e_o{}, e_d{}, nee_tgt{}, nee_d{}, nee_val{};
+    float dvcm = 0.f, dvc = 0.f, dvm = 0.f, cdvcm = 0.f, cdvc = 0.f;
+    Bsdf b;
+    b.mat = 0;
+    if (j < n) {
+      p = B.q_path[cur][j];
+      const int prim = B.q_prim[cur][j];
+      if (prim >= 0) {
+        const float t = B.q_t[cur][j];
+        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
+        const Hit h = rebuild_hit(S, prim, t, o, d);
+        bsdf_init(b, -d, h.n, h.mat, S.mats);
+        if (b.mat != 0) {
+          hp = h.p;
+          pix = B.c_pix[p];
+          dvcm = B.c_dvcm[p];
+          dvc = B.c_dvc[p];
+          dvm = V.c_dvm[p];
+          len = B.c_len[p];
+          thr = ld3(B.c_thr, P, p);
+          dvcm *= (t * t);  // (:190-193)
+          dvcm /= fabsf(b.wi.z);
+          dvc /= fabsf(b.wi.z);
+          dvm /= fabsf(b.wi.z);
+          cthr = thr;
+          cdvcm = dvcm;
+          cdvc = dvc;
+          if (h.mat < 0) {  // (:195-209)
+            if (len >= X.minlen) {
+              const DLight L = S.lights[-h.mat - 1];
+              float dpa, ep;
+              V3 r = light_radiance(L, d, &dpa, &ep);
+              if (!black(r)) {
+                if (len != 1) {
+                  dpa *= lpp;
+                  ep *= lpp;
+                  const float wc = dpa * dvcm + ep * dvc;
+                  r = r * (1.f / (1.f + wc));
+                }
+                film_add(A.film, pix, mul(thr, r));
+              }
+            }
+          } else if (len < A.maxlen) {
+            Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), B.c_ctr[p]};
+            if (!b.delta && len + 1 >= X.minlen) {  // getDirectIllumination (:216-222, :516-573)
+              const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
+              const DLight L = S.lights[lid];
+              V3 dtl;
+              float dist = 0.f, dpdf = 0.f, epdf = 0.f, cal = 0.f;
+              const V3 illu = light_illuminance(L, hp, rng.v(), &dtl, &dist, &dpdf, &epdf, &cal);
+              if (!black(illu)) {
+                float cos_to = 0.f, bdp, brp;
+                const V3 bf = bsdf_f(b, S.mats, dtl, &cos_to, &bdp, &brp);
+                if (!black(bf)) {
+                  bdp *= b.cont;  // AreaLight is not delta
+                  brp *= b.cont;
+                  const float wl = bdp / (lpp * dpdf);
+                  const float wc = (epdf * cos_to / (dpdf * cal)) * (X.mis_vm + dvcm + dvc * brp);
+                  const float w = 1.f / (wl + 1.f + wc);
+                  const V3 res = mul(illu, bf) * (w * cos_to / (lpp * dpdf));
+                  if (!black(res)) {
+                    nee = true;
+                    nee_d = normalize(dtl);
+                    nee_tgt = hp + dtl * dist;
+                    nee_val = mul(thr, res);
+                  }
+                }
+              }
+            }
+            if (!b.delta) {
+              conn_phase = true;
+              nv = B.v_count[p];
+              if (any_verts) {  // vertex merging (:265-276)
+                query = true;
+                const V3 acc = vcm_merge(X, b, hp, len, dvcm, dvm, found, merged);
+                film_add(A.film, pix, mul(thr, acc) * X.vm_norm);
+              }
+            }
+            V3 so = ld3(B.c_o, P, p), sd = ld3(B.c_d, P, p);
+            if (vcm_scatter(X, rng, b, hp, so, sd, thr, dvcm, dvc, dvm)) {
+              ext = true;
+              e_o = so + sd * WR_EPS;
+              e_d = normalize(sd);
+              st3(B.c_o, P, p, so);
+              st3(B.c_d, P, p, sd);
+              st3(B.c_thr, P, p, thr);
+              B.c_dvcm[p] = dvcm;
+              B.c_dvc[p] = dvc;
+              V.c_dvm[p] = dvm;
+              B.c_len[p] = len + 1;
+            }
+            B.c_ctr[p] = rng.ctr;
+          }
+        }
+      }
+    }
+    wave_count(&A.ctr->vm_queries, query);
+    {
+      const unsigned long long fs = wave_sum(found), ms = wave_sum(merged);
+      if (lane_id() == 0 && fs) {
+        atomicAdd(&A.ctr->vm_found, fs);
+        atomicAdd(&A.ctr->vm_merged, ms);
+      }
+    }
+    const int ni = wave_append(&A.sc->sq[slot + 1], nee);
+    if (nee) {  // resolved like a connection: value added when unoccluded
+      st3(Q.o, cap, ni, hp);
+      st3(Q.d, cap, ni, nee_d);
+      st3(Q.tgt, cap, ni, nee_tgt);
+      st3(Q.val, cap, ni, nee_val);
+      Q.meta[ni] = (SQ_CONN << 30) | p;
+      Q.pix[ni] = pix;
+    }
+    // vertex connections to the paired light path (:224-262)
+    if (__ballot(conn_phase && nv > 0)) {
+      for (int k = 0; __ballot(conn_phase && k < nv); ++k) {
+        bool shoot = false;
+        V3 sdir{}, stgt{}, sval{};
+        if (conn_phase && k < nv) {
+          const int vs = k * P + p;
+          const int llen = B.v_len[vs];
+          if (llen + 1 + len > A.maxlen) {
+            nv = k;  // break (:242-244)
+          } else if (llen + 1 + len >= X.minlen && B.v_mat[vs] > 0) {  // emitter vertices: BSDF::f is black
+            // connectVertices (:575-636)
+            const V3 lpos = ld3(B.v_pos, kVMax * P, vs);
+            V3 dir = lpos - hp;
+            const float d2 = sqr_len(dir);
+            const float dist = sqrtf(d2);
+            dir = div_guarded(dir, dist);
+            float cos_c = 0.f, cdp, crp;
+            const V3 cf = bsdf_f(b, S.mats, dir, &cos_c, &cdp, &crp);
+            if (!black(cf)) {
+              cdp *= b.cont;
+              crp *= b.cont;
+              Bsdf lb;
+              lb.mat = B.v_mat[vs];
+              lb.fr = frame_from_z(ld3(B.v_n, kVMax * P, vs));
+              lb.wi = ld3(B.v_wi, kVMax * P, vs);
+              lb.pd = B.v_pd[vs];
+              lb.pg = B.v_pg[vs];
+              lb.cont = B.v_cont[vs];
+              float cos_l = 0.f, ldp, lrp;
+              const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
+              if (!black(lf)) {
+                ldp *= lb.cont;
+                lrp *= lb.cont;
+                const float G = cos_l * cos_c / d2;
+                if (!(cmpf(G) < 0)) {
+                  const float cdpa = cdp * fabsf(cos_l) / (dist * dist);  // pdfWtoA (math.cpp:13-16)
+                  const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
+                  const float wl = cdpa * (X.mis_vm + B.v_dvcm[vs] + B.v_dvc[vs] * lrp);
+                  const float wc = ldpa * (X.mis_vm + cdvcm + cdvc * crp);
+                  const float w = 1.f / (wl + 1.f + wc);
+                  const V3 res = mul(cf, lf) * w * G;
+                  if (!black(res)) {
+                    shoot = true;
+                    sdir = normalize(dir);
+                    stgt = hp + dir * dist;
+                    sval = mul(mul(cthr, ld3(B.v_thr, kVMax * P, vs)), res);
+                  }
+                }
+              }
+            }
+          }
+        }
+        const int si = wave_append(&A.sc->sq[slot + 1], shoot);
+        if (shoot) {
+          st3(Q.o, cap, si, hp);
+          st3(Q.d, cap, si, sdir);
+          st3(Q.tgt, cap, si, stgt);
+          st3(Q.val, cap, si, sval);
+          Q.meta[si] = (SQ_CONN << 30) | p;
+          Q.pix[si] = pix;
+        }
+      }
+    }
+    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
+    if (ext) {
+      st3(B.q_o[nxt], P, ei, e_o);
+      st3(B.q_d[nxt], P, ei, e_d);
+      B.q_path[nxt][ei] = p;
+    }
+  }
+}
+
+// One camera-pass step after its traversal: resolve the step's shadow rays
+// (blocks [0, nres)) and shade its camera vertices (the rest).
+__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_camera_step(VcmGroup G_, int slot, int nres,
+                                                                             int shade) {
+  const VcmArgs& X = G_.a[blockIdx.y];
+  if (static_cast<int>(blockIdx.x) < nres) sq_resolve_body(X.a, slot, blockIdx.x, nres);
+  else if (shade) vcm_camera_shade_body(X, slot, blockIdx.x - nres, gridDim.x - nres);
+}

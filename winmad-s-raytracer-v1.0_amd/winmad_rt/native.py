@@ -19,6 +19,7 @@ K_TRACE, K_SHADE, K_RESOLVE, K_GEN, K_OTHER = 0, 1, 2, 3, 4
 # every entry point declared in include/winmad_rt.h
 EXPORTS = ["wr_scene_load", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free", "wr_device_count",
            "wr_create", "wr_destroy", "wr_set_pipelines", "wr_trace_closest", "wr_occluded", "wr_render_bdpt", "wr_render_path",
+           "wr_render_vcm",
            "wr_film_write_ppm", "wr_film_write_image", "wr_last_error", "wr_api_version"]
 
 
@@ -52,10 +53,18 @@ class WrPathParams(C.Structure):
                 ("time_kernels", C.c_int32), ("count_work", C.c_int32)]
 
 
+class WrVcmParams(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("iterations", C.c_int32),
+                ("iter_begin", C.c_int32), ("min_path_length", C.c_int32), ("max_path_length", C.c_int32),
+                ("radius_factor", C.c_float), ("radius_alpha", C.c_float), ("seed", C.c_uint32),
+                ("time_kernels", C.c_int32), ("count_work", C.c_int32)]
+
+
 class WrStats(C.Structure):
     _fields_ = [("closest_rays", C.c_int64), ("shadow_rays", C.c_int64), ("inner_visits", C.c_int64),
                 ("leaf_visits", C.c_int64), ("prim_refs", C.c_int64), ("seconds", C.c_double),
-                ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8), ("trace_wall_ms", C.c_double)]
+                ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8), ("trace_wall_ms", C.c_double),
+                ("vm_queries", C.c_int64), ("vm_found", C.c_int64), ("vm_merged", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
@@ -109,6 +118,7 @@ def lib():
         L.wr_occluded.argtypes = [P, C.POINTER(WrRay), C.POINTER(C.c_float), I64, C.POINTER(C.c_uint8)]
         L.wr_render_bdpt.argtypes = [P, C.POINTER(WrBdptParams), P, I, C.POINTER(WrStats)]
         L.wr_render_path.argtypes = [P, C.POINTER(WrPathParams), P, I, C.POINTER(WrStats)]
+        L.wr_render_vcm.argtypes = [P, C.POINTER(WrVcmParams), P, I, C.POINTER(WrStats)]
         L.wr_film_write_ppm.argtypes = [C.POINTER(C.c_float), I, I, C.c_float, C.c_float, I, C.c_char_p]
         L.wr_film_write_image.argtypes = [C.POINTER(C.c_float), I, I, C.c_float, C.c_float, I, C.c_char_p]
         L.wr_last_error.restype = C.c_char_p
@@ -215,6 +225,21 @@ class Context:
         if film is None:
             film = np.zeros((height, width, 3), np.float32)
         check(lib().wr_render_bdpt(self.h, C.byref(p), film.ctypes.data_as(C.c_void_p), 0, C.byref(st)))
+        return film, st
+
+    def render_vcm(self, width, height, iterations=1, seed=5489, iter_begin=0, min_path_length=0,
+                   max_path_length=10, radius_factor=0.003, radius_alpha=0.75, time_kernels=0, count_work=0,
+                   film=None, film_ptr=None):
+        """VertexCM::render (vertex connection and merging).  Film as render_bdpt."""
+        p = WrVcmParams(width, height, iterations, iter_begin, min_path_length, max_path_length, radius_factor,
+                        radius_alpha, seed, time_kernels, count_work)
+        st = WrStats()
+        if film_ptr is not None:
+            check(lib().wr_render_vcm(self.h, C.byref(p), C.c_void_p(film_ptr), 1, C.byref(st)))
+            return None, st
+        if film is None:
+            film = np.zeros((height, width, 3), np.float32)
+        check(lib().wr_render_vcm(self.h, C.byref(p), film.ctypes.data_as(C.c_void_p), 0, C.byref(st)))
         return film, st
 
     def render_path(self, width, height, spp, max_depth=7, seed=5489, sample_begin=0, sample_count=0,
