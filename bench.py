@@ -13,7 +13,9 @@ wall time, in Mrays/s.
 
 --config picks the SURVEY.md 8(d) configuration: c2 (default; the BASELINE.json
 metric), c3 (cbox + dragon PT, one step = one sample index of a 512-spp
-stratified render), c4 (the 1M-triangle synthetic torus, BDPT).
+stratified render), c4 (the 1M-triangle synthetic torus, BDPT), vcm (torus.scene
+with VertexCM, SURVEY 8(f) item 4: one step = one VCM iteration, merge radius
+0.003 x sceneRadius shrinking with the global iteration index).
 
 Extra JSON keys: spp_per_sec, roofline (dominant kernel = KD traversal, HIP
 events on the context stream), cpu_baseline (the oracle's C port, MT-serial,
@@ -74,12 +76,14 @@ def cpu_baseline(kind, scene_path, W, H, budget, chunks=16):
         t0 = time.perf_counter()
         if kind == "bdpt":
             _, st = s.bdpt(W, H, 1, 5489 + c, mode=0, path_range=(b, b + per))
+        elif kind == "vcm":
+            _, st = s.vcm(W, H, 1, 5489 + c, mode=0, path_range=(b, b + per))
         else:
             _, st = s.pt(W, H, 1, 7, 5489 + c, mode=0, pix_range=(b, b + per))
         dt += time.perf_counter() - t0
         rays += st.closest_rays + st.shadow_rays
     n = per * chunks
-    what = "camera+light path pairs of one iteration" if kind == "bdpt" else "pixels at 1 spp"
+    what = "pixels at 1 spp" if kind == "pt" else "camera+light path pairs of one iteration"
     return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
             "sample": f"oracle/cpuref.c MT-serial {kind.upper()}, {os.path.basename(scene_path)} {W}x{H}, "
                       f"{n} {what} in {chunks} evenly spaced runs ({rays} rays, {dt:.1f} s CPU); "
@@ -91,13 +95,14 @@ CONFIGS = {
     "c2": {"desc": "torus.scene BDPT", "integrator": "bdpt"},
     "c3": {"desc": "cbox + dragon PT, 512 spp stratification, MAX_TRACING_DEPTH 7", "integrator": "pt"},
     "c4": {"desc": "1M-triangle synthetic torus BDPT", "integrator": "bdpt"},
+    "vcm": {"desc": "torus.scene VertexCM", "integrator": "vcm"},
 }
 METRIC = "Mrays/sec + spp/sec at 1920x1080, torus.scene BDPT, 1/2/4/8 MI355X"
 
 
 def make_scene(cfg, W, H, tmp):
     from winmad_rt import scenes
-    if cfg == "c2":
+    if cfg in ("c2", "vcm"):
         return scenes.write(os.path.join(tmp, "torus.scene"), scenes.torus_scene(W, H))
     if cfg == "c3":
         return scenes.write(os.path.join(tmp, "cbox.scene"), scenes.cbox_scene(W, H))
@@ -114,7 +119,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
-                    help="c2 (default, the BASELINE metric), c3 PT, c4 1M triangles")
+                    help="c2 (default, the BASELINE metric), c3 PT, c4 1M triangles, vcm VertexCM")
     ap.add_argument("--spp", type=int, default=512, help="c3: stratification grid of the PT render")
     ap.add_argument("--cpu-paths", type=int, default=1000000)
     ap.add_argument("--no-cpu", action="store_true")
@@ -149,6 +154,8 @@ def main():
         if pt:
             return ctx.render_path(W, H, spp=args.spp, max_depth=7, seed=5489, sample_begin=begin,
                                    sample_count=count, **kw)
+        if cfg["integrator"] == "vcm":
+            return ctx.render_vcm(W, H, iterations=count, seed=5489, iter_begin=begin, **kw)
         return ctx.render_bdpt(W, H, iterations=count, seed=5489, iter_begin=begin, **kw)
 
     if pt and (world * K > args.spp or args.warmup > args.spp):
@@ -207,7 +214,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        budget = {"c2": args.cpu_paths, "c3": args.cpu_paths // 4, "c4": args.cpu_paths // 20}[args.config]
+        budget = {"c2": args.cpu_paths, "c3": args.cpu_paths // 4, "c4": args.cpu_paths // 20,
+                  "vcm": args.cpu_paths // 2}[args.config]
         cpu = cpu_baseline(cfg["integrator"], scene_path, W, H, budget)
 
     if rank == 0:
@@ -222,7 +230,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: reference scene assets, counter RNG, faithful ray set",
             "config": {"workload": f"{cfg['desc']} {W}x{H}, {K} {unit_name} per GPU"
-                                   + ("" if pt else ", controlLength 3, maxPathLength 10"),
+                                   + ("" if pt else ", maxPathLength 10" if cfg["integrator"] == "vcm"
+                                      else ", controlLength 3, maxPathLength 10"),
                        "scene_config": args.config.upper(), "width": W, "height": H,
                        "steps_per_gpu": K, "parallelism": f"sample-batch x{world}",
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
@@ -230,6 +239,9 @@ def main():
             "rays_per_step": round(total_rays / (K * world)),
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if cfg["integrator"] == "vcm":
+            out["merges_per_step"] = round(st.vm_merged / K)
+            out["merge_queries_per_step"] = round(st.vm_queries / K)
         if cpu:
             out["speedup_vs_cpu_port"] = round(value / cpu["value"], 1)
         print(json.dumps(out))

@@ -2112,10 +2112,18 @@ static void vcm_iteration(vcm_ctx* c, mt_state* mt, int mode, uint32_t seed, int
                  * this loop, in path order (pinned against refdrv, which matches it
                  * bit for bit).  isDelta is then computed from those, and a
                  * non-delta emitter vertex is stored and merged (vertexcm.h:77-78
-                 * reads its continueProb).  Iteration start: a zeroed slot. */
+                 * reads its continueProb).  On a path's first vertex that is the
+                 * last BSDF of an EARLIER light path: pinned on the tent-luminaire
+                 * fixtures (~500 such vertices per iteration).  Iteration start: a
+                 * zeroed slot.  The reference reads uninitialized memory here
+                 * (undefined behaviour): one refdrv build differs from this model by
+                 * 1 ulp in 232 film values of tent64 x3 iterations (seed 7, radius
+                 * factor 0.1), while the same objects relinked with an extra call
+                 * before render() -- or called per iteration -- match it bit for bit. */
                 b.pd = stale.pd; b.pg = stale.pg; b.pr = stale.pr; b.pt = stale.pt;
                 b.cont = stale.cont; b.fres = stale.fres;
                 b.delta = (cmpf(b.pd) == 0 && cmpf(b.pg) == 0);
+                if (ls.len == 1 && c->st) c->st->vm_emitter_first++;
             }
             stale = b;
             /* `pathLength > 1 || isFiniteLight == 1` (:94-95): isFiniteLight is a signed

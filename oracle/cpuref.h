@@ -37,6 +37,8 @@ typedef struct {
     int64_t vm_queries;    /* VCM: KdTree::searchInRadius calls (camera vertices) */
     int64_t vm_found;      /* VCM: light vertices within the radius               */
     int64_t vm_merged;     /* VCM: RangeQuery::process merges (mergeNum)           */
+    int64_t vm_emitter_first; /* VCM: light paths whose first vertex is an emitter
+                                 (BSDF probabilities of the previous light path)      */
 } cr_stats;
 
 /* Load a .scene (scene.cpp:259-467) and build the KD tree (scene.cpp:469-489).

@@ -19,7 +19,8 @@ class Stats(C.Structure):
                 ("inner_visits", C.c_int64), ("leaf_visits", C.c_int64),
                 ("prim_refs", C.c_int64), ("tri_tests", C.c_int64),
                 ("sph_tests", C.c_int64), ("seconds", C.c_double),
-                ("vm_queries", C.c_int64), ("vm_found", C.c_int64), ("vm_merged", C.c_int64)]
+                ("vm_queries", C.c_int64), ("vm_found", C.c_int64), ("vm_merged", C.c_int64),
+                ("vm_emitter_first", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -24,3 +24,7 @@ def cbox(W, H, mode="pt"):
 
 def spheres(W, H, mode="bdpt"):
     return path(f"spheres_{W}x{H}_{mode}.scene", scenes.spheres_scene(W, H, mode))
+
+
+def tent(W, H, mode="bdpt"):
+    return path(f"tent_{W}x{H}_{mode}.scene", scenes.tent_scene(W, H, mode))

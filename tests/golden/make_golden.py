@@ -27,7 +27,7 @@ REFDRV = os.path.join(REPO, "oracle", "_ref", "refdrv")
 
 # (scene, iterations, seed, radius factor or None = the reference's 0.003)
 VCM_CASES = [("torus64", 1, 5489, None), ("torus64", 3, 3, 0.05), ("spheres64", 2, 11, 0.1),
-             ("cboxb64x48", 3, 3, 0.05)]
+             ("cboxb64x48", 3, 3, 0.05), ("tent64", 2, 3, 0.05), ("tent64", 4, 5, 0.05)]
 
 
 def vcm_fixture(name, it, seed, rf):
@@ -146,6 +146,10 @@ def main():
     # cbox in the BDPT orientation (raster x = film row) has emitter light vertices
     sp = scenes.write(os.path.join(tmp, "cboxb64x48.scene"), scenes.cbox_scene(64, 48, "bdpt"))
     pp = scenes.write(os.path.join(tmp, "cboxb64x48.para"), scenes.params_text(64, 48))
+    # tent luminaire: light paths whose first vertex is another emitter (their
+    # BSDF probabilities come from the previous light path's last BSDF)
+    sp = scenes.write(os.path.join(tmp, "tent64.scene"), scenes.tent_scene(64, 64))
+    pp = scenes.write(os.path.join(tmp, "tent64.para"), scenes.params_text(64, 64))
     for name, it, seed, rf in VCM_CASES:
         sp, pp = os.path.join(tmp, name + ".scene"), os.path.join(tmp, name + ".para")
         extra = [] if rf is None else [rf]

@@ -230,11 +230,11 @@ def test_pipeline_count_does_not_change_the_render(pipes):
         c.set_pipelines(0)
 
 
-@pytest.mark.parametrize("mode,W,H", [("-bpt", 64, 64), ("-p", 64, 48)])
+@pytest.mark.parametrize("mode,W,H", [("-bpt", 64, 64), ("-vcm", 64, 64), ("-p", 64, 48)])
 def test_cli_renders_like_the_reference_main(mode, W, H, tmp_path):
     """wr_tot (the C++ mirror of main.cpp's -bpt / -p branches) end to end on the GPU."""
     import subprocess
-    scene = _scenes.torus(W, H) if mode == "-bpt" else _scenes.cbox(W, H)
+    scene = _scenes.torus(W, H) if mode in ("-bpt", "-vcm") else _scenes.cbox(W, H)
     para = tmp_path / "p.para"  # parameters.para: depth, spp, light / hemisphere samples, W, H, phong, lights
     para.write_text(f"#\n7\n#\n4\n8\n4\n{W}\n{H}\n5\n400\n")
     out = tmp_path / "o.ppm"

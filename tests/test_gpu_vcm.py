@@ -39,6 +39,7 @@ def _check(film, st, ref, rst, rel=1e-2):
     ("spheres64", lambda: _scenes.spheres(64, 64), 64, 64, 2, 11, 0.1),   # glass / mirror: delta vertices
     ("cboxb64x48", lambda: _scenes.cbox(64, 48, "bdpt"), 64, 48, 3, 3, 0.05),
     ("torus96x64", lambda: _scenes.torus(96, 64), 96, 64, 2, 7, 0.02),    # non-square film[x][y]
+    ("tent64", lambda: _scenes.tent(64, 64), 64, 64, 2, 3, 0.05),          # emitter-first light vertices
 ])
 def test_vcm_matches_oracle_counter_rng(name, maker, W, H, it, seed, rf):
     path = maker()

@@ -207,11 +207,13 @@ def test_spheres_bdpt_and_pt_films_mt_serial_bit_exact():
 
 VCM_SCENES = {"torus64": (lambda: _scenes.torus(64, 64), 64, 64),
               "spheres64": (lambda: _scenes.spheres(64, 64), 64, 64),
-              "cboxb64x48": (lambda: _scenes.cbox(64, 48, "bdpt"), 64, 48)}
+              "cboxb64x48": (lambda: _scenes.cbox(64, 48, "bdpt"), 64, 48),
+              "tent64": (lambda: _scenes.tent(64, 64), 64, 64)}
 
 
 @pytest.mark.parametrize("name,it,seed,rf", [("torus64", 1, 5489, None), ("torus64", 3, 3, 0.05),
-                                             ("spheres64", 2, 11, 0.1), ("cboxb64x48", 3, 3, 0.05)])
+                                             ("spheres64", 2, 11, 0.1), ("cboxb64x48", 3, 3, 0.05),
+                                             ("tent64", 2, 3, 0.05), ("tent64", 4, 5, 0.05)])
 def test_vcm_film_mt_serial_bit_exact(name, it, seed, rf):
     """VertexCM::runIteration (vertexcm.cpp:47-285): light pass with light
     tracing, the point KD tree (KDtree.h:88-175), camera pass with NEE, vertex
@@ -225,6 +227,8 @@ def test_vcm_film_mt_serial_bit_exact(name, it, seed, rf):
     ref = np.fromfile(os.path.join(GOLD, fx), np.float32).reshape(H, W, 3)
     assert np.array_equal(film.view(np.uint32), ref.view(np.uint32))
     assert st.vm_queries > 0 and st.vm_merged > 0 and st.vm_found >= st.vm_merged
+    if name == "tent64":  # the cross-path stale-BSDF case is exercised (~500 per iteration)
+        assert st.vm_emitter_first > 100 * it
 
 
 def test_vcm_kdtree_search_is_the_brute_force_set():

@@ -64,6 +64,32 @@ void BidirPathTracing::outputImage(const char* filename) {
   ok(wr_film_write_image(film.data(), height, width, 1.f / iterations, 2.2f, height == width, filename));
 }
 
+void VertexCM::init(const char* filename, Parameters& para) {
+  samplesPerPixel = para.SAMPLES_PER_PIXEL;  // stored, unused (:9)
+  height = para.HEIGHT;
+  width = para.WIDTH;
+  load(filename);
+}
+
+void VertexCM::render() {
+  wr_vcm_params p{};
+  p.width = width;
+  p.height = height;
+  p.iterations = iterations;
+  p.iter_begin = 0;
+  p.min_path_length = minPathLength;
+  p.max_path_length = maxPathLength;
+  p.radius_factor = baseRadiusFactor;
+  p.radius_alpha = radiusAlpha;
+  p.seed = seed;
+  ok(wr_render_vcm(ctx_, &p, film.data(), 0, &stats));
+}
+
+void VertexCM::outputImage(const char* filename) {
+  // transpose (square films only, :31-42), scale 1/iterations, gamma 2.2 (:44)
+  ok(wr_film_write_image(film.data(), height, width, 1.f / iterations, 2.2f, height == width, filename));
+}
+
 void PathIntegrator::init(const char* filename, Parameters& para) {
   maxTracingDepth = para.MAX_TRACING_DEPTH;
   samplesPerPixel = para.SAMPLES_PER_PIXEL;

@@ -52,6 +52,19 @@ class BidirPathTracing : public SurfaceIntegrator {
   void outputImage(const char* filename) override;               // :29-46
 };
 
+// src/surfaceIntegrator/vertexcm.{h,cpp}
+class VertexCM : public SurfaceIntegrator {
+ public:
+  int minPathLength = 0, maxPathLength = 10;
+  int iterations = 1;            // vertexcm.cpp:7
+  float baseRadiusFactor = 0.003f;  // baseRadius = 0.003 * sceneRadius (:13)
+  float radiusAlpha = 0.75f;     // :14
+  uint32_t seed = 5489;
+  void init(const char* filename, Parameters& para) override;  // :3-21
+  void render() override;                                        // :23-27
+  void outputImage(const char* filename) override;               // :29-45
+};
+
 // src/surfaceIntegrator/pathIntegrator.{h,cpp} + SurfaceIntegrator::render
 class PathIntegrator : public SurfaceIntegrator {
  public:

@@ -1,6 +1,6 @@
 // wr_tot -- command-line twin of the reference's main() (src/main.cpp:29-97) for
 // the two GPU integrators:
-//     wr_tot <scene> <out.ppm> -bpt|-p [--params FILE] [--iterations N] [--seed S] [--device D]
+//     wr_tot <scene> <out.ppm> -bpt|-vcm|-p [--params FILE] [--iterations N] [--seed S] [--device D]
 // Parameters come from src/parameters.para relative to the CWD, as in the
 // reference (main.cpp:32), unless --params is given.  Writes time.txt like
 // main.cpp:93-95 (seconds instead of clock ticks).
@@ -15,7 +15,7 @@
 
 int main(int argc, char** argv) {
   if (argc < 4) {
-    std::fprintf(stderr, "usage: %s <scene> <out.ppm> -bpt|-p [--params F] [--iterations N] [--seed S] [--device D]\n",
+    std::fprintf(stderr, "usage: %s <scene> <out.ppm> -bpt|-vcm|-p [--params F] [--iterations N] [--seed S] [--device D]\n",
                  argv[0]);
     return 2;
   }
@@ -38,6 +38,11 @@ int main(int argc, char** argv) {
       b->iterations = iterations;
       b->seed = seed;
       integ.reset(b);
+    } else if (!std::strcmp(argv[3], "-vcm")) {  // main.cpp:53-58
+      auto* v = new winmad::VertexCM();
+      v->iterations = iterations;
+      v->seed = seed;
+      integ.reset(v);
     } else if (!std::strcmp(argv[3], "-p")) {
       auto* p = new winmad::PathIntegrator();
       p->seed = seed;

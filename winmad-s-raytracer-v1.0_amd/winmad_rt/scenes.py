@@ -137,6 +137,32 @@ def spheres_scene(width, height, mode="bdpt", assets=ASSETS):
     return out
 
 
+def tent_scene(width, height, mode="bdpt", assets=ASSETS):
+    """Cornell-box walls under a tent-shaped luminaire (assets/tent_luminaire.obj,
+    four emitting faces turned inward): light subpaths can start on one slope
+    and hit another emitter first -- the VCM light vertex that inherits the
+    previous light path's BSDF probabilities (vertexcm.cpp:90-113, bsdf.h:78-83)."""
+    xres, yres = (width, height) if mode == "pt" else (height, width)
+    a = lambda f: os.path.join(assets, f)
+    out = "<scene>\n"
+    out += _camera(("-0.0439815", "-4.12529", "0.222539"),
+                   ("0.00688625", "0.998505", "-0.0542161"),
+                   ("3.73896e-4", "0.0542148", "0.998529"), xres, yres, "45")
+    out += _mat()
+    out += _mat(d=("0.803922", "0.803922", "0.803922"), e=1)
+    out += _mat(d=("0.156863", "0.803922", "0.172549"), e=1)
+    out += _mat(d=("0.803922", "0.152941", "0.152941"), e=1)
+    out += _mat(s=("1", "1", "1"), n="1.5")
+    for f in ("cbox_floor.obj", "cbox_back.obj", "cbox_ceiling.obj"):
+        out += _obj(a(f), 1)
+    out += _obj(a("cbox_greenwall.obj"), 2)
+    out += _obj(a("cbox_redwall.obj"), 3)
+    out += _sphere(("0.1", "0.2", "-0.8"), "0.35", 4)
+    out += _area(a("tent_luminaire.obj"), "12")
+    out += "</scene>\n"
+    return out
+
+
 def synth_torus_obj(path, U=1000, V=500, R=150.0, r=45.0, center=(17.0, 102.0, -15.0)):
     """The C4/C5 synthetic torus: U x V quad grid in the xy-plane, each quad
     (a b c d) written as `f a b c` / `f a c d` => 2*U*V = 1,000,000 triangles."""
