@@ -84,6 +84,7 @@ struct StepCounters {
   int fetch[kSlots];  // persistent-traversal cursor of the step's trace launch
   int vcm_pending;    // VCM: light paths whose first vertex is an emitter (k_vcm_fixup)
   int vcm_nverts;     // VCM: light vertices in the merge grid
+  int mq[kSlots];     // VCM: merge queries queued at step `slot`
 };
 struct DevCounters {
   int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
@@ -1104,6 +1105,7 @@ struct wr_context {
   int grid = 2048;
   int cus = 256;
   float sph_r = 0.f;  // sceneSphere.sceneRadius (scene.cpp:483-487): VCM base radius
+  float vcm_cell = 1.f;  // VCM merge-grid cell edge in query half-widths (WR_VCM_CELL); measured 2 -> 1: +4 %
   bool spheres = false;
   bool narrow = false;  // <= 65536 nodes, leaves <= 255 refs: 16-bit stack / pair offsets
   bool trace_log = false;  // WR_TRACE_LOG=1: per-launch ray counts and durations
@@ -1208,7 +1210,7 @@ void layout_pt(Arena& a, PtBuf& T, int P) {
 // VCM merge grid: 2^k buckets, at least twice the paths (light vertices
 // average ~0.5-1 per path in the reference scenes)
 uint32_t vcm_table(int P) {
-  uint32_t t = 1024;
+  uint32_t t = kRowW;
   while (t < 2u * static_cast<uint32_t>(P)) t <<= 1;
   return t;
 }
@@ -1231,7 +1233,24 @@ void layout_vcm(Arena& a, VcmBuf& V, int P) {
   V.pending = a.take<int>(sP);
   V.cnt = a.take<int>(size_t(T) + 1);
   V.start = a.take<int>(size_t(T) + 1);
-  V.rec = a.take<float4>(4 * sV);
+  V.rpos = a.take<float4>(sV);
+  V.rdat = a.take<float4>(2 * sV);
+  V.rdvm = a.take<float>(sV);
+  for (int k = 0; k < 2; ++k) {
+    VcmBuf::Mq& M = V.mq[k];
+    M.hp = a.take<float>(3 * sP);
+    M.n = a.take<float>(3 * sP);
+    M.wi = a.take<float>(3 * sP);
+    M.thr = a.take<float>(3 * sP);
+    M.dvcm = a.take<float>(sP);
+    M.dvm = a.take<float>(sP);
+    M.cont = a.take<float>(sP);
+    M.pd = a.take<float>(sP);
+    M.pg = a.take<float>(sP);
+    M.mat = a.take<int>(sP);
+    M.len = a.take<int>(sP);
+    M.pix = a.take<int>(sP);
+  }
   V.scan_bytes = vcm_scan_bytes(T);
   V.scan_tmp = a.take<char>(V.scan_bytes);
 }
@@ -1716,6 +1735,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   for (const auto& p : s.prims) c->spheres |= p.type != wr::kTri;
   if (const char* e = std::getenv("WR_TRACE_STAMPS")) c->stamps = std::atoi(e) != 0 && !c->spheres;
   if (const char* e = std::getenv("WR_TRACE_LOG")) c->trace_log = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WR_VCM_CELL")) c->vcm_cell = std::min(8.f, std::max(0.25f, (float)std::atof(e)));
   {
     // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
     // and registers); more would only queue behind the first wave of blocks
@@ -2011,7 +2031,13 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
       X.mis_vm = eta;
       X.mis_vc = 1.f / eta;
       X.rq = radius * 1.0009765625f;
-      X.inv_cs = 1.f / (2.f * X.rq * 1.0009765625f);
+      // the first float s with sqrtf(s) >= radius: sqrtf is correctly rounded
+      // and monotone on host and device, so `sqrtf(s) < radius` == `s < r2t`
+      float t = r2;
+      while (t > 0.f && std::sqrt(t) >= radius) t = std::nextafter(t, 0.f);
+      while (!(std::sqrt(t) >= radius)) t = std::nextafter(t, INFINITY);
+      X.r2t = t;
+      X.inv_cs = 1.f / (c->vcm_cell * X.rq);
     }
     auto sq = [&](int m, int slot) {
       const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
@@ -2060,6 +2086,10 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
       hipLaunchKernelGGL(k_vcm_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot,
                          nres, more ? 1 : 0);
       tm.mark(WR_K_SHADE);
+      if (more) {
+        hipLaunchKernelGGL(k_vcm_merge, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, slot);
+        tm.mark(WR_K_RESOLVE);
+      }
     }
   }
   HIPCHK(hipGetLastError());

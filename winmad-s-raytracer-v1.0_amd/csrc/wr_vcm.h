@@ -12,12 +12,13 @@
 // searchInRadius with exactly the vertices v for which
 // sqrtf(|x - v|^2) < radius (its pruning test |x[axis] - split| < radius is
 // exact in float; tests/test_oracle.py checks this).  The GPU finds the same
-// set in a hash grid of cell size >= 2 * radius: the query visits every cell
-// overlapping [x - r', x + r'] per axis with r' = r (1 + 2^-10), which holds
-// every vertex the float test can accept (|fl(x - v)| <= fl-distance < r, and
-// float subtraction, scaling and floor are monotone), then applies the
-// reference's test.  Only the summation order of the merged contributions
-// differs.
+// set in a hashed grid (cells of any size, WR_VCM_CELL x r'): the query visits
+// every cell overlapping [x - r', x + r'] per axis with r' = r (1 + 2^-10),
+// which holds every vertex the float test can accept (|fl(x - v)| <=
+// fl-distance < r, and float subtraction, scaling and floor are monotone),
+// applies the reference's test, and takes a vertex only in its own cell (a
+// bucket may hold several cells).  Only the summation order of the merged
+// contributions differs.
 
 struct VcmBuf {
   float *l_dvm, *c_dvm;  // dVM of the light / camera subpath state (vertexcm.h:36)
@@ -29,7 +30,17 @@ struct VcmBuf {
   int* pending;    // light paths whose first vertex is an emitter
   int* cnt;        // [T + 1] vertices per grid bucket, then 0 after the scatter
   int* start;      // [T + 1] exclusive scan of cnt
-  float4* rec;     // [kVMax * P][4] merge records, bucket-sorted
+  // merge records, bucket-sorted: the range scan reads only rpos
+  float4* rpos;    // [kVMax * P] {pos, pathLength}
+  float4* rdat;    // [kVMax * P][2] {wiWorld, continueProb}, {throughput, dVCM}
+  float* rdvm;     // [kVMax * P] dVM
+  // merge queries of a camera-pass step (k_vcm_merge), [2][field][P]: the
+  // camera vertex's position, BSDF (normal, wiLocal, probabilities, matId) and
+  // subpath state
+  struct Mq {
+    float *hp, *n, *wi, *thr, *dvcm, *dvm, *cont, *pd, *pg;
+    int *mat, *len, *pix;
+  } mq[2];
   void* scan_tmp;  // hipcub scan scratch
   size_t scan_bytes;
 };
@@ -42,6 +53,7 @@ struct VcmArgs {
   float radius, vm_norm, mis_vm, mis_vc;  // (:53-64)
   V3 org;                                // grid origin (root box corner)
   float inv_cs, rq;                      // 1 / cell size, query half-width r (1 + 2^-10)
+  float r2t;                             // sqrtf(s) < radius  <=>  s < r2t (exact, host-derived)
   uint32_t tmask;                        // T - 1
 };
 struct VcmGroup {
@@ -52,14 +64,16 @@ __device__ __forceinline__ int vcm_cell(float x, float org, float inv_cs) {
   const float c = floorf((x - org) * inv_cs);
   return static_cast<int>(clampv(c, -1073741824.f, 1073741824.f));
 }
-__device__ __forceinline__ uint32_t vcm_hash(int x, int y, int z, uint32_t mask) {
-  return ((static_cast<uint32_t>(x) * 73856093u) ^ (static_cast<uint32_t>(y) * 19349663u) ^
-          (static_cast<uint32_t>(z) * 83492791u)) &
-         mask;
+// Buckets: a grid row (cy, cz) is hashed to a run of kRowW buckets, one per
+// cx (mod kRowW), so the cells [x0, x1] of a row are one contiguous bucket
+// range (two where cx wraps): a query reads one range per row.
+constexpr int kRowBits = 10, kRowW = 1 << kRowBits;
+__device__ __forceinline__ uint32_t vcm_row(int y, int z, uint32_t tmask) {
+  return (((static_cast<uint32_t>(y) * 19349663u) ^ (static_cast<uint32_t>(z) * 83492791u)) << kRowBits) & tmask;
 }
 __device__ __forceinline__ uint32_t vcm_bucket(const VcmArgs& X, V3 p) {
-  return vcm_hash(vcm_cell(p.x, X.org.x, X.inv_cs), vcm_cell(p.y, X.org.y, X.inv_cs),
-                  vcm_cell(p.z, X.org.z, X.inv_cs), X.tmask);
+  return vcm_row(vcm_cell(p.y, X.org.y, X.inv_cs), vcm_cell(p.z, X.org.z, X.inv_cs), X.tmask) |
+         (static_cast<uint32_t>(vcm_cell(p.x, X.org.x, X.inv_cs)) & (kRowW - 1));
 }
 
 // generateLightSample (:287-330) + the first extension ray
@@ -352,11 +366,10 @@ __global__ void __launch_bounds__(kShadeBlock) k_vgrid_scatter(VcmGroup G_) {
       const Frame fr = frame_from_z(ld3(B.v_n, kVMax * P, vs));
       const V3 ldir = to_world(fr, ld3(B.v_wi, kVMax * P, vs));  // BSDF::wiWorld (bsdf.h:101-104)
       const V3 thr = ld3(B.v_thr, kVMax * P, vs);
-      float4* r = V.rec + 4 * static_cast<size_t>(idx);
-      r[0] = make_float4(pos.x, pos.y, pos.z, __int_as_float(B.v_len[vs]));
-      r[1] = make_float4(ldir.x, ldir.y, ldir.z, B.v_cont[vs]);
-      r[2] = make_float4(thr.x, thr.y, thr.z, B.v_dvcm[vs]);
-      r[3] = make_float4(V.v_dvm[vs], 0.f, 0.f, 0.f);
+      V.rpos[idx] = make_float4(pos.x, pos.y, pos.z, __int_as_float(B.v_len[vs]));
+      V.rdat[2 * static_cast<size_t>(idx)] = make_float4(ldir.x, ldir.y, ldir.z, B.v_cont[vs]);
+      V.rdat[2 * static_cast<size_t>(idx) + 1] = make_float4(thr.x, thr.y, thr.z, B.v_dvcm[vs]);
+      V.rdvm[idx] = V.v_dvm[vs];
     }
   }
 }
@@ -365,34 +378,51 @@ __global__ void __launch_bounds__(kShadeBlock) k_vgrid_scatter(VcmGroup G_) {
 // + RangeQuery::process (vertexcm.h:59-96).  Returns the contribution sum.
 __device__ __forceinline__ V3 vcm_merge(const VcmArgs& X, const Bsdf& b, V3 hp, int len, float cdvcm, float cdvm,
                                         unsigned& found, unsigned& merged) {
+  // (the reference skips the search when there are no light vertices at all)
   const VcmBuf& V = X.V;
   V3 acc = v3(0.f, 0.f, 0.f);
   const int x0 = vcm_cell(hp.x - X.rq, X.org.x, X.inv_cs), x1 = vcm_cell(hp.x + X.rq, X.org.x, X.inv_cs);
   const int y0 = vcm_cell(hp.y - X.rq, X.org.y, X.inv_cs), y1 = vcm_cell(hp.y + X.rq, X.org.y, X.inv_cs);
   const int z0 = vcm_cell(hp.z - X.rq, X.org.z, X.inv_cs), z1 = vcm_cell(hp.z + X.rq, X.org.z, X.inv_cs);
-  const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, ncell = nx * ny * (z1 - z0 + 1);
-  for (int c = 0; c < ncell; ++c) {
-    const int cx = x0 + c % nx, cy = y0 + (c / nx) % ny, cz = z0 + c / (nx * ny);
-    const uint32_t h = vcm_hash(cx, cy, cz, X.tmask);
-    bool dup = false;  // two cells of this query in one bucket: visit it once
-    for (int e = 0; e < c && !dup; ++e)
-      dup = vcm_hash(x0 + e % nx, y0 + (e / nx) % ny, z0 + e / (nx * ny), X.tmask) == h;
-    if (dup) continue;
-    const int i1 = V.start[h + 1];
-    for (int i = V.start[h]; i < i1; ++i) {
-      const float4 r0 = V.rec[4 * static_cast<size_t>(i)];
+  const int ny = y1 - y0 + 1, nrow = ny * (z1 - z0 + 1);
+  const bool whole = x1 - x0 >= kRowW - 1;
+  const uint32_t a = static_cast<uint32_t>(x0) & (kRowW - 1), bx = static_cast<uint32_t>(x1) & (kRowW - 1);
+  for (int k = 0; k < 2 * nrow; ++k) {  // row k / 2, part k % 2 (the wrapped tail of a row)
+    const int cy = y0 + (k >> 1) % ny, cz = z0 + (k >> 1) / ny;
+    const uint32_t row = vcm_row(cy, cz, X.tmask);
+    uint32_t lo, hi;
+    if (whole) {
+      if (k & 1) continue;
+      lo = row;
+      hi = row | (kRowW - 1);
+    } else if (a <= bx) {
+      if (k & 1) continue;
+      lo = row | a;
+      hi = row | bx;
+    } else {
+      lo = (k & 1) ? row : (row | a);
+      hi = (k & 1) ? (row | bx) : (row | (kRowW - 1));
+    }
+    const int i1 = V.start[hi + 1];
+    for (int i = V.start[lo]; i < i1; ++i) {
+      const float4 r0 = V.rpos[i];
       const V3 dd = hp - v3(r0.x, r0.y, r0.z);
-      if (!(sqrtf(sqr_len(dd)) < X.radius)) continue;
+      if (!(sqr_len(dd) < X.r2t)) continue;  // == sqrtf(|dd|^2) < radius (KDtree.h:171-173)
+      // buckets are shared (hashed rows, cx mod kRowW): take the vertex only
+      // from its own row and within this query's x cells
+      const int vx = vcm_cell(r0.x, X.org.x, X.inv_cs);
+      if (vcm_cell(r0.y, X.org.y, X.inv_cs) != cy || vcm_cell(r0.z, X.org.z, X.inv_cs) != cz || vx < x0 || vx > x1)
+        continue;
       ++found;
       const int llen = __float_as_int(r0.w);
       if (llen + len > X.a.maxlen || llen + len < X.minlen) continue;
-      const float4 r1 = V.rec[4 * static_cast<size_t>(i) + 1];
+      const float4 r1 = V.rdat[2 * static_cast<size_t>(i)];
       float cos_c = 0.f, dp, rp;
       const V3 f = bsdf_f(b, X.a.S.mats, v3(r1.x, r1.y, r1.z), &cos_c, &dp, &rp);
       if (black(f)) continue;
       ++merged;
-      const float4 r2 = V.rec[4 * static_cast<size_t>(i) + 2];
-      const float ldvm = V.rec[4 * static_cast<size_t>(i) + 3].x;
+      const float4 r2 = V.rdat[2 * static_cast<size_t>(i) + 1];
+      const float ldvm = V.rdvm[i];
       dp *= b.cont;
       rp *= r1.w;
       const float wl = r2.w * X.mis_vc + ldvm * dp;
@@ -434,9 +464,8 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
   for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
     bool ext = false, conn_phase = false, nee = false, query = false;
     int p = -1, pix = -1, nv = 0, len = 0;
-    unsigned found = 0, merged = 0;
-    V3 hp{}, thr{}, cthr{}, e_o{}, e_d{}, nee_tgt{}, nee_d{}, nee_val{};
-    float dvcm = 0.f, dvc = 0.f, dvm = 0.f, cdvcm = 0.f, cdvc = 0.f;
+    V3 hp{}, hn{}, thr{}, cthr{}, e_o{}, e_d{}, nee_tgt{}, nee_d{}, nee_val{};
+    float dvcm = 0.f, dvc = 0.f, dvm = 0.f, cdvcm = 0.f, cdvc = 0.f, cdvm = 0.f;
     Bsdf b;
     b.mat = 0;
     if (j < n) {
@@ -449,6 +478,7 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
         bsdf_init(b, -d, h.n, h.mat, S.mats);
         if (b.mat != 0) {
           hp = h.p;
+          hn = h.n;
           pix = B.c_pix[p];
           dvcm = B.c_dvcm[p];
           dvc = B.c_dvc[p];
@@ -507,11 +537,8 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
             if (!b.delta) {
               conn_phase = true;
               nv = B.v_count[p];
-              if (any_verts) {  // vertex merging (:265-276)
-                query = true;
-                const V3 acc = vcm_merge(X, b, hp, len, dvcm, dvm, found, merged);
-                film_add(A.film, pix, mul(thr, acc) * X.vm_norm);
-              }
+              query = any_verts;  // vertex merging (:265-276): queued for k_vcm_merge
+              cdvm = dvm;
             }
             V3 so = ld3(B.c_o, P, p), sd = ld3(B.c_d, P, p);
             if (vcm_scatter(X, rng, b, hp, so, sd, thr, dvcm, dvc, dvm)) {
@@ -532,12 +559,21 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
       }
     }
     wave_count(&A.ctr->vm_queries, query);
-    {
-      const unsigned long long fs = wave_sum(found), ms = wave_sum(merged);
-      if (lane_id() == 0 && fs) {
-        atomicAdd(&A.ctr->vm_found, fs);
-        atomicAdd(&A.ctr->vm_merged, ms);
-      }
+    const int mi = wave_append(&A.sc->mq[slot], query);
+    if (query) {
+      const VcmBuf::Mq& M = V.mq[slot & 1];
+      st3(M.hp, P, mi, hp);
+      st3(M.n, P, mi, hn);
+      st3(M.wi, P, mi, b.wi);
+      st3(M.thr, P, mi, cthr);
+      M.dvcm[mi] = cdvcm;
+      M.dvm[mi] = cdvm;
+      M.cont[mi] = b.cont;
+      M.pd[mi] = b.pd;
+      M.pg[mi] = b.pg;
+      M.mat[mi] = b.mat;
+      M.len[mi] = len;
+      M.pix[mi] = pix;
     }
     const int ni = wave_append(&A.sc->sq[slot + 1], nee);
     if (nee) {  // resolved like a connection: value added when unoccluded
@@ -617,6 +653,36 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
       st3(B.q_o[nxt], P, ei, e_o);
       st3(B.q_d[nxt], P, ei, e_d);
       B.q_path[nxt][ei] = p;
+    }
+  }
+}
+
+// Vertex merging of one camera-pass step's queued vertices (:265-276): one
+// lane per query, outside the vertex kernel so that its long, divergent range
+// scans run at the occupancy of a small kernel.
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_vcm_merge(VcmGroup G_, int slot) {
+  const VcmArgs& X = G_.a[blockIdx.y];
+  const VcmBuf::Mq& M = X.V.mq[slot & 1];
+  const int n = X.a.sc->mq[slot], P = X.a.P;
+  const int gstride = gridDim.x * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    unsigned found = 0, merged = 0;
+    if (j < n) {
+      Bsdf b;
+      b.mat = M.mat[j];
+      b.fr = frame_from_z(ld3(M.n, P, j));
+      b.wi = ld3(M.wi, P, j);
+      b.pd = M.pd[j];
+      b.pg = M.pg[j];
+      b.cont = M.cont[j];
+      const V3 acc = vcm_merge(X, b, ld3(M.hp, P, j), M.len[j], M.dvcm[j], M.dvm[j], found, merged);
+      film_add(X.a.film, M.pix[j], mul(ld3(M.thr, P, j), acc) * X.vm_norm);
+    }
+    const unsigned long long fs = wave_sum(found), ms = wave_sum(merged);
+    if (lane_id() == 0 && fs) {
+      atomicAdd(&X.a.ctr->vm_found, fs);
+      atomicAdd(&X.a.ctr->vm_merged, ms);
     }
   }
 }
