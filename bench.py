@@ -18,8 +18,10 @@ with VertexCM, SURVEY 8(f) item 4: one step = one VCM iteration, merge radius
 0.003 x sceneRadius shrinking with the global iteration index).
 
 Extra JSON keys: spp_per_sec, roofline (dominant kernel = KD traversal, HIP
-events on the context stream), cpu_baseline (the oracle's C port, MT-serial,
-single thread, bounded sample of the same frame).
+events on the context stream), cpu_baseline (the reference itself, built from
+its sources by oracle/Makefile, one thread, the same scene at reduced
+resolution), cpu_port (the oracle's C port, MT-serial, one thread, a bounded
+sample of the full frame).
 """
 import argparse
 import json
@@ -90,6 +92,54 @@ def cpu_baseline(kind, scene_path, W, H, budget, chunks=16):
                       f"spp/s={n / dt:.0f}"}
 
 
+REFDRV = os.path.join(REPO, "oracle", "_ref", "refdrv")
+
+
+def cpu_reference(cfg_name, kind, W, H, tmp, shrink):
+    """The reference ITSELF on the host: oracle/_ref/refdrv is the reference's own
+    translation units compiled by oracle/Makefile (test infrastructure).  It
+    renders whole frames only, so the bounded sample is the same scene at
+    (W/shrink) x (H/shrink), one iteration / one sample per pixel, one thread;
+    time = its render() wall time (refdrv prints it, scene load and KD build
+    excluded).  The reference counts no rays: the count of that exact run comes
+    from the oracle's MT-serial replica, whose film must equal the reference's
+    bit for bit (checked, reported as film_bit_exact)."""
+    import subprocess
+    import numpy as np
+    from winmad_rt import scenes
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle
+    if not os.path.exists(REFDRV):
+        return None
+    w, h = max(8, W // shrink), max(8, H // shrink)
+    d = os.path.join(tmp, "ref")
+    os.makedirs(d, exist_ok=True)
+    scene = make_scene(cfg_name, w, h, d, obj=os.path.join(tmp, "torus_1m.obj"))
+    para = scenes.write(os.path.join(d, "ref.para"), scenes.params_text(w, h, 7, 1))
+    out = os.path.join(d, "ref.f32")
+    args = {"bdpt": ["bdpt", scene, para, 1, 5489, out], "vcm": ["vcm", scene, para, 1, 5489, out],
+            "pt": ["pt", scene, para, 5489, out]}[kind]
+    r = subprocess.run([REFDRV, *map(str, args)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, REFDRV_CWD=d))
+    if r.returncode != 0:
+        return None
+    sec = float(next(l for l in r.stdout.splitlines() if l.startswith("render_seconds")).split()[1])
+    s = _oracle.Scene(scene)
+    if kind == "bdpt":
+        film, st = s.bdpt(w, h, 1, 5489, mode=0)
+    elif kind == "vcm":
+        film, st = s.vcm(w, h, 1, 5489, mode=0)
+    else:
+        film, st = s.pt(w, h, 1, 7, 5489, mode=0)
+    ref = np.fromfile(out, np.float32).reshape(h, w, 3)
+    rays = st.closest_rays + st.shadow_rays
+    return {"value": round(rays / sec / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "reference",
+            "sample": f"oracle/_ref/refdrv {kind} (the reference's own code, g++ -O3), {os.path.basename(scene)} "
+                      f"{w}x{h}, 1 {'spp' if kind == 'pt' else 'iteration'}, {rays} rays in {sec:.2f} s; "
+                      f"spp/s={w * h / sec:.0f}",
+            "film_bit_exact": bool(np.array_equal(film.view(np.uint32), ref.view(np.uint32)))}
+
+
 # SURVEY.md 8(d) configurations a bench line can be quoted on
 CONFIGS = {
     "c2": {"desc": "torus.scene BDPT", "integrator": "bdpt"},
@@ -100,14 +150,15 @@ CONFIGS = {
 METRIC = "Mrays/sec + spp/sec at 1920x1080, torus.scene BDPT, 1/2/4/8 MI355X"
 
 
-def make_scene(cfg, W, H, tmp):
+def make_scene(cfg, W, H, tmp, obj=None):
     from winmad_rt import scenes
     if cfg in ("c2", "vcm"):
         return scenes.write(os.path.join(tmp, "torus.scene"), scenes.torus_scene(W, H))
     if cfg == "c3":
         return scenes.write(os.path.join(tmp, "cbox.scene"), scenes.cbox_scene(W, H))
-    obj = os.path.join(tmp, "torus_1m.obj")
-    scenes.synth_torus_obj(obj)
+    obj = obj or os.path.join(tmp, "torus_1m.obj")
+    if not os.path.exists(obj):
+        scenes.synth_torus_obj(obj)
     return scenes.write(os.path.join(tmp, "torus_1m.scene"), scenes.torus_scene(W, H, torus_obj=obj))
 
 
@@ -212,11 +263,14 @@ def main():
                     # (traffic << algorithmic bytes): the L2 peak is the tighter ceiling
                     "l2_peak": L2_PEAK_GBS, "l2_frac": round(achieved / L2_PEAK_GBS, 4)}
 
-    cpu = None
+    cpu = port = None
     if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_reference(args.config, cfg["integrator"], W, H, tmp, 8 if args.config == "c4" else 4)
         budget = {"c2": args.cpu_paths, "c3": args.cpu_paths // 4, "c4": args.cpu_paths // 20,
                   "vcm": args.cpu_paths // 2}[args.config]
-        cpu = cpu_baseline(cfg["integrator"], scene_path, W, H, budget)
+        port = cpu_baseline(cfg["integrator"], scene_path, W, H, budget)
+        if cpu is None:  # no reference build on this machine: the port is the baseline
+            cpu, port = port, None
 
     if rank == 0:
         value = total_rays / elapsed / 1e6
@@ -243,7 +297,10 @@ def main():
             out["merges_per_step"] = round(st.vm_merged / K)
             out["merge_queries_per_step"] = round(st.vm_queries / K)
         if cpu:
-            out["speedup_vs_cpu_port"] = round(value / cpu["value"], 1)
+            out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        if port:
+            out["cpu_port"] = port
+            out["speedup_vs_cpu_port"] = round(value / port["value"], 1)
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
