@@ -265,7 +265,7 @@ def main():
 
     cpu = port = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_reference(args.config, cfg["integrator"], W, H, tmp, 8 if args.config == "c4" else 4)
+        cpu = cpu_reference(args.config, cfg["integrator"], W, H, tmp, 4 if args.config == "c4" else 2)
         budget = {"c2": args.cpu_paths, "c3": args.cpu_paths // 4, "c4": args.cpu_paths // 20,
                   "vcm": args.cpu_paths // 2}[args.config]
         port = cpu_baseline(cfg["integrator"], scene_path, W, H, budget)
