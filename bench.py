@@ -55,10 +55,11 @@ def pmc_traffic():
         return None, None
 
 
-def algorithmic_bytes(rays, inner, leaves, refs):
+def algorithmic_bytes(rays, inner, leaves, refs, tests):
     """B_ray = 32 (ray) + 16 (hit) + 8 x (inner + leaf visits)
-    + 4 x (primitive refs read) + 40 x (triangles tested)."""
-    return 48.0 * rays + 8.0 * (inner + leaves) + 4.0 * refs + 40.0 * refs
+    + 4 x (primitive refs read) + 40 x (triangles tested).  Tests = the ones
+    the kernel runs (repeats of a (ray, primitive) pair are skipped)."""
+    return 48.0 * rays + 8.0 * (inner + leaves) + 4.0 * refs + 40.0 * tests
 
 
 def cpu_baseline(kind, scene_path, W, H, budget, chunks=16):
@@ -239,7 +240,7 @@ def main():
         # the counter RNG makes the work a pure function of (seed, iteration, path))
         _, cst = render(it0, K, count_work=1, film=None)
         assert cst.closest_rays == st.closest_rays and cst.shadow_rays == st.shadow_rays
-        total_bytes = algorithmic_bytes(rays, cst.inner_visits, cst.leaf_visits, cst.prim_refs)
+        total_bytes = algorithmic_bytes(rays, cst.inner_visits, cst.leaf_visits, cst.prim_refs, cst.prim_tests)
         per_launch = total_bytes / max(1, trace_launches)
         # launches of the concurrent pipelines overlap: the rate is the bytes over
         # the union of the traversal launch intervals (HIP events on each stream);
@@ -256,7 +257,8 @@ def main():
                     "trace_wall_ms": round(st.trace_wall_ms, 3),
                     "wall_ms_per_launch": round(st.trace_wall_ms / max(1, trace_launches), 4),
                     "launches": int(trace_launches),
-                    "tests_per_ray": round(cst.prim_refs / rays, 2),
+                    "refs_per_ray": round(cst.prim_refs / rays, 2),
+                    "tests_per_ray": round(cst.prim_tests / rays, 2),
                     "nodes_per_ray": round((cst.inner_visits + cst.leaf_visits) / rays, 2),
                     "trace_share_of_wall": round(st.trace_wall_ms / 1e3 / max(1e-9, elapsed), 3),
                     # a scene that fits L2 / Infinity Cache is read from there, not HBM

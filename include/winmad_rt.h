@@ -125,6 +125,8 @@ typedef struct {
   int64_t vm_queries;        /* VCM: range queries (KdTree::searchInRadius calls)  */
   int64_t vm_found;          /* VCM: light vertices found within the radius       */
   int64_t vm_merged;         /* VCM: RangeQuery::process merges (non-black BSDF)   */
+  int64_t prim_tests;        /* count_work only: primitive tests run; < prim_refs
+                                by the (ray, primitive) repeats skipped            */
 } wr_stats;
 
 /* ---- scene (Scene::init, scene/scene.cpp:469-489 + loadScene :259-467) ---- */

@@ -89,7 +89,7 @@ struct StepCounters {
 struct DevCounters {
   int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
   unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
-  unsigned long long closest, shadow, inner, leaves, refs;
+  unsigned long long closest, shadow, inner, leaves, refs, tests;
   unsigned long long vm_queries, vm_found, vm_merged;  // VCM range queries / vertices in radius / merges
 };
 
@@ -141,14 +141,16 @@ template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
 // 4 waves/SIMD (<= 128 VGPRs) to match the LDS-limited 16 waves/CU
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32 k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
   extern __shared__ uint32_t smem[];
-  TraceCounters tc{0, 0, 0};
+  TraceCounters tc{0, 0, 0, 0};
   trace_queue<COUNT, SPH, NARROW, STAMP>(S, Q, fetch, smem, tc, ctr->stamps);
   if (COUNT) {
-    unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs);
+    unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs),
+                       e = wave_sum(tc.tests);
     if (lane_id() == 0) {
       atomicAdd(&ctr->inner, a);
       atomicAdd(&ctr->leaves, b);
       atomicAdd(&ctr->refs, c);
+      atomicAdd(&ctr->tests, e);
     }
   }
 }
@@ -1423,6 +1425,7 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
     sum.inner += h.inner;
     sum.leaves += h.leaves;
     sum.refs += h.refs;
+    sum.tests += h.tests;
     sum.vm_queries += h.vm_queries;
     sum.vm_found += h.vm_found;
     sum.vm_merged += h.vm_merged;
@@ -1433,6 +1436,7 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
   st->inner_visits += static_cast<int64_t>(sum.inner);
   st->leaf_visits += static_cast<int64_t>(sum.leaves);
   st->prim_refs += static_cast<int64_t>(sum.refs);
+  st->prim_tests += static_cast<int64_t>(sum.tests);
   st->vm_queries += static_cast<int64_t>(sum.vm_queries);
   st->vm_found += static_cast<int64_t>(sum.vm_found);
   st->vm_merged += static_cast<int64_t>(sum.vm_merged);

@@ -48,7 +48,7 @@ struct DevScene {
 };
 
 struct TraceCounters {  // algorithmic work, for the roofline's byte count
-  uint32_t inner, leaves, refs;
+  uint32_t inner, leaves, refs, tests;
 };
 
 // AABB::hit (AABB.cpp:9-32)
@@ -213,10 +213,28 @@ constexpr int kLeavesPerRound = WR_LEAVES_PER_ROUND;
 #endif
 constexpr int kRayGrab = WR_RAY_GRAB;  // queue indices a wave reserves per atomic (>= 64)  // leaves a lane may collect per round
 constexpr int kLeavesWait = WR_LEAVES_WAIT;           // the walk runs until every lane has this many
+// Per-ray mailbox of recently tested primitives (direct-mapped by prim id):
+// a (ray, primitive) pair tested before -- the KD build duplicates straddling
+// triangles into every leaf they touch (torus: 2.88 refs per triangle) -- is
+// skipped.  A repeat cannot change the result: it yields the same t, and the
+// earlier test either set best <= t or was rejected against a best that has
+// only decreased since, so `cmp(t - best) < 0` fails again.  Measured on torus
+// BDPT rays: 60 % of the reference's tests are repeats; an 8-entry mailbox
+// catches 40 % of all tests (C4: 3,248 -> 819 tests per ray).  It is OFF (0):
+// the filter pass (primitive load + mailbox per slot, then compaction) costs
+// about what the skipped tests save -- the pair phase is bound by its
+// dependent L2 round trips, not by the triangle arithmetic -- and the extra LDS
+// lowers occupancy.  Measured (Mrays/s, 8 pipelines): C2 871 -> 702 (m8),
+// C4 36.3 -> 34.5 (m8); scripts/build_variant.sh m8 -DWR_MAILBOX=8.
+#ifndef WR_MAILBOX
+#define WR_MAILBOX 0
+#endif
+constexpr int kMail = WR_MAILBOX;
+static_assert((kMail & (kMail - 1)) == 0, "mailbox size: power of two");
 __host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
   return size_t(depth) * 64 * (narrow ? 6 : 8) +
          size_t(4) * (8 * 64 + 64 + kLeavesPerRound * 64 + kLeavesPerRound * (narrow ? 32 : 64) + kPairBatch / 4 +
-                      4 * 64 + 16);
+                      4 * 64 + 16 + kMail * 64 + (kMail > 0 ? kPairBatch / 2 : 0));
 }
 
 // Persistent closest-hit traversal over the ray queues of one launch (one wave
@@ -312,6 +330,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
   unsigned long long* olo = reinterpret_cast<unsigned long long*>(own + kPairBatch);  // [64] key << 32 | prim
   unsigned long long* ohi = olo + 64;  // [64] (INT_MAX - key) << 32 | prim
   uint8_t* onear = reinterpret_cast<uint8_t*>(ohi + 64);  // [64]
+  int* mail = reinterpret_cast<int*>(onear + 64);  // [64][kMail] prim keys tested per ray (0: empty)
+  uint16_t* cslot = reinterpret_cast<uint16_t*>(mail + 64 * kMail);  // [kPairBatch] kept slots of the batch
   int qend[kMaxQueues];  // queue i holds launch indices [qend[i-1], qend[i])
   {
     int acc = 0;
@@ -433,6 +453,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
             inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
             ray4[2 * lane] = make_float4(o.x, o.y, o.z, d.x);
             ray4[2 * lane + 1] = make_float4(d.y, d.z, rtmin, rtmax);
+#pragma unroll
+            for (int k = 0; k < kMail; ++k) mail[lane * kMail + k] = 0;
           }
         }
         if (__ballot(idle && idx >= n)) pool = false;
@@ -554,21 +576,57 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
       }
       __syncthreads();
       WR_STAMP(2)
-      // kPairsInFlight pairs per lane per trip: j, j + 64, ... of the batch; all
-      // their records are requested before the first test.  A lane keeps the t
-      // of its own pairs (slot (j - lane) / 64) in registers.
+      // Mailbox filter: each slot of the batch (j = lane + 64 k, in slot order,
+      // i.e. leaf order per ray) reads its primitive and checks the ray's
+      // mailbox; the pairs to test are compacted into cslot[0, nk).  The first
+      // slot of a (ray, primitive) to be checked is kept and marks the
+      // mailbox; later ones -- this batch or later -- are dropped.
+      int nk = lim;
+      if constexpr (kMail > 0) {
+        nk = 0;
+        uint32_t fref[kPairBatch / 64];
+        int fown[kPairBatch / 64];
+        float fprim[kPairBatch / 64];
+#pragma unroll
+        for (int k = 0; k < kPairBatch / 64; ++k) {
+          const int j = min(lane + 64 * k, lim - 1);
+          const int id = own[j];
+          fown[k] = id / kLeavesPerRound;
+          fref[k] = leaf_first[id] + static_cast<uint32_t>(base + j - static_cast<int>(leaf_off[id]));
+        }
+#pragma unroll
+        for (int k = 0; k < kPairBatch / 64; ++k) fprim[k] = (lane + 64 * k < lim) ? S.ref_c[fref[k]].y : 0.f;
+#pragma unroll
+        for (int k = 0; k < kPairBatch / 64; ++k) {
+          bool keep = false;
+          if (lane + 64 * k < lim) {
+            const int key = __float_as_int(fprim[k]) ^ static_cast<int>(0x80000000u);  // != 0 (empty)
+            int* slot = mail + fown[k] * kMail + (key & (kMail - 1));
+            keep = *slot != key;
+            if (keep) *slot = key;
+          }
+          const unsigned long long m = __ballot(keep);
+          if (keep) cslot[nk + __popcll(m & ((1ull << lane) - 1ull))] = static_cast<uint16_t>(lane + 64 * k);
+          nk += __popcll(m);
+        }
+        __syncthreads();
+      }
+      // kPairsInFlight pairs per lane per trip: c, c + 64, ... of the kept
+      // slots; all their records are requested before the first test.  A lane
+      // keeps the t of its own pairs ((c - lane) / 64) in registers.
       float tv[kPairBatch / 64];
 #pragma unroll
       for (int k = 0; k < kPairBatch / 64; ++k) tv[k] = __int_as_float(0x7fc00000);  // NaN: no hit
 #pragma unroll
       for (int tr = 0; tr < kPairBatch / (64 * kPairsInFlight); ++tr) {
-        const int j0 = lane + 64 * kPairsInFlight * tr;
-        if (j0 >= lim) break;
+        const int c0 = lane + 64 * kPairsInFlight * tr;
+        if (64 * kPairsInFlight * tr >= nk) break;  // wave-uniform
         uint32_t ref[kPairsInFlight];
         int owner[kPairsInFlight];
 #pragma unroll
         for (int u = 0; u < kPairsInFlight; ++u) {
-          const int j = min(j0 + 64 * u, lim - 1);
+          const int c = min(c0 + 64 * u, max(nk - 1, 0));
+          const int j = kMail > 0 ? static_cast<int>(cslot[c]) : c;
           const int id = own[j];
           owner[u] = id / kLeavesPerRound;
           ref[u] = leaf_first[id] + static_cast<uint32_t>(base + j - static_cast<int>(leaf_off[id]));
@@ -583,7 +641,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
         }
 #pragma unroll
         for (int u = 0; u < kPairsInFlight; ++u) {
-          if (j0 + 64 * u >= lim) break;
+          if (c0 + 64 * u >= nk) break;
+          if (COUNT) ++ctr.tests;
           const int L = owner[u];
           const float4 x = ray4[2 * L], y = ray4[2 * L + 1];
           const int prim = __float_as_int(rc[u].y);
@@ -601,10 +660,10 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
       // flag owners with a hit in (min, min + 2 EPS]
 #pragma unroll
       for (int k = 0; k < kPairBatch / 64; ++k) {
-        const int j = lane + 64 * k;
+        const int c = lane + 64 * k;
         const float t = tv[k];
-        if (j < lim && t == t) {
-          const int L = own[j] / kLeavesPerRound;
+        if (c < nk && t == t) {
+          const int L = own[kMail > 0 ? static_cast<int>(cslot[c]) : c] / kLeavesPerRound;
           const float m = __int_as_float(static_cast<int>(olo[L] >> 32));
           if (t != m && t - m <= 2.f * WR_EPS) onear[L] = 1;
         }

@@ -64,7 +64,8 @@ class WrStats(C.Structure):
     _fields_ = [("closest_rays", C.c_int64), ("shadow_rays", C.c_int64), ("inner_visits", C.c_int64),
                 ("leaf_visits", C.c_int64), ("prim_refs", C.c_int64), ("seconds", C.c_double),
                 ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8), ("trace_wall_ms", C.c_double),
-                ("vm_queries", C.c_int64), ("vm_found", C.c_int64), ("vm_merged", C.c_int64)]
+                ("vm_queries", C.c_int64), ("vm_found", C.c_int64), ("vm_merged", C.c_int64),
+                ("prim_tests", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
