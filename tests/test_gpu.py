@@ -156,6 +156,21 @@ def test_bdpt_1080p_properties_and_sharding():
     assert 3.5 < rpp < 4.8, rpp
 
 
+def test_bdpt_1080p_matches_oracle_counter_rng():
+    """BASELINE.json's own frame (torus.scene 1920x1080, C2), one iteration:
+    the GPU film against the oracle's counter-RNG film -- the same gates as the
+    small films (the oracle needs ~5-15 s of one CPU core here)."""
+    W, H = 1920, 1080
+    path = _scenes.torus(W, H)
+    film, st = ctx(path).render_bdpt(W, H, iterations=1, seed=5489)
+    ref, rst = _oracle.Scene(path).bdpt(W, H, 1, 5489, mode=1)
+    rmse, rms, ch = film_err(film, ref)
+    assert rmse / rms < 1e-2, (rmse, rms)
+    assert np.all(ch < 1e-3), ch
+    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+    assert abs(st.shadow_rays - rst.shadow_rays) <= 0.005 * rst.shadow_rays
+
+
 def test_film_on_device_pointer():
     torch = pytest.importorskip("torch")
     path = _scenes.torus(64, 64)

@@ -59,6 +59,17 @@ def test_vcm_path_length_window():
     _check(film, st, ref, rst)
 
 
+def test_vcm_1080p_matches_oracle_counter_rng():
+    """torus.scene at 1920x1080 with the reference's own merge radius, one
+    iteration, against the oracle (counter RNG)."""
+    W, H = 1920, 1080
+    path = _scenes.torus(W, H)
+    film, st = ctx(path).render_vcm(W, H, iterations=1, seed=5489)
+    ref, rst = _oracle.Scene(path).vcm(W, H, 1, 5489, mode=1)
+    assert rst.vm_merged > 1000000
+    _check(film, st, ref, rst)
+
+
 def test_vcm_iteration_sharding_is_additive_at_1080p():
     """Full C2 frame: iterations [0, 2) == [0, 1) + [1, 2) (each iteration has
     its own radius, keyed by the global index), identical ray and merge counts."""
