@@ -30,10 +30,10 @@ import sys
 import tempfile
 import time
 
-# At least 8 hardware queues for this process (HIP's default, and the GPU
-# box's environment, is 4) so that the library runs 8 concurrent render
+# At least 16 hardware queues for this process (HIP's default, and the GPU
+# box's environment, is 4) so that the library runs 16 concurrent render
 # pipelines; must be set before HIP initialises.  DESIGN.md section 4.
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)))
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(16, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)))
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "winmad-s-raytracer-v1.0_amd"))

@@ -144,7 +144,7 @@ void wr_destroy(wr_context* ctx);
  * ~5 GB per pair of iterations at 1080p): iterations / samples are dealt
  * round-robin to them so that one stream's late-bounce traversal tail overlaps
  * another's full launches.  1..16; default = the process's hardware queues
- * (GPU_MAX_HW_QUEUES, HIP default 4) up to 8, or env WR_PIPES.
+ * (GPU_MAX_HW_QUEUES, HIP default 4) up to 16, or env WR_PIPES.
  * GPU-specific scheduling; no reference counterpart. */
 int wr_set_pipelines(wr_context* ctx, int n);
 

@@ -1588,12 +1588,12 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     }
   }
   // one pipeline per hardware queue of this process (HIP's GPU_MAX_HW_QUEUES,
-  // default 4; pipeline 0 shares the context stream), at most 8: streams that
+  // default 4; pipeline 0 shares the context stream), at most 16: streams that
   // share a hardware queue serialize behind each other
   {
     const char* q = std::getenv("GPU_MAX_HW_QUEUES");
     const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
-    c->npipes = std::max(1, std::min(8, hwq));
+    c->npipes = std::max(1, std::min(kMaxPipes, hwq));
   }
   if (const char* e = std::getenv("WR_PIPES")) c->npipes = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   hipDeviceProp_t prop;
