@@ -5,11 +5,14 @@
 # Usage: scripts/profile_round.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r1}; shift
-ARGS=${@:---steps 4 --warmup 1 --no-cpu --no-count}
+# trace pass: the default bench command itself (so that rocprof's average
+# k_trace duration is comparable with the line's roofline.avg_launch_ms: with
+# 16 overlapping pipelines a launch's duration depends on the run's length)
+ARGS=${@:-}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace pass failed rc=$?"; tail -5 $OUT/trace.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace pass failed rc=$?"; tail -5 $OUT/trace.log; exit 1; }
 echo "trace pass ok"
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
