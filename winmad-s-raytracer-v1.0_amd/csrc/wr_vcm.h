@@ -660,7 +660,11 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
 // Vertex merging of one camera-pass step's queued vertices (:265-276): one
 // lane per query, outside the vertex kernel so that its long, divergent range
 // scans run at the occupancy of a small kernel.
-__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_vcm_merge(VcmGroup G_, int slot) {
+#ifndef WR_MERGE_WAVES
+#define WR_MERGE_WAVES 6
+#endif
+__global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WR_MERGE_WAVES, 8))) WR_NO_PK_FP32
+k_vcm_merge(VcmGroup G_, int slot) {
   const VcmArgs& X = G_.a[blockIdx.y];
   const VcmBuf::Mq& M = X.V.mq[slot & 1];
   const int n = X.a.sc->mq[slot], P = X.a.P;
