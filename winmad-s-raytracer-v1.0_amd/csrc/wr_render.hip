@@ -1271,7 +1271,9 @@ void layout_set(Arena& a, Pipe* dst, int g, int kind, int P) {
 }
 
 int ensure_work(Pipe& p, int kind, int P, int sets) {
-  if (p.work_kind == kind && p.work_key == static_cast<size_t>(P) && p.work_sets >= sets) return WR_OK;
+  // a VCM layout starts with the complete BDPT layout, so it serves BDPT too
+  const bool same = p.work_kind == kind || (kind == 1 && p.work_kind == 3);
+  if (same && p.work_key == static_cast<size_t>(P) && p.work_sets >= sets) return WR_OK;
   p.work_kind = 0;
   auto lay = [&](Arena& a, Pipe* dst) {
     for (int g = 0; g < sets; ++g) layout_set(a, dst, g, kind, P);
