@@ -1625,6 +1625,30 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     }
     nrec[i] = make_uint4(self.x, self.y, l.x, l.y);
   }
+  // three-level records (WR_NODE_LEVELS = 3): self, children, grandchildren
+  std::vector<uint4> nrec3(4 * nn, make_uint4(0u, 0u, 0u, 0u));
+  {
+    auto word = [&](int64_t i) { return i >= 0 ? nodes[static_cast<size_t>(i)] : make_uint2(0u, 0u); };
+    auto kids = [&](int64_t i, int64_t& l, int64_t& r) {
+      l = r = -1;
+      if (i >= 0 && s.nodes[static_cast<size_t>(i)].axis >= 0) {
+        l = i + 1;
+        r = s.nodes[static_cast<size_t>(i)].right;
+      }
+    };
+    for (size_t i = 0; i < nn; ++i) {
+      int64_t L, R, LL, LR, RL, RR;
+      kids(static_cast<int64_t>(i), L, R);
+      kids(L, LL, LR);
+      kids(R, RL, RR);
+      const uint2 w0 = word(static_cast<int64_t>(i)), wl = word(L), wr = word(R), wll = word(LL), wlr = word(LR),
+                  wrl = word(RL), wrr = word(RR);
+      nrec3[4 * i] = make_uint4(w0.x, w0.y, wl.x, wl.y);
+      nrec3[4 * i + 1] = make_uint4(wr.x, wr.y, wll.x, wll.y);
+      nrec3[4 * i + 2] = make_uint4(wlr.x, wlr.y, wrl.x, wrl.y);
+      nrec3[4 * i + 3] = make_uint4(wrr.x, wrr.y, 0u, 0u);
+    }
+  }
   std::vector<float4> ra(nr), rb(nr);
   std::vector<float2> rcv(nr);
   for (size_t i = 0; i < nr; ++i) {
@@ -1672,7 +1696,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                    v3(m.specular.x, m.specular.y, m.specular.z), m.phong_exp, m.index};
   }
   auto total = measure([&](Arena& a) {
-    a.take<uint4>(nn); a.take<uint2>(nn); a.take<float4>(nr); a.take<float4>(nr); a.take<float2>(nr);
+    a.take<uint4>(nn); a.take<uint2>(nn); a.take<uint4>(4 * nn); a.take<float4>(nr); a.take<float4>(nr);
+    a.take<float2>(nr);
     a.take<int>(np); a.take<int>(np); a.take<float4>(np); a.take<float2>(np); a.take<float4>(np);
     a.take<float4>(np); a.take<float2>(np); a.take<DLight>(lights.size() + 1); a.take<DMat>(mats.size());
     a.take<DevCounters>(1);
@@ -1688,6 +1713,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   DevScene& d = c->ds;
   uint4* dn = A.take<uint4>(nn);
   uint2* dnr = A.take<uint2>(nn);
+  uint4* dn3 = A.take<uint4>(4 * nn);
   float4* dra = A.take<float4>(nr);
   float4* drb = A.take<float4>(nr);
   float2* drc = A.take<float2>(nr);
@@ -1702,7 +1728,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   DMat* dm = A.take<DMat>(mats.size());
   c->ctr = A.take<DevCounters>(1);
   hipError_t e = hipSuccess;
-  for (hipError_t x : {up(dn, nrec), up(dnr, nrec_r), up(dra, ra), up(drb, rb), up(drc, rcv), up(dpm, pmat), up(dpt, ptype),
+  for (hipError_t x : {up(dn, nrec), up(dnr, nrec_r), up(dn3, nrec3), up(dra, ra), up(drb, rb), up(drc, rcv), up(dpm, pmat), up(dpt, ptype),
                        up(dptri, ptri), up(dptri2, ptri2), up(dpsph, psph), up(dpsb0, psb0), up(dpsb1, psb1),
                        up(dm, mats)})
     if (x != hipSuccess) e = x;
@@ -1713,6 +1739,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   }
   d.nrec = dn;
   d.nrec_r = dnr;
+  d.nrec3 = dn3;
   d.ref_a = dra;
   d.ref_b = drb;
   d.ref_c = drc;

@@ -29,6 +29,10 @@ struct DevScene {
   // right << 2 | axis) with left = i + 1; leaf (first ref, count << 2 | 3)
   const uint4* nrec;
   const uint2* nrec_r;
+  // three levels per record (WR_NODE_LEVELS = 3): node i's word, its two
+  // children's and its four grandchildren's, 64 bytes:
+  //   [4i] = (self, L)  [4i+1] = (R, LL)  [4i+2] = (LR, RL)  [4i+3] = (RR, 0)
+  const uint4* nrec3;
   const float4* ref_a;
   const float4* ref_b;
   const float2* ref_c;
@@ -196,6 +200,9 @@ struct TraceQueues {
 #define WR_PAIR_BATCH 256
 #endif
 constexpr int kPairBatch = WR_PAIR_BATCH;  // multiple of 256
+#ifndef WR_NODE_LEVELS
+#define WR_NODE_LEVELS 3  // tree levels resolved per dependent record load (2 or 3); 3: C2 892 -> 911 Mrays/s
+#endif
 static_assert(kPairBatch % 256 == 0, "the owner-table scan covers 4 bytes per lane per 256 slots");
 #ifndef WR_LEAVES_PER_ROUND
 #define WR_LEAVES_PER_ROUND 4
@@ -473,6 +480,29 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
     int nl = 0, count = 0;
     while (__ballot(more && nl < kLeavesWait)) {
       if (more && nl < kLeavesPerRound) {
+#if WR_NODE_LEVELS == 3
+        const uint4* rp = S.nrec3 + 4 * static_cast<size_t>(node);
+        const uint4 q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3];
+        asm volatile("" : : "v"(q0.y), "v"(q1.x), "v"(q2.x), "v"(q3.x));
+        uint2 nd = make_uint2(q0.x, q0.y);
+        bool leaf = (nd.y & 3u) == 3u;
+        if (!leaf) {
+          const uint32_t at = node;
+          node = step(nd, at);
+          const bool lft = node == at + 1;
+          nd = lft ? make_uint2(q0.z, q0.w) : make_uint2(q1.x, q1.y);
+          leaf = (nd.y & 3u) == 3u;
+          if (!leaf) {
+            const uint32_t c = node;
+            node = step(nd, c);
+            const bool l2 = node == c + 1;
+            nd = lft ? (l2 ? make_uint2(q1.z, q1.w) : make_uint2(q2.x, q2.y))
+                     : (l2 ? make_uint2(q2.z, q2.w) : make_uint2(q3.x, q3.y));
+            leaf = (nd.y & 3u) == 3u;
+            if (!leaf) node = step(nd, node);
+          }
+        }
+#else
         const uint4 q = S.nrec[node];
         const uint2 qr = S.nrec_r[node];
         // keep both loads in flight together: otherwise the second is sunk into
@@ -487,6 +517,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
           leaf = (nd.y & 3u) == 3u;
           if (!leaf) node = step(nd, node);
         }
+#endif
         if (leaf) {
           leaf_first[lane * kLeavesPerRound + nl] = nd.x;
           leaf_off[lane * kLeavesPerRound + nl] = static_cast<PairIdx>(count);
