@@ -836,8 +836,13 @@ struct PtBuf {
   uint32_t* ctr;
   float *q_o[2], *q_d[2], *q_t[2];
   int *q_path[2], *q_prim[2];
-  float *s_o, *s_d, *s_tgt, *s_val, *s_t;
-  int *s_pix, *s_prim;
+  // NEE shadow rays, two buffers: those of step `slot` are [slot & 1], so a
+  // step's resolve and the next vertex shading (writing [(slot + 1) & 1]) run
+  // in one launch
+  struct Sq {
+    float *o, *d, *tgt, *val, *t;
+    int *pix, *prim;
+  } sq[2];
 };
 struct PtArgs {
   DevScene S;
@@ -883,17 +888,16 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_gen(PtGroup G_
 }
 
 // One PathIntegrator::raytracing iteration (pathIntegrator.cpp:43-146)
-__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_shade(PtGroup G_, int slot) {
-  const PtArgs& A = G_.a[blockIdx.y];
+__device__ __forceinline__ void pt_shade_body(const PtArgs& A, int slot, int bid, int nblk) {
   const PtBuf& T = A.T;
   const DevScene& S = A.S;
   const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
   const int n = A.sc->ext[slot];
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
-  const int gstride = gridDim.x * blockDim.x;
+  if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
+  const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
   const float lpp = 1.f / static_cast<float>(S.nlights);
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
     bool ext = false, shadow = false;
     int p = -1, pix = -1;
     V3 e_o{}, e_d{}, s_o{}, s_d{}, s_tgt{}, s_val{};
@@ -984,35 +988,47 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_shade(PtGroup 
     }
     const int si = wave_append(&A.sc->sq[slot + 1], shadow);
     if (shadow) {
-      st3(T.s_o, P, si, s_o);
-      st3(T.s_d, P, si, s_d);
-      st3(T.s_tgt, P, si, s_tgt);
-      st3(T.s_val, P, si, s_val);
-      T.s_pix[si] = pix;
+      const PtBuf::Sq& Q = T.sq[(slot + 1) & 1];
+      st3(Q.o, P, si, s_o);
+      st3(Q.d, P, si, s_d);
+      st3(Q.tgt, P, si, s_tgt);
+      st3(Q.val, P, si, s_val);
+      Q.pix[si] = pix;
     }
   }
 }
 
-__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_resolve(PtGroup G_, int slot) {
-  const PtArgs& A = G_.a[blockIdx.y];
+// NEE shadow rays of step `slot` after traversal (pathIntegrator.cpp:95-110):
+// unoccluded => the queued contribution goes to the film
+__device__ __forceinline__ void pt_resolve_body(const PtArgs& A, int slot, int bid, int nblk) {
   const PtBuf& T = A.T;
+  const PtBuf::Sq& Q = T.sq[slot & 1];
   const int n = A.sc->sq[slot], P = A.P;
-  const int gstride = gridDim.x * blockDim.x;
+  const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
     bool is = false;
     if (j < n) {
       is = true;
       bool unocc = true;
-      const int prim = T.s_prim[j];
+      const int prim = Q.prim[j];
       if (prim >= 0) {
-        const V3 o = ld3(T.s_o, P, j), d = ld3(T.s_d, P, j);
-        unocc = near_eq(o + d * T.s_t[j], ld3(T.s_tgt, P, j));
+        const V3 o = ld3(Q.o, P, j), d = ld3(Q.d, P, j);
+        unocc = near_eq(o + d * Q.t[j], ld3(Q.tgt, P, j));
       }
-      if (unocc) film_add(A.film, T.s_pix[j], ld3(T.s_val, P, j));
+      if (unocc) film_add(A.film, Q.pix[j], ld3(Q.val, P, j));
     }
     wave_count(&A.ctr->shadow, is);
   }
+}
+
+// One PT step after its traversal: resolve the step's shadow rays (blocks
+// [0, nres)) and shade its vertices (the rest, `shade` = 0 after the last
+// bounce) -- they read and write different shadow-queue buffers.
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_step(PtGroup G_, int slot, int nres, int shade) {
+  const PtArgs& A = G_.a[blockIdx.y];
+  if (static_cast<int>(blockIdx.x) < nres) pt_resolve_body(A, slot, blockIdx.x, nres);
+  else if (shade) pt_shade_body(A, slot, blockIdx.x - nres, gridDim.x - nres);
 }
 
 __global__ void k_film_accumulate(float* dst, const float* src, int64_t n) {
@@ -1200,13 +1216,16 @@ void layout_pt(Arena& a, PtBuf& T, int P) {
     T.q_path[q] = a.take<int>(sP);
     T.q_prim[q] = a.take<int>(sP);
   }
-  T.s_o = a.take<float>(3 * sP);
-  T.s_d = a.take<float>(3 * sP);
-  T.s_tgt = a.take<float>(3 * sP);
-  T.s_val = a.take<float>(3 * sP);
-  T.s_t = a.take<float>(sP);
-  T.s_pix = a.take<int>(sP);
-  T.s_prim = a.take<int>(sP);
+  for (int k = 0; k < 2; ++k) {
+    PtBuf::Sq& Q = T.sq[k];
+    Q.o = a.take<float>(3 * sP);
+    Q.d = a.take<float>(3 * sP);
+    Q.tgt = a.take<float>(3 * sP);
+    Q.val = a.take<float>(3 * sP);
+    Q.t = a.take<float>(sP);
+    Q.pix = a.take<int>(sP);
+    Q.prim = a.take<int>(sP);
+  }
 }
 
 // VCM merge grid: 2^k buckets, at least twice the paths (light vertices
@@ -2186,7 +2205,8 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
       QueueList ql;
       for (int m = 0; m < gn; ++m) {
         const PtBuf& T = pp.pb[m];
-        ql.add(rq(T.s_o, T.s_d, P, &pp.sc[m].sq[b], T.s_t, T.s_prim), P);
+        const PtBuf::Sq& Q = T.sq[b & 1];
+        ql.add(rq(Q.o, Q.d, P, &pp.sc[m].sq[b], Q.t, Q.prim), P);
       }
       if (more)
         for (int m = 0; m < gn; ++m) {
@@ -2194,11 +2214,12 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
           ql.add(rq(T.q_o[q], T.q_d[q], P, &pp.sc[m].ext[b], T.q_t[q], T.q_prim[q]), P);
         }
       trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays);
-      hipLaunchKernelGGL(k_pt_resolve, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
-      tm.mark(WR_K_RESOLVE);
-      if (!more) break;
-      hipLaunchKernelGGL(k_pt_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
+      // resolve this step's shadow rays and shade its vertices in one launch
+      const int nres = shade_grid(c, P);
+      hipLaunchKernelGGL(k_pt_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, b, nres,
+                         more ? 1 : 0);
       tm.mark(WR_K_SHADE);
+      if (!more) break;
     }
   }
   HIPCHK(hipGetLastError());
