@@ -2135,13 +2135,11 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
       trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays);
       const int nres = shade_grid(c, sq_max);
-      hipLaunchKernelGGL(k_vcm_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot,
-                         nres, more ? 1 : 0);
+      // + the merge queries of the previous step (none before the first)
+      const int nsh = more ? g : 0, nmg = b > 0 ? g : 0;
+      hipLaunchKernelGGL(k_vcm_camera_step, dim3(nres + nsh + nmg, gn), dim3(kShadeBlock), 0, sm, GA, slot, nres,
+                         nsh);
       tm.mark(WR_K_SHADE);
-      if (more) {
-        hipLaunchKernelGGL(k_vcm_merge, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, slot);
-        tm.mark(WR_K_RESOLVE);
-      }
     }
   }
   HIPCHK(hipGetLastError());

@@ -6,7 +6,7 @@
 //   light pass  : gen -> [trace -> shade] x 9                 (:67-140)
 //   fix-up      : emitter-first light vertices (stale BSDF, below)
 //   merge grid  : count -> exclusive scan -> scatter          (replaces :152)
-//   camera pass : gen -> [trace -> resolve + shade] x 11      (:157-283)
+//   camera pass : gen -> [trace -> resolve + shade + merge] x 11 (:157-283)
 //
 // The reference's point KD tree (scene/KDtree.h:88-175) answers
 // searchInRadius with exactly the vertices v for which
@@ -34,7 +34,7 @@ struct VcmBuf {
   float4* rpos;    // [kVMax * P] {pos, pathLength}
   float4* rdat;    // [kVMax * P][2] {wiWorld, continueProb}, {throughput, dVCM}
   float* rdvm;     // [kVMax * P] dVM
-  // merge queries of a camera-pass step (k_vcm_merge), [2][field][P]: the
+  // merge queries of a camera-pass step (vcm_merge_body), [2][field][P]: the
   // camera vertex's position, BSDF (normal, wiLocal, probabilities, matId) and
   // subpath state
   struct Mq {
@@ -537,7 +537,7 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
             if (!b.delta) {
               conn_phase = true;
               nv = B.v_count[p];
-              query = any_verts;  // vertex merging (:265-276): queued for k_vcm_merge
+              query = any_verts;  // vertex merging (:265-276): queued for the next launch
               cdvm = dvm;
             }
             V3 so = ld3(B.c_o, P, p), sd = ld3(B.c_d, P, p);
@@ -660,17 +660,12 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
 // Vertex merging of one camera-pass step's queued vertices (:265-276): one
 // lane per query, outside the vertex kernel so that its long, divergent range
 // scans run at the occupancy of a small kernel.
-#ifndef WR_MERGE_WAVES
-#define WR_MERGE_WAVES 6
-#endif
-__global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WR_MERGE_WAVES, 8))) WR_NO_PK_FP32
-k_vcm_merge(VcmGroup G_, int slot) {
-  const VcmArgs& X = G_.a[blockIdx.y];
+__device__ __forceinline__ void vcm_merge_body(const VcmArgs& X, int slot, int bid, int nblk) {
   const VcmBuf::Mq& M = X.V.mq[slot & 1];
   const int n = X.a.sc->mq[slot], P = X.a.P;
-  const int gstride = gridDim.x * blockDim.x;
+  const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
     unsigned found = 0, merged = 0;
     if (j < n) {
       Bsdf b;
@@ -691,11 +686,16 @@ k_vcm_merge(VcmGroup G_, int slot) {
   }
 }
 
-// One camera-pass step after its traversal: resolve the step's shadow rays
-// (blocks [0, nres)) and shade its camera vertices (the rest).
+// One camera-pass step after its traversal, three disjoint parts in one launch:
+// blocks [0, nres) resolve the step's shadow rays, [nres, nres + nsh) shade its
+// camera vertices (queueing merge queries into mq[slot & 1]), the rest merge
+// the queries the previous step queued (mq[(slot - 1) & 1]; vertex merging
+// only adds to the film, so it need not finish before this step's traversal).
 __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_camera_step(VcmGroup G_, int slot, int nres,
-                                                                             int shade) {
+                                                                             int nsh) {
   const VcmArgs& X = G_.a[blockIdx.y];
-  if (static_cast<int>(blockIdx.x) < nres) sq_resolve_body(X.a, slot, blockIdx.x, nres);
-  else if (shade) vcm_camera_shade_body(X, slot, blockIdx.x - nres, gridDim.x - nres);
+  const int bx = static_cast<int>(blockIdx.x);
+  if (bx < nres) sq_resolve_body(X.a, slot, bx, nres);
+  else if (bx < nres + nsh) vcm_camera_shade_body(X, slot, bx - nres, nsh);
+  else vcm_merge_body(X, slot - 1, bx - nres - nsh, gridDim.x - nres - nsh);
 }
