@@ -49,13 +49,14 @@ def test_vcm_matches_oracle_counter_rng(name, maker, W, H, it, seed, rf):
     _check(film, st, ref, rst)
 
 
-def test_vcm_path_length_window():
+@pytest.mark.parametrize("lo,hi", [(3, 5), (0, 2), (2, 3)])
+def test_vcm_path_length_window(lo, hi):
     """min / max path length (RangeQuery::process :61-63, connection loop
-    :236-244, light pass :129): a narrow window matches the oracle too."""
+    :236-244, light pass :129): narrow windows match the oracle too."""
     path = _scenes.torus(64, 64)
-    film, st = ctx(path).render_vcm(64, 64, iterations=2, seed=5, min_path_length=3, max_path_length=5,
+    film, st = ctx(path).render_vcm(64, 64, iterations=2, seed=5, min_path_length=lo, max_path_length=hi,
                                     radius_factor=0.05)
-    ref, rst = _oracle.Scene(path).vcm(64, 64, 2, 5, mode=1, min_len=3, max_len=5, radius_factor=0.05)
+    ref, rst = _oracle.Scene(path).vcm(64, 64, 2, 5, mode=1, min_len=lo, max_len=hi, radius_factor=0.05)
     _check(film, st, ref, rst)
 
 

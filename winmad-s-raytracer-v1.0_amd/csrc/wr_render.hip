@@ -1,5 +1,7 @@
 // MI355X (gfx950) implementation of the reference's hot path behind the C ABI of
-// include/winmad_rt.h:
+// include/winmad_rt.h (kernels in wr_traverse.h, wr_bdpt.h, wr_vcm.h, wr_pt.h;
+// this file: shared device helpers, the runtime -- pipelines, work buffers,
+// launches, timing -- and the C entry points):
 //   * KD-tree closest-hit traversal (wr_traverse.h) as one generic queue kernel
 //   * BidirPathTracing::runIteration (bidirPathTracing.cpp:53-265) as a wavefront:
 //       light pass  : gen -> [trace -> shade] x 9 -> trace(splat rays) -> resolve
@@ -201,840 +203,11 @@ __global__ void __launch_bounds__(256) k_api_finish(DevScene S, const float* o3,
   }
 }
 
-// =============================================================== BDPT state
-struct BdptBuf {
-  int P = 0, cap_sq = 0;
-  // light subpath state (bidirPathTracing.h:7-18)
-  float *l_o, *l_d, *l_thr, *l_dvcm, *l_dvc;
-  int *l_len, *l_nspec;
-  uint32_t* l_ctr;
-  // stored light vertices [kVMax][...][P]
-  float *v_pos, *v_n, *v_wi, *v_thr, *v_dvcm, *v_dvc, *v_cont, *v_pd, *v_pg;
-  int *v_len, *v_nspec, *v_mat, *v_count;
-  // camera subpath state
-  float *c_o, *c_d, *c_thr, *c_dvcm, *c_dvc;
-  int *c_len, *c_nspec, *c_pix;
-  uint32_t* c_ctr;
-  // extension-ray queues (double buffered)
-  float *q_o[2], *q_d[2], *q_t[2];
-  int *q_path[2], *q_prim[2];
-  // shadow + aux closest-hit queue (splat / connection / NEE / DI-BSDF)
-  // shadow / aux queue and DI records, two each: the ones of step `slot` are
-  // [slot & 1], so a step's resolve and the next step's vertex shading (which
-  // writes [(slot + 1) & 1]) can run in one launch
-  struct Sq {
-    float *o, *d, *tgt, *val, *t;
-    int *meta, *pix, *prim;
-  } sq[2];
-  struct Di {
-    float *nee, *neew, *bsdf, *thr, *wlen;
-    int *flags, *light, *pix;
-    int* state;  // rays still to resolve | DI_VIS | DI_SAME (one atomic per resolved ray)
-  } di[2];
-  // direct-illumination records (getDirectIllumination, :484-608)
-};
-
-struct BdptArgs {
-  DevScene S;
-  BdptBuf B;
-  DevCounters* ctr;
-  StepCounters* sc;  // this iteration's queue counters
-  float* film;
-  int W, H, P;
-  uint32_t seed, iter;
-  int ctl, maxlen, faithful;
-};
-struct BdptGroup {
-  BdptArgs a[kGroup];
-};
-
-__device__ __forceinline__ bool len_ok(int ctl, int L) { return ctl <= 0 || L == ctl; }
-
-// generateLightSample (:267-311) + the first extension ray
-__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_light_gen(BdptGroup G_) {
-  const BdptArgs& A = G_.a[blockIdx.y];
-  const BdptBuf& B = A.B;
-  const int P = A.P;
-  const float lpp = 1.f / static_cast<float>(A.S.nlights);
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-    Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), 0};
-    const int id = min(static_cast<int>(rng.f() * static_cast<float>(A.S.nlights)), A.S.nlights - 1);
-    const DLight L = A.S.lights[id];
-    V3 pos, dir, rad;
-    float epdf = 0.f, dpdf = 0.f;
-    for (int tries = 0; tries < 64; ++tries) {
-      // emit(..., rng.randVector3(), rng.randVector3(), ...): the reference's
-      // compiler evaluates the second argument (posRand3) first
-      V3 pr = rng.v();
-      V3 dr = rng.v();
-      rad = light_emit(L, dr, pr, &pos, &dir, &epdf, &dpdf);
-      if (epdf > 1e-7f) break;
-    }
-    V3 thr = rad;
-    epdf *= lpp;
-    dpdf *= lpp;
-    thr = div_plain(thr, epdf);
-    st3(B.l_o, P, p, pos);
-    st3(B.l_d, P, p, dir);
-    st3(B.l_thr, P, p, thr);
-    B.l_dvcm[p] = dpdf / epdf;
-    B.l_dvc[p] = 1.f / epdf;  // AreaLight::isDelta() == 0
-    B.l_len[p] = 1;
-    B.l_nspec[p] = 0;
-    B.l_ctr[p] = rng.ctr;
-    B.v_count[p] = 0;
-    // Ray(origin + dir * EPS, dir) (:79-80)
-    st3(B.q_o[0], P, p, pos + dir * WR_EPS);
-    st3(B.q_d[0], P, p, normalize(dir));
-    B.q_path[0][p] = p;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = P;
-}
-
-// sampleScattering (:370-416).  Returns false when the subpath ends.
-__device__ __forceinline__ bool sample_scatter(const DevScene& S, Rng& rng, const Bsdf& b, V3 hit, V3& o, V3& dir,
-                                               V3& thr, float& dvcm, float& dvc, int& nspec) {
-  float dpdf = 0.f, cos_wo = 0.f;
-  int type;
-  V3 wo = dir;
-  const V3 f = bsdf_sample(b, S.mats, rng.v(), &wo, &dpdf, &cos_wo, &type);
-  if (black(f)) return false;
-  dir = wo;
-  float rpdf = dpdf;
-  if ((type & T_SPEC) == 0) rpdf = bsdf_pdf(b, S.mats, dir, true);
-  const float cp = b.cont;
-  if (rng.f() > cp) return false;
-  dpdf *= cp;
-  rpdf *= cp;
-  if (type & T_SPEC) {
-    ++nspec;
-    dvcm = 0.f;
-    dvc *= cos_wo;
-  } else {
-    dvc = (1.f / dpdf) * (dvcm + dvc * rpdf);
-    dvcm = 1.f / dpdf;
-  }
-  o = hit;
-  thr = mul(thr, f) * (cos_wo / dpdf);
-  return true;
-}
-
-// One light-subpath vertex (:77-128)
-__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGroup G_, int slot) {
-  const BdptArgs& A = G_.a[blockIdx.y];
-  const BdptBuf& B = A.B;
-  const DevScene& S = A.S;
-  const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
-  const int n = A.sc->ext[slot];
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
-  const int gstride = gridDim.x * blockDim.x;
-  const int nround = (n + gstride - 1) / gstride * gstride;  // whole waves reach the appends
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
-    bool ext = false, splat = false;
-    V3 e_o, e_d, s_o, s_d, s_val;
-    int s_pix = -1, p = -1;
-    if (j < n) {
-      p = B.q_path[cur][j];
-      const int prim = B.q_prim[cur][j];
-      if (prim >= 0) {
-        const float t = B.q_t[cur][j];
-        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
-        const Hit h = rebuild_hit(S, prim, t, o, d);
-        Bsdf b;
-        bsdf_init(b, -d, h.n, h.mat, S.mats);
-        if (b.mat != 0) {
-          float dvcm = B.l_dvcm[p], dvc = B.l_dvc[p];
-          int len = B.l_len[p], nspec = B.l_nspec[p];
-          V3 thr = ld3(B.l_thr, P, p);
-          dvcm *= (t * t);  // pathLength > 1 || isFiniteLight: always for area lights (:94-97)
-          dvcm /= fabsf(b.wi.z);
-          dvc /= fabsf(b.wi.z);
-          if (!b.delta) {  // lightStates.push_back (:101-102)
-            const int k = B.v_count[p];
-            const int slot = k * P + p;
-            st3(B.v_pos, kVMax * P, slot, h.p);
-            st3(B.v_n, kVMax * P, slot, h.n);
-            st3(B.v_wi, kVMax * P, slot, b.wi);
-            st3(B.v_thr, kVMax * P, slot, thr);
-            B.v_dvcm[slot] = dvcm;
-            B.v_dvc[slot] = dvc;
-            B.v_cont[slot] = b.cont;
-            B.v_pd[slot] = b.pd;
-            B.v_pg[slot] = b.pg;
-            B.v_len[slot] = len;
-            B.v_nspec[slot] = nspec;
-            B.v_mat[slot] = b.mat;
-            B.v_count[p] = k + 1;
-            if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
-              const DCam& cam = S.cam;
-              const V3 ip = t_point(cam.w2r, h.p);
-              if (check_raster(cam, ip.x, ip.y)) {
-                V3 dtc = cam.pos - h.p;
-                if (dot(-dtc, cam.fwd) > 0) {
-                  const float d2 = sqr_len(dtc);
-                  const float dist = sqrtf(d2);
-                  dtc = div_guarded(dtc, dist);
-                  float cos_to = 0.f, dp, rp;
-                  const V3 f = bsdf_f(b, S.mats, dtc, &cos_to, &dp, &rp);
-                  if (!black(f)) {
-                    rp *= b.cont;
-                    const float cos_at = dot(-dtc, cam.fwd);
-                    const float ipd = cam.plane_dist / cos_at;
-                    const float i2sa = (ipd * ipd) / cos_at;
-                    const float i2s = i2sa * fabsf(cos_to) / d2;
-                    const float pdf_a = i2s;
-                    const float s2i = 1.f / i2s;
-                    const V3 res = div_plain(mul(thr, f), static_cast<float>(P) * s2i);
-                    if (!black(res)) {
-                      const float wl = (pdf_a / static_cast<float>(P)) * (dvcm + rp * dvc);
-                      const float w = 1.f / (wl + 1.f);
-                      splat = true;
-                      s_o = h.p;
-                      s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
-                      s_val = res * w;
-                      s_pix = pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W);
-                    }
-                  }
-                }
-              }
-            }
-          }
-          if (!(len + 2 > A.maxlen)) {  // (:123-127)
-            Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), B.l_ctr[p]};
-            V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
-            if (sample_scatter(S, rng, b, h.p, lo, ld, thr, dvcm, dvc, nspec)) {
-              ext = true;
-              ++len;
-              e_o = lo + ld * WR_EPS;
-              e_d = normalize(ld);
-              st3(B.l_o, P, p, lo);
-              st3(B.l_d, P, p, ld);
-              st3(B.l_thr, P, p, thr);
-              B.l_dvcm[p] = dvcm;
-              B.l_dvc[p] = dvc;
-              B.l_len[p] = len;
-              B.l_nspec[p] = nspec;
-            }
-            B.l_ctr[p] = rng.ctr;
-          }
-        }
-      }
-    }
-    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
-    if (ext) {
-      st3(B.q_o[nxt], P, ei, e_o);
-      st3(B.q_d[nxt], P, ei, e_d);
-      B.q_path[nxt][ei] = p;
-    }
-    const int si = wave_append(&A.sc->sq[kCamSlot], splat);  // traced with the camera primaries
-    if (splat) {
-      const BdptBuf::Sq& Q = B.sq[kCamSlot & 1];
-      st3(Q.o, B.cap_sq, si, s_o);
-      st3(Q.d, B.cap_sq, si, s_d);
-      st3(Q.tgt, B.cap_sq, si, S.cam.pos);
-      st3(Q.val, B.cap_sq, si, s_val);
-      Q.meta[si] = SQ_SPLAT << 30;
-      Q.pix[si] = s_pix;
-    }
-  }
-}
-
-// generateCameraSample (:418-452) + first extension ray, for queue entry s;
-// returns the path index.  (VertexCM::generateCameraSample, vertexcm.cpp:446-479,
-// is the same plus dVM = 0.)
-__device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
-  const BdptBuf& B = A.B;
-  const DCam& cam = A.S.cam;
-  const int P = A.P;
-  // queue order: 8x8 raster tiles per wave (coherent primary rays); the
-  // path <-> pixel mapping stays the reference's (x = p / W, y = p % W, :422-423)
-  const bool tiled = (A.W % 8) == 0 && (A.H % 8) == 0;
-  const int tiles_y = A.W / 8;
-  int x, y;
-  if (tiled) {
-    const int t = s >> 6, w = s & 63;
-    x = (t / tiles_y) * 8 + (w >> 3);
-    y = (t % tiles_y) * 8 + (w & 7);
-  } else {
-    x = s / A.W;
-    y = s % A.W;
-  }
-  const int p = x * A.W + y;
-  Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), 0};
-  const V3 jit = rng.v();
-  const float sx = static_cast<float>(x) + jit.x, sy = static_cast<float>(y) + jit.y;
-  const V3 rp = t_point(cam.r2w, v3(sx, sy, 0.f));
-  const V3 d = normalize(rp - cam.pos);  // Ray(pos, p - pos) (camera.cpp:37-42)
-  const float cos_at = dot(cam.fwd, d);
-  const float ipd = cam.plane_dist / cos_at;
-  const float i2sa = (ipd * ipd) / cos_at;
-  st3(B.c_o, P, p, cam.pos);
-  st3(B.c_d, P, p, d);
-  st3(B.c_thr, P, p, v3(1.f, 1.f, 1.f));
-  B.c_dvcm[p] = static_cast<float>(P) / i2sa;
-  B.c_dvc[p] = 0.f;
-  B.c_len[p] = 1;
-  B.c_nspec[p] = 0;
-  B.c_ctr[p] = rng.ctr;
-  B.c_pix[p] = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
-  st3(B.q_o[0], P, s, cam.pos + d * WR_EPS);
-  st3(B.q_d[0], P, s, normalize(d));
-  B.q_path[0][s] = p;
-  return p;
-}
-__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGroup G_) {
-  const BdptArgs& A = G_.a[blockIdx.y];
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < A.P; s += gridDim.x * blockDim.x) camera_gen_one(A, s);
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[kCamSlot] = A.P;
-}
-
-// One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
-// connections (shadow rays queued), scattering.
-__device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, int bid, int nblk) {
-  const BdptBuf& B = A.B;
-  const DevScene& S = A.S;
-  const int P = A.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;
-  const int n = A.sc->ext[slot];
-  if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
-  const int gstride = nblk * blockDim.x;
-  const int nround = (n + gstride - 1) / gstride * gstride;
-  const float lpp = 1.f / static_cast<float>(S.nlights);
-  const BdptBuf::Sq& Q = B.sq[(slot + 1) & 1];  // rays traced at the next step
-  const BdptBuf::Di& D = B.di[(slot + 1) & 1];
-  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
-    bool live = false, ext = false, conn_phase = false, nee = false, dib = false;
-    int p = -1, pix = -1, nv = 0, len = 0, nspec = 0, cnspec = 0;
-    V3 hp{}, thr{}, cthr{}, e_o{}, e_d{}, nee_tgt{}, nee_d{}, dib_o{}, dib_d{};
-    float dvcm = 0.f, dvc = 0.f, cdvcm = 0.f, cdvc = 0.f;
-    Bsdf b;
-    b.mat = 0;
-    if (j < n) {
-      p = B.q_path[cur][j];
-      const int prim = B.q_prim[cur][j];
-      if (prim >= 0) {
-        const float t = B.q_t[cur][j];
-        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
-        const Hit h = rebuild_hit(S, prim, t, o, d);
-        bsdf_init(b, -d, h.n, h.mat, S.mats);
-        if (b.mat != 0) {
-          hp = h.p;
-          pix = B.c_pix[p];
-          dvcm = B.c_dvcm[p];
-          dvc = B.c_dvc[p];
-          len = B.c_len[p];
-          nspec = B.c_nspec[p];
-          thr = ld3(B.c_thr, P, p);
-          dvcm *= (t * t);  // (:180-182)
-          dvcm /= fabsf(b.wi.z);
-          dvc /= fabsf(b.wi.z);
-          // this vertex's state, used by DI and the connections; the scatter
-          // below updates thr / dvcm / dvc / nspec for the next vertex
-          cthr = thr;
-          cdvcm = dvcm;
-          cdvc = dvc;
-          cnspec = nspec;
-          if (h.mat < 0) {  // hit an emitter (:184-199)
-            if (len_ok(A.ctl, len)) {
-              const DLight L = S.lights[-h.mat - 1];
-              float dpa, ep;
-              V3 r = light_radiance(L, d, &dpa, &ep);
-              if (!black(r)) {
-                if (len != 1) {  // getLightRadiance (:454-482)
-                  dpa *= lpp;
-                  ep *= lpp;
-                  const float wc = dpa * dvcm + ep * dvc;
-                  r = r * (1.f / (1.f + wc));
-                }
-                film_add(A.film, pix, mul(thr, r));
-              }
-            }
-          } else if (len < A.maxlen) {
-            live = true;
-            Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), B.c_ctr[p]};
-            if (!b.delta && len_ok(A.ctl, len + 1)) {  // getDirectIllumination (:205-217, :484-608)
-              const float wlen = 1.f / (static_cast<float>(len) + 1.f - static_cast<float>(nspec));
-              const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
-              const DLight L = S.lights[lid];
-              V3 dtl;
-              float dist = 0.f, dpdf = 0.f, epdf = 0.f, cal = 0.f;
-              const V3 illu = light_illuminance(L, hp, rng.v(), &dtl, &dist, &dpdf, &epdf, &cal);
-              int flags = 0;
-              V3 nee_val = v3(0.f, 0.f, 0.f), bsdf_val = v3(0.f, 0.f, 0.f);
-              float nee_w = 0.f;
-              if (!black(illu) && dpdf > 0) {
-                float cos_to = 0.f, bdp, brp;
-                const V3 bf = bsdf_f(b, S.mats, dtl, &cos_to, &bdp, &brp);
-                if (!black(bf)) {
-                  bdp *= b.cont;
-                  brp *= b.cont;
-                  const V3 tmp = div_plain(mul(illu, bf) * cos_to, dpdf * lpp);
-                  if (!black(tmp)) {
-                    nee = true;
-                    flags |= DI_NEE;
-                    nee_d = normalize(dtl);
-                    nee_tgt = hp + dtl * dist;
-                    const float wl = bdp / (dpdf * lpp);
-                    const float wc = (epdf * cos_to / (dpdf * cal)) * (dvcm + brp * dvc);
-                    nee_w = 1.f / (wl + 1.f + wc);
-                    nee_val = tmp * (dpdf / (dpdf + bdp));
-                  }
-                }
-              }
-              V3 dtl2 = dtl;
-              float dpdf2 = dpdf, cos_s = 0.f;
-              int type;
-              const V3 bf2 = bsdf_sample(b, S.mats, rng.v(), &dtl2, &dpdf2, &cos_s, &type);
-              if (!black(bf2) && dpdf2 > 0) {
-                float w = 1.f;
-                V3 illu2 = illu;
-                bool early = false;
-                if (!(type & T_SPEC)) {
-                  float lpdf, ep2;
-                  illu2 = light_radiance(L, dtl2, &lpdf, &ep2);
-                  if (cmpf(lpdf) == 0) early = true;  // (:563-564) returns res unweighted
-                  else w = dpdf2 / (dpdf2 + lpdf);
-                }
-                if (early) {
-                  flags |= DI_EARLY;
-                } else {
-                  dib = true;
-                  flags |= DI_BSDF;
-                  dib_o = hp + dtl2 * WR_EPS;
-                  dib_d = normalize(dtl2);
-                  if (!black(illu2)) bsdf_val = div_plain(mul(illu2, bf2) * cos_s, dpdf2) * w;
-                }
-              }
-              // a record only when a ray will be resolved: with neither the NEE
-              // nor the BSDF ray the contribution is exactly zero (:533-607)
-              const int nrays = (nee ? 1 : 0) + (dib ? 1 : 0);
-              if (nrays > 0) {
-                D.flags[p] = flags;
-                st3(D.nee, P, p, nee_val);
-                D.neew[p] = nee_w;
-                st3(D.bsdf, P, p, bsdf_val);
-                st3(D.thr, P, p, thr);
-                D.wlen[p] = wlen;
-                D.light[p] = lid;
-                D.pix[p] = pix;
-                D.state[p] = nrays;
-              }
-            }
-            if (!b.delta) {
-              conn_phase = true;
-              nv = B.v_count[p];
-            }
-            V3 so = ld3(B.c_o, P, p), sd = ld3(B.c_d, P, p);
-            if (sample_scatter(S, rng, b, hp, so, sd, thr, dvcm, dvc, nspec)) {
-              ext = true;
-              e_o = so + sd * WR_EPS;
-              e_d = normalize(sd);
-            }
-            B.c_ctr[p] = rng.ctr;
-            // state for the NEXT vertex; the connections below use the values of
-            // THIS vertex, so keep them (thr/dvcm/dvc/nspec are re-read below)
-            st3(B.c_o, P, p, so);
-            st3(B.c_d, P, p, sd);
-          }
-        }
-      }
-    }
-    // DI queue entries
-    {
-      const int ni = wave_append(&A.sc->sq[slot + 1], nee);
-      if (nee) {
-        st3(Q.o, cap, ni, hp);
-        st3(Q.d, cap, ni, nee_d);
-        st3(Q.tgt, cap, ni, nee_tgt);
-        Q.meta[ni] = (SQ_NEE << 30) | p;
-        Q.pix[ni] = pix;
-      }
-      const int bi = wave_append(&A.sc->sq[slot + 1], dib);
-      if (dib) {
-        st3(Q.o, cap, bi, dib_o);
-        st3(Q.d, cap, bi, dib_d);
-        Q.meta[bi] = (SQ_DIB << 30) | p;
-        Q.pix[bi] = pix;
-      }
-    }
-    // vertex connections to the paired light subpath (:219-257)
-    if (__ballot(conn_phase && nv > 0)) {
-      for (int k = 0; __ballot(conn_phase && k < nv); ++k) {
-        bool shoot = false;
-        V3 sdir{}, stgt{}, sval{};
-        if (conn_phase && k < nv) {
-          const int slot = k * P + p;
-          const int llen = B.v_len[slot];
-          if (llen + 1 + len > A.maxlen) {
-            nv = k;  // break (:237-239)
-          } else {
-            // connectVertices (:610-665)
-            const V3 lpos = ld3(B.v_pos, kVMax * P, slot);
-            V3 dir = lpos - hp;
-            const float d2 = sqr_len(dir);
-            const float dist = sqrtf(d2);
-            dir = div_guarded(dir, dist);
-            float cos_c = 0.f, cdp, crp;
-            const V3 cf = bsdf_f(b, S.mats, dir, &cos_c, &cdp, &crp);
-            if (!black(cf)) {
-              cdp *= b.cont;
-              crp *= b.cont;
-              Bsdf lb;
-              lb.mat = B.v_mat[slot];
-              lb.fr = frame_from_z(ld3(B.v_n, kVMax * P, slot));
-              lb.wi = ld3(B.v_wi, kVMax * P, slot);
-              lb.pd = B.v_pd[slot];
-              lb.pg = B.v_pg[slot];
-              lb.cont = B.v_cont[slot];
-              float cos_l = 0.f, ldp, lrp;
-              const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
-              if (!black(lf)) {
-                ldp *= lb.cont;
-                lrp *= lb.cont;
-                const float G = cos_l * cos_c / d2;
-                if (!(cmpf(G) < 0)) {
-                  const float cdpa = cdp * fabsf(cos_l) / (dist * dist);
-                  const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
-                  const V3 res = mul(cf, lf) * G;
-                  if (!black(res)) {
-                    const float wl = cdpa * (B.v_dvcm[slot] + lrp * B.v_dvc[slot]);
-                    const float wc = ldpa * (cdvcm + crp * cdvc);
-                    const float w = 1.f / (wl + 1.f + wc);
-                    const bool counts = len_ok(A.ctl, llen + 1 + len);
-                    if (counts || A.faithful) {
-                      shoot = true;
-                      sdir = normalize(dir);
-                      stgt = hp + dir * dist;
-                      if (counts) {
-                        const float wlen = 1.f / (static_cast<float>(llen) + 1.f + static_cast<float>(len) -
-                                                  static_cast<float>(B.v_nspec[slot]) - static_cast<float>(cnspec));
-                        const V3 lthr = ld3(B.v_thr, kVMax * P, slot);
-                        sval = mul(mul(cthr, lthr), res * w) * wlen;
-                      }
-                    }
-                  }
-                }
-              }
-            }
-          }
-        }
-        const int si = wave_append(&A.sc->sq[slot + 1], shoot);
-        if (shoot) {
-          st3(Q.o, cap, si, hp);
-          st3(Q.d, cap, si, sdir);
-          st3(Q.tgt, cap, si, stgt);
-          st3(Q.val, cap, si, sval);
-          Q.meta[si] = (SQ_CONN << 30) | p;
-          Q.pix[si] = pix;
-        }
-      }
-    }
-    if (live) {  // commit scattered state (:259-260) and the loop increment
-      if (ext) {
-        st3(B.c_thr, P, p, thr);
-        B.c_dvcm[p] = dvcm;
-        B.c_dvc[p] = dvc;
-        B.c_nspec[p] = nspec;
-        B.c_len[p] = len + 1;
-      }
-    }
-    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
-    if (ext) {
-      st3(B.q_o[nxt], P, ei, e_o);
-      st3(B.q_d[nxt], P, ei, e_d);
-      B.q_path[nxt][ei] = p;
-    }
-  }
-}
-
-// Light-tracing splats and camera-pass shadow / aux rays after traversal.
-// Light-tracing splats and camera-pass shadow / aux rays of step `slot` after
-// traversal.  A DI record is finalized (getDirectIllumination's combination,
-// :533-607) by whichever of its rays is resolved last: each resolve adds
-// (its result bit - 1) to the record's state word in one atomic.
-__device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int bid, int nblk) {
-  const BdptBuf& B = A.B;
-  const DevScene& S = A.S;
-  const BdptBuf::Sq& Q = B.sq[slot & 1];
-  const BdptBuf::Di& D = B.di[slot & 1];
-  const int n = A.sc->sq[slot], cap = B.cap_sq, P = A.P;
-  const int gstride = nblk * blockDim.x;
-  const int nround = (n + gstride - 1) / gstride * gstride;
-  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
-    bool is_shadow = false, is_closest = false;
-    if (j < n) {
-      const int meta = Q.meta[j];
-      const int kind = (meta >> 30) & 3, p = meta & 0x3fffffff;
-      const int prim = Q.prim[j];
-      const float t = Q.t[j];
-      int di_bits = -1;  // >= 0: this ray belongs to DI record p
-      if (kind == SQ_DIB) {  // DI BSDF-sampled ray: same light? (:570-596)
-        is_closest = true;
-        bool same = false;
-        if (prim >= 0) {
-          const int m = S.prim_mat[prim];
-          same = m < 0 && -m - 1 == D.light[p];
-        }
-        di_bits = same ? DI_SAME : 0;
-      } else {  // Scene::occluded: position equality (scene.cpp:55-69)
-        is_shadow = true;
-        bool unocc = true;
-        if (prim >= 0) {
-          const V3 o = ld3(Q.o, cap, j), d = ld3(Q.d, cap, j);
-          unocc = near_eq(o + d * t, ld3(Q.tgt, cap, j));
-        }
-        if (kind == SQ_NEE) {
-          di_bits = unocc ? DI_VIS : 0;
-        } else if (unocc) {
-          film_add(A.film, Q.pix[j], ld3(Q.val, cap, j));
-        }
-      }
-      if (di_bits >= 0) {
-        const int st = atomicAdd(&D.state[p], di_bits - 1) + di_bits - 1;
-        if ((st & DI_COUNT) == 0) {
-          const int flags = D.flags[p];
-          V3 res = v3(0.f, 0.f, 0.f);
-          float weight = 0.f;
-          if ((flags & DI_NEE) && (st & DI_VIS)) {
-            weight = D.neew[p];
-            res = res + ld3(D.nee, P, p);
-          }
-          V3 di;
-          if (flags & DI_EARLY) {
-            di = res;
-          } else {
-            if ((flags & DI_BSDF) && (st & DI_SAME)) res = res + ld3(D.bsdf, P, p);
-            di = res * weight;
-          }
-          film_add(A.film, D.pix[p], mul(ld3(D.thr, P, p), di) * D.wlen[p]);
-        }
-      }
-    }
-    wave_count(&A.ctr->shadow, is_shadow);
-    wave_count(&A.ctr->closest, is_closest);
-  }
-}
-
-// One camera-pass step after its traversal: resolve the step's shadow / aux
-// rays (blocks [0, nres)) and shade its camera vertices (the rest) -- they touch
-// different queue / DI buffers.  The last step has no vertices (shade = 0).
-__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_step(BdptGroup G_, int slot, int nres,
-                                                                         int shade) {
-  const BdptArgs& A = G_.a[blockIdx.y];
-  if (static_cast<int>(blockIdx.x) < nres) sq_resolve_body(A, slot, blockIdx.x, nres);
-  else if (shade) camera_shade_body(A, slot, blockIdx.x - nres, gridDim.x - nres);
-}
-
-// =============================================================== VCM
+// =============================================================== BDPT, VCM, PT
+#include "wr_bdpt.h"
 #include "wr_vcm.h"
 static_assert(sizeof(VcmGroup) <= 4000, "kernel argument block too large");
-
-// =============================================================== PT
-struct PtBuf {
-  int P = 0;
-  float *o, *d, *pw, *last_pdf;
-  int *last_spec, *len, *pix;
-  uint32_t* ctr;
-  float *q_o[2], *q_d[2], *q_t[2];
-  int *q_path[2], *q_prim[2];
-  // NEE shadow rays, two buffers: those of step `slot` are [slot & 1], so a
-  // step's resolve and the next vertex shading (writing [(slot + 1) & 1]) run
-  // in one launch
-  struct Sq {
-    float *o, *d, *tgt, *val, *t;
-    int *pix, *prim;
-  } sq[2];
-};
-struct PtArgs {
-  DevScene S;
-  PtBuf T;
-  DevCounters* ctr;
-  StepCounters* sc;  // this sample's queue counters
-  float* film;
-  int W, H, P, spp, grid_len, max_depth;
-  uint32_t seed, k;
-};
-struct PtGroup {
-  PtArgs a[kGroup];
-};
-
-// SurfaceIntegrator::render per-sample setup (surfaceIntegrator.cpp:26-34)
-__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_gen(PtGroup G_) {
-  const PtArgs& A = G_.a[blockIdx.y];
-  const PtBuf& T = A.T;
-  const DCam& cam = A.S.cam;
-  const int P = A.P;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-    const int i = p / A.W, jj = p % A.W;
-    Rng rng{stream_key(A.seed, A.k, 2, static_cast<uint32_t>(p)), 0};
-    const V3 v0 = v3(static_cast<float>(jj) - 0.5f, static_cast<float>(i) - 0.5f, 0.f);
-    const V3 v1 = v3(static_cast<float>(jj) + 0.5f, static_cast<float>(i) - 0.5f, 0.f);
-    const V3 v2 = v3(static_cast<float>(jj) - 0.5f, static_cast<float>(i) + 0.5f, 0.f);
-    const V3 pr = sample_rect_strat(rng.v(), v0, v1, v2, static_cast<int>(A.k), A.grid_len);
-    const V3 wp = t_point(cam.r2w, v3(pr.x, pr.y, 0.f));
-    const V3 d = normalize(wp - cam.pos);
-    st3(T.o, P, p, cam.pos);
-    st3(T.d, P, p, d);
-    st3(T.pw, P, p, v3(1.f, 1.f, 1.f));
-    T.last_pdf[p] = 1.f;
-    T.last_spec[p] = 1;
-    T.len[p] = 1;
-    T.pix[p] = i * A.W + jj;
-    T.ctr[p] = rng.ctr;
-    st3(T.q_o[0], P, p, cam.pos);  // Ray r(ray): no EPS offset for the primary ray
-    st3(T.q_d[0], P, p, d);
-    T.q_path[0][p] = p;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = P;
-}
-
-// One PathIntegrator::raytracing iteration (pathIntegrator.cpp:43-146)
-__device__ __forceinline__ void pt_shade_body(const PtArgs& A, int slot, int bid, int nblk) {
-  const PtBuf& T = A.T;
-  const DevScene& S = A.S;
-  const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
-  const int n = A.sc->ext[slot];
-  if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
-  const int gstride = nblk * blockDim.x;
-  const int nround = (n + gstride - 1) / gstride * gstride;
-  const float lpp = 1.f / static_cast<float>(S.nlights);
-  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
-    bool ext = false, shadow = false;
-    int p = -1, pix = -1;
-    V3 e_o{}, e_d{}, s_o{}, s_d{}, s_tgt{}, s_val{};
-    if (j < n) {
-      p = T.q_path[cur][j];
-      const int prim = T.q_prim[cur][j];
-      if (prim >= 0) {
-        const float t = T.q_t[cur][j];
-        const V3 o = ld3(T.q_o[cur], P, j), d = ld3(T.q_d[cur], P, j);
-        const Hit h = rebuild_hit(S, prim, t, o, d);
-        Bsdf b;
-        bsdf_init(b, -d, h.n, h.mat, S.mats);
-        pix = T.pix[p];
-        if (b.mat != 0) {
-          V3 pw = ld3(T.pw, P, p);
-          const int len = T.len[p];
-          if (b.mat < 0) {  // (:53-73)
-            const DLight L = S.lights[-b.mat - 1];
-            float dpa, ep;
-            const V3 c = light_radiance(L, d, &dpa, &ep);
-            if (!black(c)) {
-              float mw = 1.f;
-              if (len > 1 && !T.last_spec[p]) {
-                const float dp = dpa * (t * t) / fabsf(b.wi.z);  // pdfAtoW
-                const float lp = T.last_pdf[p];
-                mw = lp / (lp + dp * lpp);
-              }
-              film_add(A.film, pix, mul(pw, c) * mw);
-            }
-          } else if (!(len > A.max_depth) && cmpf(b.cont) != 0) {
-            Rng rng{stream_key(A.seed, A.k, 2, static_cast<uint32_t>(p)), T.ctr[p]};
-            if (!b.delta) {  // (:81-118)
-              const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
-              const DLight L = S.lights[lid];
-              V3 dtl;
-              float dist = 0.f, dpdf = 0.f, ep, cal;
-              const V3 illu = light_illuminance(L, h.p, rng.v(), &dtl, &dist, &dpdf, &ep, &cal);
-              if (!black(illu)) {
-                shadow = true;
-                s_o = h.p + dtl * WR_EPS;
-                s_d = normalize(dtl);
-                s_tgt = h.p + dtl * (dist - WR_EPS);
-                float bp, cw = 0.f;
-                const V3 bf = bsdf_f(b, S.mats, dtl, &cw, &bp, nullptr);
-                s_val = v3(0.f, 0.f, 0.f);
-                if (!black(bf)) {
-                  bp *= b.cont;
-                  const float w = (dpdf * lpp) / ((dpdf * lpp) + bp);
-                  const V3 c = mul(illu, bf) * (w * cw / (lpp * dpdf));
-                  s_val = mul(c, pw);
-                }
-              }
-            }
-            float pdf = 0.f, cw = 0.f;
-            int type;
-            V3 dn = d;
-            const V3 bf = bsdf_sample(b, S.mats, rng.v(), &dn, &pdf, &cw, &type);
-            if (!black(bf)) {  // (:124-145)
-              const float cp = b.cont;
-              const int lspec = (type & T_SPEC) != 0;
-              const float lpdf = pdf * cp;
-              bool cont = true;
-              if (cmpf(cp - 1.f) < 0) {
-                if (cmpf(rng.f() - cp) > 0) cont = false;
-                else pdf *= cp;
-              }
-              if (cont) {
-                pw = mul(pw, bf) * (cw / pdf);
-                ext = true;
-                e_o = h.p + dn * WR_EPS;
-                e_d = dn;  // r.dir stays un-normalised (:144-145)
-                st3(T.pw, P, p, pw);
-                T.last_spec[p] = lspec;
-                T.last_pdf[p] = lpdf;
-                T.len[p] = len + 1;
-              }
-            }
-            T.ctr[p] = rng.ctr;
-          }
-        }
-      }
-    }
-    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
-    if (ext) {
-      st3(T.q_o[nxt], P, ei, e_o);
-      st3(T.q_d[nxt], P, ei, e_d);
-      T.q_path[nxt][ei] = p;
-    }
-    const int si = wave_append(&A.sc->sq[slot + 1], shadow);
-    if (shadow) {
-      const PtBuf::Sq& Q = T.sq[(slot + 1) & 1];
-      st3(Q.o, P, si, s_o);
-      st3(Q.d, P, si, s_d);
-      st3(Q.tgt, P, si, s_tgt);
-      st3(Q.val, P, si, s_val);
-      Q.pix[si] = pix;
-    }
-  }
-}
-
-// NEE shadow rays of step `slot` after traversal (pathIntegrator.cpp:95-110):
-// unoccluded => the queued contribution goes to the film
-__device__ __forceinline__ void pt_resolve_body(const PtArgs& A, int slot, int bid, int nblk) {
-  const PtBuf& T = A.T;
-  const PtBuf::Sq& Q = T.sq[slot & 1];
-  const int n = A.sc->sq[slot], P = A.P;
-  const int gstride = nblk * blockDim.x;
-  const int nround = (n + gstride - 1) / gstride * gstride;
-  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
-    bool is = false;
-    if (j < n) {
-      is = true;
-      bool unocc = true;
-      const int prim = Q.prim[j];
-      if (prim >= 0) {
-        const V3 o = ld3(Q.o, P, j), d = ld3(Q.d, P, j);
-        unocc = near_eq(o + d * Q.t[j], ld3(Q.tgt, P, j));
-      }
-      if (unocc) film_add(A.film, Q.pix[j], ld3(Q.val, P, j));
-    }
-    wave_count(&A.ctr->shadow, is);
-  }
-}
-
-// One PT step after its traversal: resolve the step's shadow rays (blocks
-// [0, nres)) and shade its vertices (the rest, `shade` = 0 after the last
-// bounce) -- they read and write different shadow-queue buffers.
-__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_step(PtGroup G_, int slot, int nres, int shade) {
-  const PtArgs& A = G_.a[blockIdx.y];
-  if (static_cast<int>(blockIdx.x) < nres) pt_resolve_body(A, slot, blockIdx.x, nres);
-  else if (shade) pt_shade_body(A, slot, blockIdx.x - nres, gridDim.x - nres);
-}
-
-__global__ void k_film_accumulate(float* dst, const float* src, int64_t n) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    dst[i] = dst[i] + src[i];
-}
+#include "wr_pt.h"
 
 }  // namespace
 
