@@ -170,6 +170,17 @@ int wr_render_bdpt(wr_context* ctx, const wr_bdpt_params* p, float* film, int fi
  * radiance SUM (the reference's final film->scale(1/spp) is left to the caller). */
 int wr_render_path(wr_context* ctx, const wr_path_params* p, float* film, int film_on_device, wr_stats* stats);
 
+/* PathIntegrator::raytracing(const Ray& ray, int dep) (pathIntegrator.cpp:29-148),
+ * the per-sample estimator SurfaceIntegrator::render calls, for a batch of
+ * caller rays (o and d used as given, like a constructed Ray; tmin / tmax
+ * ignored: the reference traces with 0 / INF).  rgb: n*3 floats, overwritten
+ * with the radiance of each ray.  Ray k draws from the counter-RNG stream
+ * (seed, sample, 2, k) -- the PT render's streams skip that stream's first
+ * draw, which stratifies the pixel sample.  `dep` is unused by the reference
+ * and has no counterpart. */
+int wr_path_radiance(wr_context* ctx, const wr_ray* rays, int64_t n, int32_t max_depth, uint32_t seed,
+                     int32_t sample, float* rgb, wr_stats* stats);
+
 /* VertexCM::render (surfaceIntegrator/vertexcm.cpp:23-27, runIteration :47-285):
  * vertex connection + vertex merging.  The reference's point KD tree over the
  * light vertices (scene/KDtree.h) is replaced by a hash grid: searchInRadius

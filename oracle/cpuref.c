@@ -2362,6 +2362,23 @@ int cr_render_pt(const cr_scene* s, int W, int H, int spp, int max_depth, uint32
     return 0;
 }
 
+/* PathIntegrator::raytracing for caller rays (o, d as given), counter RNG
+ * stream (seed, sample, 2, k) from its first draw: the check of wr_path_radiance */
+int cr_pt_radiance(const cr_scene* s, const float* rays6, int64_t n, int max_depth, uint32_t seed,
+                   uint32_t sample, float* out3, cr_stats* st) {
+    init_consts();
+    if (!s || s->nprims == 0 || s->nlights == 0) { set_err("scene has no geometry or lights", NULL); return -1; }
+    rng_t rng;
+    for (int64_t k = 0; k < n; k++) {
+        rng_for(&rng, CR_RNG_COUNTER, NULL, seed, sample, 2, (uint32_t)k);
+        ray_t r = {mk(rays6[6 * k], rays6[6 * k + 1], rays6[6 * k + 2]),
+                   mk(rays6[6 * k + 3], rays6[6 * k + 4], rays6[6 * k + 5]), 0.f, R_INF};
+        c3 v = pt_trace(s, &rng, r, max_depth, st);
+        out3[3 * k] = v.r; out3[3 * k + 1] = v.g; out3[3 * k + 2] = v.b;
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------------- */
 /* Known-answer hooks                                                         */
 /* ------------------------------------------------------------------------- */

@@ -80,6 +80,11 @@ int cr_render_vcm(const cr_scene* s, int W, int H, int iter_begin, int iteration
 int cr_render_pt(const cr_scene* s, int W, int H, int spp, int max_depth, uint32_t seed,
                  int rng_mode, int64_t pix_begin, int64_t pix_end, float* film, cr_stats* st);
 
+/* PathIntegrator::raytracing per caller ray (rays6: o, d as given), counter RNG
+ * stream (seed, sample, 2, k) from its first draw; out3: radiance per ray. */
+int cr_pt_radiance(const cr_scene* s, const float* rays6, int64_t n, int max_depth, uint32_t seed,
+                   uint32_t sample, float* out3, cr_stats* st);
+
 /* Counter RNG (shared spec with the HIP path). */
 uint64_t cr_stream_key(uint32_t seed, uint32_t iteration, uint32_t subpath, uint32_t path);
 uint32_t cr_stream_u32(uint64_t key, uint32_t index);

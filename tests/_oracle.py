@@ -46,6 +46,7 @@ def lib():
         L.cr_render_vcm.argtypes = [P, I, I, I, I, U32, I, I, I, C.c_float, C.c_float, I64, I64, F,
                                     C.POINTER(Stats)]
         L.cr_render_pt.argtypes = [P, I, I, I, I, U32, I, I64, I64, F, C.POINTER(Stats)]
+        L.cr_pt_radiance.argtypes = [P, F, I64, I, U32, U32, F, C.POINTER(Stats)]
         L.cr_stream_key.restype = C.c_uint64
         L.cr_stream_key.argtypes = [U32, U32, U32, U32]
         L.cr_stream_u32.restype = C.c_uint32
@@ -126,6 +127,16 @@ class Scene:
         if rc:
             raise RuntimeError(self.L.cr_last_error().decode())
         return film, st
+
+    def pt_radiance(self, rays6, max_depth, seed, sample=0):
+        rays6 = np.ascontiguousarray(rays6, np.float32)
+        out = np.zeros((rays6.shape[0], 3), np.float32)
+        st = Stats()
+        rc = self.L.cr_pt_radiance(self.h, fptr(rays6), rays6.shape[0], max_depth, seed, sample, fptr(out),
+                                   C.byref(st))
+        if rc:
+            raise RuntimeError(self.L.cr_last_error().decode())
+        return out, st
 
     def pt(self, W, H, spp, max_depth, seed, mode=0, pix_range=None):
         film = np.zeros((H, W, 3), np.float32)

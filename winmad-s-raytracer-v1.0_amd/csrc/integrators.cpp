@@ -114,6 +114,10 @@ void PathIntegrator::render() {
   for (float& v : film) v = v * inv;
 }
 
+void PathIntegrator::raytracing(const wr_ray* rays, int64_t n, float* rgb, int sample) {
+  ok(wr_path_radiance(ctx_, rays, n, maxTracingDepth, seed, sample, rgb, &stats));
+}
+
 void PathIntegrator::outputImage(const char* filename) {
   ok(wr_film_write_image(film.data(), height, width, 1.f, 2.2f, 0, filename));
 }

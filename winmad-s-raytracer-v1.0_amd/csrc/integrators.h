@@ -73,6 +73,9 @@ class PathIntegrator : public SurfaceIntegrator {
   void init(const char* filename, Parameters& para) override;  // pathIntegrator.cpp:3-15
   void render() override;                                        // surfaceIntegrator.cpp:14-46
   void outputImage(const char* filename) override;               // surfaceIntegrator.cpp:47-50
+  // raytracing(const Ray&, int dep) (pathIntegrator.cpp:29-148) for a batch of
+  // rays; rgb: n * 3 radiance values (dep is unused by the reference)
+  void raytracing(const wr_ray* rays, int64_t n, float* rgb, int sample = 0);
 };
 
 }  // namespace winmad

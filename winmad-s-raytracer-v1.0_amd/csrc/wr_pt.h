@@ -63,6 +63,31 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_gen(PtGroup G_
   if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = P;
 }
 
+// PathIntegrator::raytracing(ray, dep) for caller rays (wr_path_radiance): the
+// path starts from the Ray object as given (o, d; no EPS offset, like the
+// camera ray of k_pt_gen); output p is "pixel" p of an n x 1 film.
+__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_gen_rays(PtGroup G_, const wr_ray* rays) {
+  const PtArgs& A = G_.a[blockIdx.y];
+  const PtBuf& T = A.T;
+  const int P = A.P;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    const wr_ray r = rays[p];
+    const V3 o = v3(r.o[0], r.o[1], r.o[2]), d = v3(r.d[0], r.d[1], r.d[2]);
+    st3(T.o, P, p, o);
+    st3(T.d, P, p, d);
+    st3(T.pw, P, p, v3(1.f, 1.f, 1.f));
+    T.last_pdf[p] = 1.f;
+    T.last_spec[p] = 1;
+    T.len[p] = 1;
+    T.pix[p] = p;
+    T.ctr[p] = 0;
+    st3(T.q_o[0], P, p, o);
+    st3(T.q_d[0], P, p, d);
+    T.q_path[0][p] = p;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = P;
+}
+
 // One PathIntegrator::raytracing iteration (pathIntegrator.cpp:43-146)
 __device__ __forceinline__ void pt_shade_body(const PtArgs& A, int slot, int bid, int nblk) {
   const PtBuf& T = A.T;

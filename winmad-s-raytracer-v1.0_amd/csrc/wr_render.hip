@@ -1320,6 +1320,66 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
   return film_return(c, film, film_on_device, nf);
 }
 
+int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max_depth, uint32_t seed,
+                     int32_t sample, float* rgb, wr_stats* st) {
+  if (!c || ((!rays || !rgb) && n64) || n64 < 0) return fail(WR_E_ARG, "bad argument");
+  if (max_depth < 0 || max_depth > kSlots - 3) return fail(WR_E_ARG, "max_depth must be in 0..61");
+  if (n64 > (1 << 26)) return fail(WR_E_ARG, "at most 2^26 rays per call");
+  if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "path tracing needs at least one area light");
+  if (n64 == 0) return WR_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const double t0 = host_now();
+  const int P = static_cast<int>(n64);
+  if (pipelines_that_fit(c, 2, P, 1, 1) < 1) return WR_E_HIP;
+  Pipe& pp = c->pipes[0];  // the context stream
+  const size_t nf = size_t(P) * 3;
+  std::memset(rgb, 0, nf * sizeof(float));
+  float* dfilm = nullptr;
+  if (int rc = film_target(c, rgb, 0, nf, &dfilm)) return rc;
+  wr_ray* drays = nullptr;
+  HIPCHK(hipMalloc(&drays, size_t(P) * sizeof(wr_ray)));
+  HIPCHK(hipMemcpyAsync(drays, rays, size_t(P) * sizeof(wr_ray), hipMemcpyHostToDevice, pp.stream));
+  begin_render(c, 1, 0);
+  PtGroup GA;
+  PtArgs& A = GA.a[0];
+  A.S = c->ds;
+  A.T = pp.pb[0];
+  A.ctr = pp.ctr;
+  A.sc = pp.sc;
+  A.film = dfilm;
+  A.W = P;
+  A.H = 1;
+  A.P = P;
+  A.spp = 1;
+  A.grid_len = 1;
+  A.max_depth = max_depth;
+  A.seed = seed;
+  A.k = static_cast<uint32_t>(sample);
+  const hipStream_t sm = pp.stream;
+  Timer tm(c, &pp);
+  const int g = shade_grid(c, P);
+  HIPCHK(hipMemsetAsync(pp.sc, 0, sizeof(StepCounters), sm));
+  hipLaunchKernelGGL(k_pt_gen_rays, dim3(g, 1), dim3(kShadeBlock), 0, sm, GA, drays);
+  for (int b = 0; b <= max_depth + 1; ++b) {
+    const bool more = b <= max_depth;
+    const PtBuf& T = pp.pb[0];
+    const PtBuf::Sq& Q = T.sq[b & 1];
+    QueueList ql;
+    ql.add(rq(Q.o, Q.d, P, &pp.sc[0].sq[b], Q.t, Q.prim), P);
+    if (more) ql.add(rq(T.q_o[b & 1], T.q_d[b & 1], P, &pp.sc[0].ext[b], T.q_t[b & 1], T.q_prim[b & 1]), P);
+    trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, false, ql.Q, ql.max_rays);
+    const int nres = shade_grid(c, P);
+    hipLaunchKernelGGL(k_pt_step, dim3(nres + (more ? g : 0), 1), dim3(kShadeBlock), 0, sm, GA, b, nres,
+                       more ? 1 : 0);
+    if (!more) break;
+  }
+  HIPCHK(hipGetLastError());
+  const int rc = finish_render(c, 1, st, t0);
+  (void)hipFree(drays);
+  if (rc) return rc;
+  return film_return(c, rgb, 0, nf);
+}
+
 int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int film_on_device, wr_stats* st) {
   if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
   if (prm->width <= 0 || prm->height <= 0 || prm->spp <= 0) return fail(WR_E_ARG, "bad film size / spp");

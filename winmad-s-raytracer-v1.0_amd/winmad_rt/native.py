@@ -19,7 +19,7 @@ K_TRACE, K_SHADE, K_RESOLVE, K_GEN, K_OTHER = 0, 1, 2, 3, 4
 # every entry point declared in include/winmad_rt.h
 EXPORTS = ["wr_scene_load", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free", "wr_device_count",
            "wr_create", "wr_destroy", "wr_set_pipelines", "wr_trace_closest", "wr_occluded", "wr_render_bdpt", "wr_render_path",
-           "wr_render_vcm",
+           "wr_render_vcm", "wr_path_radiance",
            "wr_film_write_ppm", "wr_film_write_image", "wr_last_error", "wr_api_version"]
 
 
@@ -120,6 +120,8 @@ def lib():
         L.wr_render_bdpt.argtypes = [P, C.POINTER(WrBdptParams), P, I, C.POINTER(WrStats)]
         L.wr_render_path.argtypes = [P, C.POINTER(WrPathParams), P, I, C.POINTER(WrStats)]
         L.wr_render_vcm.argtypes = [P, C.POINTER(WrVcmParams), P, I, C.POINTER(WrStats)]
+        L.wr_path_radiance.argtypes = [P, C.POINTER(WrRay), I64, I, C.c_uint32, I, C.POINTER(C.c_float),
+                                       C.POINTER(WrStats)]
         L.wr_film_write_ppm.argtypes = [C.POINTER(C.c_float), I, I, C.c_float, C.c_float, I, C.c_char_p]
         L.wr_film_write_image.argtypes = [C.POINTER(C.c_float), I, I, C.c_float, C.c_float, I, C.c_char_p]
         L.wr_last_error.restype = C.c_char_p
@@ -242,6 +244,17 @@ class Context:
             film = np.zeros((height, width, 3), np.float32)
         check(lib().wr_render_vcm(self.h, C.byref(p), film.ctypes.data_as(C.c_void_p), 0, C.byref(st)))
         return film, st
+
+    def path_radiance(self, rays8, max_depth=7, seed=5489, sample=0):
+        """PathIntegrator::raytracing for each ray of rays8 ((n, 8) float32:
+        o, d, tmin, tmax; d used as given).  Returns (n, 3) radiance, stats."""
+        rays8 = np.ascontiguousarray(rays8, np.float32)
+        n = rays8.shape[0]
+        out = np.zeros((n, 3), np.float32)
+        st = WrStats()
+        check(lib().wr_path_radiance(self.h, rays8.ctypes.data_as(C.POINTER(WrRay)), n, max_depth, seed, sample,
+                                     out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)))
+        return out, st
 
     def render_path(self, width, height, spp, max_depth=7, seed=5489, sample_begin=0, sample_count=0,
                     time_kernels=0, count_work=0, film=None, film_ptr=None):
