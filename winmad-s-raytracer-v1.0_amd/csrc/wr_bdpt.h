@@ -27,7 +27,7 @@ struct BdptBuf {
   // [slot & 1], so a step's resolve and the next step's vertex shading (which
   // writes [(slot + 1) & 1]) can run in one launch
   struct Sq {
-    float *o, *d, *tgt, *val, *t;
+    float *o, *d, *tgt, *val, *t, *cut;  // cut: occl_cut (-INF for closest-hit DI-BSDF rays)
     int *meta, *pix, *prim;
   } sq[2];
   struct Di {
@@ -237,6 +237,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
       st3(Q.d, B.cap_sq, si, s_d);
       st3(Q.tgt, B.cap_sq, si, S.cam.pos);
       st3(Q.val, B.cap_sq, si, s_val);
+      Q.cut[si] = occl_cut(s_o, S.cam.pos, dot(S.cam.pos - s_o, s_d));
       Q.meta[si] = SQ_SPLAT << 30;
       Q.pix[si] = s_pix;
     }
@@ -449,6 +450,7 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
         st3(Q.o, cap, ni, hp);
         st3(Q.d, cap, ni, nee_d);
         st3(Q.tgt, cap, ni, nee_tgt);
+        Q.cut[ni] = occl_cut(hp, nee_tgt, dot(nee_tgt - hp, nee_d));
         Q.meta[ni] = (SQ_NEE << 30) | p;
         Q.pix[ni] = pix;
       }
@@ -456,6 +458,7 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
       if (dib) {
         st3(Q.o, cap, bi, dib_o);
         st3(Q.d, cap, bi, dib_d);
+        Q.cut[bi] = -WR_INF;  // needs the closest hit (same light?)
         Q.meta[bi] = (SQ_DIB << 30) | p;
         Q.pix[bi] = pix;
       }
@@ -527,6 +530,7 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
           st3(Q.d, cap, si, sdir);
           st3(Q.tgt, cap, si, stgt);
           st3(Q.val, cap, si, sval);
+          Q.cut[si] = occl_cut(hp, stgt, dot(stgt - hp, sdir));
           Q.meta[si] = (SQ_CONN << 30) | p;
           Q.pix[si] = pix;
         }

@@ -16,7 +16,7 @@ struct PtBuf {
   // step's resolve and the next vertex shading (writing [(slot + 1) & 1]) run
   // in one launch
   struct Sq {
-    float *o, *d, *tgt, *val, *t;
+    float *o, *d, *tgt, *val, *t, *cut;  // cut: occl_cut
     int *pix, *prim;
   } sq[2];
 };
@@ -194,6 +194,7 @@ __device__ __forceinline__ void pt_shade_body(const PtArgs& A, int slot, int bid
       st3(Q.d, P, si, s_d);
       st3(Q.tgt, P, si, s_tgt);
       st3(Q.val, P, si, s_val);
+      Q.cut[si] = occl_cut(s_o, s_tgt, dot(s_tgt - s_o, s_d));
       Q.pix[si] = pix;
     }
   }

@@ -160,12 +160,17 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 // C-ABI traversal, before: AoS wr_ray -> SoA queue (occlusion rays re-normalised
 // as Scene::occluded's Ray(p1, dir) does, scene.cpp:74)
 __global__ void __launch_bounds__(256) k_api_prep(const wr_ray* rays, int n, int occ, float* o3, float* d3,
-                                                  float* tmin, float* tmax) {
+                                                  float* tmin, float* tmax, const float* targets, float* cut) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const wr_ray r = rays[i];
+    const V3 o = v3(r.o[0], r.o[1], r.o[2]);
     V3 d = v3(r.d[0], r.d[1], r.d[2]);
-    if (occ) d = normalize(d);
-    st3(o3, n, i, v3(r.o[0], r.o[1], r.o[2]));
+    if (occ) {
+      d = normalize(d);
+      const V3 tg = v3(targets[3 * i], targets[3 * i + 1], targets[3 * i + 2]);
+      cut[i] = occl_cut(o, tg, dot(tg - o, d));
+    }
+    st3(o3, n, i, o);
     st3(d3, n, i, d);
     tmin[i] = r.tmin;
     tmax[i] = r.tmax;
@@ -355,6 +360,7 @@ void layout_bdpt(Arena& a, BdptBuf& B, int P) {
     q.tgt = a.take<float>(3 * sQ);
     q.val = a.take<float>(3 * sQ);
     q.t = a.take<float>(sQ);
+    q.cut = a.take<float>(sQ);
     q.meta = a.take<int>(sQ);
     q.pix = a.take<int>(sQ);
     q.prim = a.take<int>(sQ);
@@ -396,6 +402,7 @@ void layout_pt(Arena& a, PtBuf& T, int P) {
     Q.tgt = a.take<float>(3 * sP);
     Q.val = a.take<float>(3 * sP);
     Q.t = a.take<float>(sP);
+    Q.cut = a.take<float>(sP);
     Q.pix = a.take<int>(sP);
     Q.prim = a.take<int>(sP);
   }
@@ -522,8 +529,8 @@ struct Timer {
 };
 
 RayQueue rq(const float* o3, const float* d3, int cap, const int* cnt, float* t, int* prim,
-            const float* tmin = nullptr, const float* tmax = nullptr) {
-  return RayQueue{o3, d3, cap, cnt, tmin, tmax, t, prim};
+            const float* tmin = nullptr, const float* tmax = nullptr, const float* cut = nullptr) {
+  return RayQueue{o3, d3, cap, cnt, tmin, tmax, t, prim, cut};
 }
 // queues of one launch (empty `count` pointers are skipped)
 struct QueueList {
@@ -1024,7 +1031,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   // one scratch block: rays, SoA queue, results, counters
   char* buf = nullptr;
   const size_t nb = size_t(n);
-  const size_t bytes = nb * (sizeof(wr_ray) + 4 * 13 + sizeof(wr_hit) + 1) + 16 * 256;
+  const size_t bytes = nb * (sizeof(wr_ray) + 4 * 14 + sizeof(wr_hit) + 1) + 16 * 256;
   HIPCHK(hipMalloc(&buf, bytes));
   char* q = buf;
   auto take = [&](size_t sz) { char* r = q; q += (sz + 255) & ~size_t(255); return r; };
@@ -1036,6 +1043,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   float* tt = reinterpret_cast<float*>(take(nb * 4));
   int* pr = reinterpret_cast<int*>(take(nb * 4));
   float* dtg = reinterpret_cast<float*>(take(nb * 12));
+  float* dcut = reinterpret_cast<float*>(take(nb * 4));
   wr_hit* dh = reinterpret_cast<wr_hit*>(take(nb * sizeof(wr_hit)));
   uint8_t* dox = reinterpret_cast<uint8_t*>(take(nb));
   int* cnt = reinterpret_cast<int*>(take(sizeof(int)));
@@ -1043,12 +1051,12 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   if (occ) HIPCHK(hipMemcpyAsync(dtg, targets, nb * 12, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(cnt, &n, sizeof(int), hipMemcpyHostToDevice, c->stream));
   const int g = std::max(1, std::min(c->grid, (n + 255) / 256));
-  hipLaunchKernelGGL(k_api_prep, dim3(g), dim3(256), 0, c->stream, dr, n, occ ? 1 : 0, o3, d3, tmn, tmx);
+  hipLaunchKernelGGL(k_api_prep, dim3(g), dim3(256), 0, c->stream, dr, n, occ ? 1 : 0, o3, d3, tmn, tmx, dtg, dcut);
   c->timing = false;
   Timer tm(c, nullptr);
   HIPCHK(hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream));
   QueueList ql;
-  ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx), n);
+  ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
   trace_launch(c, c->stream, c->ctr, &c->ctr->fetch, tm, false, ql.Q, ql.max_rays);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
@@ -1145,7 +1153,7 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
     }
     auto sq = [&](int m, int slot) {
       const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
-      return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim);
+      return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut);
     };
     auto ext = [&](int m, int slot) {
       const BdptBuf& B = pp.bb[m];
@@ -1266,7 +1274,7 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
     }
     auto sq = [&](int m, int slot) {
       const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
-      return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim);
+      return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut);
     };
     auto ext = [&](int m, int slot) {
       const BdptBuf& B = pp.bb[m];
@@ -1365,7 +1373,7 @@ int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max
     const PtBuf& T = pp.pb[0];
     const PtBuf::Sq& Q = T.sq[b & 1];
     QueueList ql;
-    ql.add(rq(Q.o, Q.d, P, &pp.sc[0].sq[b], Q.t, Q.prim), P);
+    ql.add(rq(Q.o, Q.d, P, &pp.sc[0].sq[b], Q.t, Q.prim, nullptr, nullptr, Q.cut), P);
     if (more) ql.add(rq(T.q_o[b & 1], T.q_d[b & 1], P, &pp.sc[0].ext[b], T.q_t[b & 1], T.q_prim[b & 1]), P);
     trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, false, ql.Q, ql.max_rays);
     const int nres = shade_grid(c, P);
@@ -1437,7 +1445,7 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
       for (int m = 0; m < gn; ++m) {
         const PtBuf& T = pp.pb[m];
         const PtBuf::Sq& Q = T.sq[b & 1];
-        ql.add(rq(Q.o, Q.d, P, &pp.sc[m].sq[b], Q.t, Q.prim), P);
+        ql.add(rq(Q.o, Q.d, P, &pp.sc[m].sq[b], Q.t, Q.prim, nullptr, nullptr, Q.cut), P);
       }
       if (more)
         for (int m = 0; m < gn; ++m) {

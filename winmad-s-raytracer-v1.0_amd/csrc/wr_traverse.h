@@ -173,7 +173,25 @@ struct RayQueue {
   const float* tmax;
   float* out_t;
   int* out_prim;
+  // shadow rays (Scene::occluded, scene.cpp:55-69): a ray may stop as soon as
+  // its best hit is below cut[k] -- see occl_cut.  nullptr / -INF: closest hit
+  const float* cut;
 };
+
+// Scene::occluded(p1, dir, p2) answers "unoccluded" iff the closest hit is
+// missing or its point equals p2 within EPS per component.  Best only
+// decreases during the traversal, so once a hit at t < cut is accepted the
+// closest hit's point lies at least cut's margin short of p2 along the ray --
+// farther than EPS in the ray's largest direction component (>= 1/sqrt(3)),
+// with room for the float error of both points (<= 7 * 2^-24 * M) -- and the
+// answer is "occluded" whatever the rest of the traversal finds.  Exact: the
+// occlusion result equals the full traversal's; only the returned (t, prim)
+// can differ, and nothing else reads them.
+__device__ __forceinline__ float occl_cut(V3 o, V3 tgt, float dist) {
+  const float m = fmaxf(fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(tgt.x))),
+                        fmaxf(fmaxf(fabsf(tgt.y), fabsf(tgt.z)), dist));
+  return dist - 2.f * (WR_EPS + 1e-6f * m);
+}
 
 // The queues of one traversal launch, fetched in order (the shadow / aux queue
 // of an iteration first: its long rays start early and overlap the extension
@@ -363,7 +381,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
   int pb = 0, pe = 0;    // wave-uniform: reserved queue indices [pb, pe)
   bool more = false;     // the lane's ray has nodes left to visit
   V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
-  float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmax = WR_INF, root_tmax = 0.f;
+  float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmax = WR_INF, root_tmax = 0.f, rcut = -WR_INF;
   int best = -1, sp = 0;
   uint32_t node = 0;
   // one level of KDtreeAccelNode descent (:325-358) from inner node `at` (word w)
@@ -442,8 +460,10 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
           const float* tmx = sel([](const RayQueue& x) { return x.tmax; });
           o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
           d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+          const float* cutp = sel([](const RayQueue& x) { return x.cut; });
           const float rtmin = tmn ? tmn[r] : 0.f;
           rtmax = tmx ? tmx[r] : WR_INF;
+          rcut = cutp ? cutp[r] : -WR_INF;
           t_best = WR_INF;
           best = -1;
           sp = 0;
@@ -734,6 +754,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
               }
             }
           }
+          if (t_best < rcut) more = false;  // occlusion settled (occl_cut)
         }
       }
       WR_STAMP(4)

@@ -294,6 +294,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
       st3(Q.d, B.cap_sq, si, s_d);
       st3(Q.tgt, B.cap_sq, si, S.cam.pos);
       st3(Q.val, B.cap_sq, si, s_val);
+      Q.cut[si] = occl_cut(s_o, S.cam.pos, dot(S.cam.pos - s_o, s_d));
       Q.meta[si] = SQ_SPLAT << 30;
       Q.pix[si] = s_pix;
     }
@@ -581,6 +582,7 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
       st3(Q.d, cap, ni, nee_d);
       st3(Q.tgt, cap, ni, nee_tgt);
       st3(Q.val, cap, ni, nee_val);
+      Q.cut[ni] = occl_cut(hp, nee_tgt, dot(nee_tgt - hp, nee_d));
       Q.meta[ni] = (SQ_CONN << 30) | p;
       Q.pix[ni] = pix;
     }
@@ -643,6 +645,7 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
           st3(Q.d, cap, si, sdir);
           st3(Q.tgt, cap, si, stgt);
           st3(Q.val, cap, si, sval);
+          Q.cut[si] = occl_cut(hp, stgt, dot(stgt - hp, sdir));
           Q.meta[si] = (SQ_CONN << 30) | p;
           Q.pix[si] = pix;
         }
