@@ -139,12 +139,12 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 
 // =============================================================== trace kernels
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
-template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
+template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false, bool CUT = false>
 // 4 waves/SIMD (<= 128 VGPRs) to match the LDS-limited 16 waves/CU
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32 k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
   extern __shared__ uint32_t smem[];
   TraceCounters tc{0, 0, 0, 0};
-  trace_queue<COUNT, SPH, NARROW, STAMP>(S, Q, fetch, smem, tc, ctr->stamps);
+  trace_queue<COUNT, SPH, NARROW, STAMP, CUT>(S, Q, fetch, smem, tc, ctr->stamps);
   if (COUNT) {
     unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs),
                        e = wave_sum(tc.tests);
@@ -543,8 +543,19 @@ struct QueueList {
 };
 
 using TraceKernel = void (*)(DevScene, TraceQueues, DevCounters*, int*);
-TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps) {
+// cut: the launch's shadow rays may stop once occlusion is settled (occl_cut).
+// Only PT, VCM and the API use it: BDPT launches carry 3 % shadow rays, and
+// the check costs C2 1.5 % (measured).
+TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, bool cut = false) {
   if (stamps) return narrow ? k_trace<false, false, true, true> : k_trace<false, false, false, true>;
+  if (cut) {
+    if (count) {
+      if (spheres) return narrow ? k_trace<true, true, true, false, true> : k_trace<true, true, false, false, true>;
+      return narrow ? k_trace<true, false, true, false, true> : k_trace<true, false, false, false, true>;
+    }
+    if (spheres) return narrow ? k_trace<false, true, true, false, true> : k_trace<false, true, false, false, true>;
+    return narrow ? k_trace<false, false, true, false, true> : k_trace<false, false, false, false, true>;
+  }
   if (count) {
     if (spheres) return narrow ? k_trace<true, true, true> : k_trace<true, true, false>;
     return narrow ? k_trace<true, false, true> : k_trace<true, false, false>;
@@ -556,7 +567,7 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps) {
 // One persistent traversal launch over qa then qb (max_rays bounds the grid).
 // `fetch` must be zero (the iteration's counter memset, or the caller).
 int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, int* fetch, Timer& tm, bool count,
-                 const TraceQueues& Q, int max_rays) {
+                 const TraceQueues& Q, int max_rays, bool cut = false) {
   const size_t lds = trace_lds_bytes(c->ds.max_stack, c->narrow);
   const int grid = std::max(1, std::min(c->trace_blocks, (max_rays + kTraceBlock - 1) / kTraceBlock));
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -565,7 +576,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, int* fetch
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, stream);
   }
-  hipLaunchKernelGGL(trace_kernel(count, c->spheres, c->narrow, c->stamps), dim3(grid), dim3(kTraceBlock), lds,
+  hipLaunchKernelGGL(trace_kernel(count, c->spheres, c->narrow, c->stamps, cut), dim3(grid), dim3(kTraceBlock), lds,
                      stream, c->ds, Q, ctr, fetch);
   tm.mark(WR_K_TRACE);
   if (c->trace_log) {
@@ -1057,7 +1068,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   HIPCHK(hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream));
   QueueList ql;
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
-  trace_launch(c, c->stream, c->ctr, &c->ctr->fetch, tm, false, ql.Q, ql.max_rays);
+  trace_launch(c, c->stream, c->ctr, &c->ctr->fetch, tm, false, ql.Q, ql.max_rays, occ != nullptr);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
   HIPCHK(hipGetLastError());
@@ -1314,7 +1325,7 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
       for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), sq_max);
       if (more)
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays, true);
       const int nres = shade_grid(c, sq_max);
       // + the merge queries of the previous step (none before the first)
       const int nsh = more ? g : 0, nmg = b > 0 ? g : 0;
@@ -1375,7 +1386,7 @@ int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max
     QueueList ql;
     ql.add(rq(Q.o, Q.d, P, &pp.sc[0].sq[b], Q.t, Q.prim, nullptr, nullptr, Q.cut), P);
     if (more) ql.add(rq(T.q_o[b & 1], T.q_d[b & 1], P, &pp.sc[0].ext[b], T.q_t[b & 1], T.q_prim[b & 1]), P);
-    trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, false, ql.Q, ql.max_rays);
+    trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, false, ql.Q, ql.max_rays, true);
     const int nres = shade_grid(c, P);
     hipLaunchKernelGGL(k_pt_step, dim3(nres + (more ? g : 0), 1), dim3(kShadeBlock), 0, sm, GA, b, nres,
                        more ? 1 : 0);
@@ -1452,7 +1463,7 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
           const PtBuf& T = pp.pb[m];
           ql.add(rq(T.q_o[q], T.q_d[q], P, &pp.sc[m].ext[b], T.q_t[q], T.q_prim[q]), P);
         }
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays, true);
       // resolve this step's shadow rays and shade its vertices in one launch
       const int nres = shade_grid(c, P);
       hipLaunchKernelGGL(k_pt_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, b, nres,

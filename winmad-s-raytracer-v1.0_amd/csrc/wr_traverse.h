@@ -323,7 +323,7 @@ __device__ __forceinline__ uint64_t stamp_now() {
   return t;
 }
 
-template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false>
+template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false, bool CUT = false>
 __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues& Q, int* fetch,
                                             uint32_t* lds, TraceCounters& ctr,
                                             unsigned long long* stamps = nullptr) {
@@ -460,10 +460,12 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
           const float* tmx = sel([](const RayQueue& x) { return x.tmax; });
           o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
           d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
-          const float* cutp = sel([](const RayQueue& x) { return x.cut; });
           const float rtmin = tmn ? tmn[r] : 0.f;
           rtmax = tmx ? tmx[r] : WR_INF;
-          rcut = cutp ? cutp[r] : -WR_INF;
+          if constexpr (CUT) {
+            const float* cutp = sel([](const RayQueue& x) { return x.cut; });
+            rcut = cutp ? cutp[r] : -WR_INF;
+          }
           t_best = WR_INF;
           best = -1;
           sp = 0;
@@ -754,7 +756,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
               }
             }
           }
-          if (t_best < rcut) more = false;  // occlusion settled (occl_cut)
+          if (CUT && t_best < rcut) more = false;  // occlusion settled (occl_cut)
         }
       }
       WR_STAMP(4)
