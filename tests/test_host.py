@@ -184,3 +184,38 @@ def test_image_writer_formats(tmp_path):
         native.write_image(film, tmp_path / "a.jpg")
     with pytest.raises(native.WrError):
         native.write_image(film, tmp_path / "t.ppm", transpose=True)  # non-square
+
+
+def test_occlusion_cutoff_margin_holds_in_float32():
+    """occl_cut (wr_traverse.h): a shadow ray may stop once its best hit t is
+    below cut = proj - 2 (EPS + 1e-6 M); then the hit point o + d t must differ
+    from the target by more than EPS in some component (Scene::occluded's
+    position test, vector.cpp:43-47), whatever t in [0, cut) the traversal
+    ends with.  Checked in float32 (same operations, no FMA) at the extreme
+    t just below cut, for targets on and off the ray and scene scales from
+    1e-2 to 1e4."""
+    rng = np.random.default_rng(12)
+    f = np.float32
+    EPS = f(1e-3)
+    bad = 0
+    for scale in (1e-2, 1.0, 30.0, 1e3, 1e4):
+        n = 20000
+        o = (rng.uniform(-1, 1, (n, 3)) * scale).astype(f)
+        tgt = (rng.uniform(-1, 1, (n, 3)) * scale).astype(f)
+        off = rng.random(n) < 0.5  # half: target off the ray direction a little
+        v = (tgt - o).astype(f)
+        l = np.sqrt((v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1] + v[:, 2] * v[:, 2]).astype(f)).astype(f)
+        d = (v / l[:, None]).astype(f)
+        jitter = (rng.normal(size=(n, 3)) * 0.01 * scale).astype(f)
+        tgt = np.where(off[:, None], (tgt + jitter).astype(f), tgt)
+        w = (tgt - o).astype(f)
+        proj = ((w[:, 0] * d[:, 0] + w[:, 1] * d[:, 1]).astype(f) + (w[:, 2] * d[:, 2]).astype(f)).astype(f)
+        m = np.max(np.abs(np.concatenate([o, tgt, proj[:, None]], 1)), axis=1).astype(f)
+        cut = (proj - f(2) * (EPS + f(1e-6) * m)).astype(f)
+        ok = cut > 0
+        t = np.nextafter(cut, f(-np.inf)).astype(f)
+        p = (o + (d * t[:, None]).astype(f)).astype(f)
+        diff = (p - tgt).astype(f)
+        equal = np.all((diff >= -EPS) & (diff <= EPS), axis=1)
+        bad += int(np.sum(equal & ok))
+    assert bad == 0
