@@ -238,6 +238,9 @@ constexpr int kLeavesPerRound = WR_LEAVES_PER_ROUND;
 #endif
 constexpr int kRayGrab = WR_RAY_GRAB;  // queue indices a wave reserves per atomic (>= 64)  // leaves a lane may collect per round
 constexpr int kLeavesWait = WR_LEAVES_WAIT;           // the walk runs until every lane has this many
+// leaf ids lane * kLeavesPerRound + i are stored in the byte-wide owner table
+static_assert(64 * kLeavesPerRound <= 256, "owner table holds leaf ids in bytes: kLeavesPerRound <= 4");
+static_assert(kLeavesWait >= 1 && kLeavesWait <= kLeavesPerRound, "kLeavesWait in 1..kLeavesPerRound");
 // Per-ray mailbox of recently tested primitives (direct-mapped by prim id):
 // a (ray, primitive) pair tested before -- the KD build duplicates straddling
 // triangles into every leaf they touch (torus: 2.88 refs per triangle) -- is
