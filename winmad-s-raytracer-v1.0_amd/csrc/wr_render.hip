@@ -140,8 +140,19 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 // =============================================================== trace kernels
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
 template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false, bool CUT = false>
-// 4 waves/SIMD (<= 128 VGPRs) to match the LDS-limited 16 waves/CU
-__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32 k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
+// Register budget: 4 waves/SIMD (<= 128 VGPRs) matches the LDS-limited 16
+// waves/CU and fills the register file.  The CUT instances (PT, VCM camera
+// pass, API occlusion) are held to <= 96 VGPRs, leaving 128 per SIMD for a wave
+// of the shading kernel of another pipeline beside the traversal: C3 2,538 ->
+// 2,626 Mrays/s.  BDPT keeps 128 (at 96: C2 -0.8 %).
+#ifndef WR_TRACE_WAVES_PER_EU
+#define WR_TRACE_WAVES_PER_EU 4
+#endif
+#ifndef WR_TRACE_CUT_WAVES_PER_EU
+#define WR_TRACE_CUT_WAVES_PER_EU 5
+#endif
+__global__ void __launch_bounds__(kTraceBlock)
+__attribute__((amdgpu_waves_per_eu(CUT ? WR_TRACE_CUT_WAVES_PER_EU : WR_TRACE_WAVES_PER_EU, 8))) WR_NO_PK_FP32 k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
   extern __shared__ uint32_t smem[];
   TraceCounters tc{0, 0, 0, 0};
   trace_queue<COUNT, SPH, NARROW, STAMP, CUT>(S, Q, fetch, smem, tc, ctr->stamps);
@@ -1007,7 +1018,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
 }
 
 int wr_set_pipelines(wr_context* c, int n) {
-  if (!c || n < 1 || n > kMaxPipes) return fail(WR_E_ARG, "pipelines must be in 1..8");
+  if (!c || n < 1 || n > kMaxPipes) return fail(WR_E_ARG, "pipelines must be in 1..16");
   c->npipes = n;
   return WR_OK;
 }
