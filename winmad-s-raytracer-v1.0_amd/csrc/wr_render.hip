@@ -139,23 +139,24 @@ __device__ __forceinline__ int pix_index(int h, int w, int H, int W) {
 
 // =============================================================== trace kernels
 // Generic persistent queue traversal: rays [3][cap] SoA, count on device.
-template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false, bool CUT = false>
+template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false, bool CUT = false, bool DENSE = false>
 // Register budget: 4 waves/SIMD (<= 128 VGPRs) matches the LDS-limited 16
-// waves/CU and fills the register file.  The CUT instances (PT, VCM camera
-// pass, API occlusion) are held to <= 96 VGPRs, leaving 128 per SIMD for a wave
-// of the shading kernel of another pipeline beside the traversal: C3 2,538 ->
-// 2,626 Mrays/s.  BDPT keeps 128 (at 96: C2 -0.8 %).
+// waves/CU and fills the register file (BDPT at 96: C2 -0.8 %; the VCM camera
+// pass, CUT, at 96: -1 %).  DENSE (PT): <= 96 VGPRs and no ray records in LDS
+// -> 20 waves/CU on torus-sized trees.  C3 2,538 (4 waves) -> 2,620 (96 VGPRs,
+// a shading wave of another pipeline fits beside the traversal) -> 2,697
+// Mrays/s (DENSE); on BDPT DENSE loses (C2 -1 %), on VCM too (-1.3 %).
 #ifndef WR_TRACE_WAVES_PER_EU
 #define WR_TRACE_WAVES_PER_EU 4
 #endif
 #ifndef WR_TRACE_CUT_WAVES_PER_EU
-#define WR_TRACE_CUT_WAVES_PER_EU 5
+#define WR_TRACE_CUT_WAVES_PER_EU 4
 #endif
 __global__ void __launch_bounds__(kTraceBlock)
-__attribute__((amdgpu_waves_per_eu(CUT ? WR_TRACE_CUT_WAVES_PER_EU : WR_TRACE_WAVES_PER_EU, 8))) WR_NO_PK_FP32 k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
+__attribute__((amdgpu_waves_per_eu(DENSE ? 5 : (CUT ? WR_TRACE_CUT_WAVES_PER_EU : WR_TRACE_WAVES_PER_EU), 8))) WR_NO_PK_FP32 k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
   extern __shared__ uint32_t smem[];
   TraceCounters tc{0, 0, 0, 0};
-  trace_queue<COUNT, SPH, NARROW, STAMP, CUT>(S, Q, fetch, smem, tc, ctr->stamps);
+  trace_queue<COUNT, SPH, NARROW, STAMP, CUT, DENSE>(S, Q, fetch, smem, tc, ctr->stamps);
   if (COUNT) {
     unsigned long long a = wave_sum(tc.inner), b = wave_sum(tc.leaves), c = wave_sum(tc.refs),
                        e = wave_sum(tc.tests);
@@ -317,7 +318,8 @@ struct wr_context {
   bool narrow = false;  // <= 65536 nodes, leaves <= 255 refs: 16-bit stack / pair offsets
   bool trace_log = false;  // WR_TRACE_LOG=1: per-launch ray counts and durations
   bool stamps = false;  // WR_TRACE_STAMPS=1: diagnostic traversal with phase stamps
-  int trace_blocks = 4096;  // resident one-wave workgroups of the traversal
+  int trace_blocks = 4096;        // resident one-wave workgroups of the traversal
+  int trace_blocks_dense = 4096;  // the same for the TRACE_DENSE layout
   bool timing = false;
 };
 
@@ -556,10 +558,23 @@ struct QueueList {
 using TraceKernel = void (*)(DevScene, TraceQueues, DevCounters*, int*);
 // cut: the launch's shadow rays may stop once occlusion is settled (occl_cut).
 // Only PT, VCM and the API use it: BDPT launches carry 3 % shadow rays, and
-// the check costs C2 1.5 % (measured).
-TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, bool cut = false) {
+// the check costs C2 1.5 % (measured).  TRACE_DENSE: cut + the 20-waves/CU
+// layout (PT).
+enum TraceMode { TRACE_PLAIN = 0, TRACE_CUT = 1, TRACE_DENSE = 2 };
+#ifndef WR_VCM_TRACE_MODE
+#define WR_VCM_TRACE_MODE TRACE_CUT  // camera pass of VCM (TRACE_DENSE: -1.3 %)
+#endif
+TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, int mode = TRACE_PLAIN) {
   if (stamps) return narrow ? k_trace<false, false, true, true> : k_trace<false, false, false, true>;
-  if (cut) {
+  if (mode == TRACE_DENSE) {
+    if (count) {
+      if (spheres) return narrow ? k_trace<true, true, true, false, true, true> : k_trace<true, true, false, false, true, true>;
+      return narrow ? k_trace<true, false, true, false, true, true> : k_trace<true, false, false, false, true, true>;
+    }
+    if (spheres) return narrow ? k_trace<false, true, true, false, true, true> : k_trace<false, true, false, false, true, true>;
+    return narrow ? k_trace<false, false, true, false, true, true> : k_trace<false, false, false, false, true, true>;
+  }
+  if (mode == TRACE_CUT) {
     if (count) {
       if (spheres) return narrow ? k_trace<true, true, true, false, true> : k_trace<true, true, false, false, true>;
       return narrow ? k_trace<true, false, true, false, true> : k_trace<true, false, false, false, true>;
@@ -578,16 +593,18 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, boo
 // One persistent traversal launch over qa then qb (max_rays bounds the grid).
 // `fetch` must be zero (the iteration's counter memset, or the caller).
 int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, int* fetch, Timer& tm, bool count,
-                 const TraceQueues& Q, int max_rays, bool cut = false) {
-  const size_t lds = trace_lds_bytes(c->ds.max_stack, c->narrow);
-  const int grid = std::max(1, std::min(c->trace_blocks, (max_rays + kTraceBlock - 1) / kTraceBlock));
+                 const TraceQueues& Q, int max_rays, int mode = TRACE_PLAIN) {
+  const bool dense = mode == TRACE_DENSE && !c->stamps;
+  const size_t lds = trace_lds_bytes(c->ds.max_stack, c->narrow, dense);
+  const int grid =
+      std::max(1, std::min(dense ? c->trace_blocks_dense : c->trace_blocks, (max_rays + kTraceBlock - 1) / kTraceBlock));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->trace_log) {  // diagnostic (WR_TRACE_LOG=1): rays and duration of every launch
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, stream);
   }
-  hipLaunchKernelGGL(trace_kernel(count, c->spheres, c->narrow, c->stamps, cut), dim3(grid), dim3(kTraceBlock), lds,
+  hipLaunchKernelGGL(trace_kernel(count, c->spheres, c->narrow, c->stamps, mode), dim3(grid), dim3(kTraceBlock), lds,
                      stream, c->ds, Q, ctr, fetch);
   tm.mark(WR_K_TRACE);
   if (c->trace_log) {
@@ -1001,17 +1018,21 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     c->narrow = nn <= 65536 && static_cast<int64_t>(max_leaf) * 64 * kLeavesPerRound < 65536;
     // test knob: WR_TRACE_WIDE=1 runs the 32-bit-stack variant on any tree
     if (const char* e = std::getenv("WR_TRACE_WIDE")) c->narrow = c->narrow && std::atoi(e) == 0;
-    const size_t lds = trace_lds_bytes(d.max_stack, c->narrow);
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel(false, c->spheres, c->narrow, false),
-                                                     kTraceBlock, lds) != hipSuccess ||
-        per_cu <= 0)
-      per_cu = 8;
+    auto resident = [&](int mode) {
+      const size_t lds = trace_lds_bytes(d.max_stack, c->narrow, mode == TRACE_DENSE);
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel(false, c->spheres, c->narrow, false, mode),
+                                                       kTraceBlock, lds) != hipSuccess ||
+          per_cu <= 0)
+        per_cu = 8;
+      // diagnostic: WR_TRACE_WAVES_PER_CU caps the resident traversal waves
+      // (leaving room for the other pipelines' shading kernels)
+      if (const char* e = std::getenv("WR_TRACE_WAVES_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
+      return per_cu;
+    };
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    // diagnostic: WR_TRACE_WAVES_PER_CU caps the resident traversal waves (leaving
-    // room for the other pipelines' shading kernels)
-    if (const char* e = std::getenv("WR_TRACE_WAVES_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
-    c->trace_blocks = c->cus * per_cu;
+    c->trace_blocks = c->cus * resident(TRACE_PLAIN);
+    c->trace_blocks_dense = c->cus * resident(TRACE_DENSE);
   }
   *out = c;
   return WR_OK;
@@ -1079,7 +1100,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   HIPCHK(hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream));
   QueueList ql;
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
-  trace_launch(c, c->stream, c->ctr, &c->ctr->fetch, tm, false, ql.Q, ql.max_rays, occ != nullptr);
+  trace_launch(c, c->stream, c->ctr, &c->ctr->fetch, tm, false, ql.Q, ql.max_rays, occ != nullptr ? TRACE_CUT : TRACE_PLAIN);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
   HIPCHK(hipGetLastError());
@@ -1336,7 +1357,7 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
       for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), sq_max);
       if (more)
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays, true);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays, WR_VCM_TRACE_MODE);
       const int nres = shade_grid(c, sq_max);
       // + the merge queries of the previous step (none before the first)
       const int nsh = more ? g : 0, nmg = b > 0 ? g : 0;
@@ -1397,7 +1418,7 @@ int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max
     QueueList ql;
     ql.add(rq(Q.o, Q.d, P, &pp.sc[0].sq[b], Q.t, Q.prim, nullptr, nullptr, Q.cut), P);
     if (more) ql.add(rq(T.q_o[b & 1], T.q_d[b & 1], P, &pp.sc[0].ext[b], T.q_t[b & 1], T.q_prim[b & 1]), P);
-    trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, false, ql.Q, ql.max_rays, true);
+    trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, false, ql.Q, ql.max_rays, TRACE_DENSE);
     const int nres = shade_grid(c, P);
     hipLaunchKernelGGL(k_pt_step, dim3(nres + (more ? g : 0), 1), dim3(kShadeBlock), 0, sm, GA, b, nres,
                        more ? 1 : 0);
@@ -1474,7 +1495,7 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
           const PtBuf& T = pp.pb[m];
           ql.add(rq(T.q_o[q], T.q_d[q], P, &pp.sc[m].ext[b], T.q_t[q], T.q_prim[q]), P);
         }
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays, true);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays, TRACE_DENSE);
       // resolve this step's shadow rays and shade its vertices in one launch
       const int nres = shade_grid(c, P);
       hipLaunchKernelGGL(k_pt_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, b, nres,

@@ -259,10 +259,18 @@ static_assert(kLeavesWait >= 1 && kLeavesWait <= kLeavesPerRound, "kLeavesWait i
 #endif
 constexpr int kMail = WR_MAILBOX;
 static_assert((kMail & (kMail - 1)) == 0, "mailbox size: power of two");
-__host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow) {
+// Where a pair's test reads its ray.  Default: the owner's 8-float record and
+// best, kept in LDS (2.3 KB per wave).  DENSE: ds_bpermute from the owner
+// lane's registers -- no LDS storage, so a torus wave fits the 8 KB of 20
+// waves/CU (with <= 96 VGPRs) at the price of 9 permutes per pair.
+__host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow, bool dense = false) {
   return size_t(depth) * 64 * (narrow ? 6 : 8) +
-         size_t(4) * (8 * 64 + 64 + kLeavesPerRound * 64 + kLeavesPerRound * (narrow ? 32 : 64) + kPairBatch / 4 +
-                      4 * 64 + 16 + kMail * 64 + (kMail > 0 ? kPairBatch / 2 : 0));
+         size_t(4) * ((dense ? 0 : 8 * 64 + 64) + kLeavesPerRound * 64 + kLeavesPerRound * (narrow ? 32 : 64) +
+                      kPairBatch / 4 + 4 * 64 + 16 + kMail * 64 + (kMail > 0 ? kPairBatch / 2 : 0));
+}
+// value of v in lane `src` (all lanes of the wave active)
+__device__ __forceinline__ float lane_get(float v, int src) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
 }
 
 // Persistent closest-hit traversal over the ray queues of one launch (one wave
@@ -326,7 +334,7 @@ __device__ __forceinline__ uint64_t stamp_now() {
   return t;
 }
 
-template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false, bool CUT = false>
+template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false, bool CUT = false, bool DENSE = false>
 __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues& Q, int* fetch,
                                             uint32_t* lds, TraceCounters& ctr,
                                             unsigned long long* stamps = nullptr) {
@@ -348,8 +356,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
   // (tmax = t), so entry k's tmax is entry k-1's tmin and entry 0's is the
   // root-box tmax -- exactly the floats the reference's todo[] would hold.
   float4* ray4 = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds) + size_t(depth) * 64 * (NARROW ? 6 : 8));
-  float* rbest = reinterpret_cast<float*>(ray4 + 2 * 64);  // [64]
-  uint32_t* leaf_first = reinterpret_cast<uint32_t*>(rbest + 64);  // [64 * kLeavesPerRound]
+  float* rbest = reinterpret_cast<float*>(ray4 + (DENSE ? 0 : 2 * 64));  // [64]
+  uint32_t* leaf_first = reinterpret_cast<uint32_t*>(rbest + (DENSE ? 0 : 64));  // [64 * kLeavesPerRound]
   // first pair of each leaf in the round's numbering (lane-local during the walk)
   using PairIdx = typename std::conditional<NARROW, uint16_t, uint32_t>::type;
   PairIdx* leaf_off = reinterpret_cast<PairIdx*>(leaf_first + kLeavesPerRound * 64);  // [64 * kLeavesPerRound]
@@ -385,6 +393,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
   bool more = false;     // the lane's ray has nodes left to visit
   V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
   float tmin = 0.f, tmax = 0.f, t_best = WR_INF, rtmax = WR_INF, root_tmax = 0.f, rcut = -WR_INF;
+  float rtmin_v = 0.f, screen0 = WR_INF;  // the ray's tmin; its best at round start
   int best = -1, sp = 0;
   uint32_t node = 0;
   // one level of KDtreeAccelNode descent (:325-358) from inner node `at` (word w)
@@ -464,6 +473,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
           o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
           d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
           const float rtmin = tmn ? tmn[r] : 0.f;
+          rtmin_v = rtmin;
           rtmax = tmx ? tmx[r] : WR_INF;
           if constexpr (CUT) {
             const float* cutp = sel([](const RayQueue& x) { return x.cut; });
@@ -483,8 +493,10 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
             more = false;
           } else {
             inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-            ray4[2 * lane] = make_float4(o.x, o.y, o.z, d.x);
-            ray4[2 * lane + 1] = make_float4(d.y, d.z, rtmin, rtmax);
+            if constexpr (!DENSE) {
+              ray4[2 * lane] = make_float4(o.x, o.y, o.z, d.x);
+              ray4[2 * lane + 1] = make_float4(d.y, d.z, rtmin, rtmax);
+            }
 #pragma unroll
             for (int k = 0; k < kMail; ++k) mail[lane * kMail + k] = 0;
           }
@@ -574,7 +586,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
 #pragma unroll
     for (int i = 0; i < kLeavesPerRound; ++i)  // nl <= kLeavesPerRound
       if (i < nl) leaf_off[lane * kLeavesPerRound + i] += static_cast<PairIdx>(excl);
-    rbest[lane] = t_best;
+    if constexpr (!DENSE) rbest[lane] = t_best;
+    screen0 = t_best;
     // ref of pair k of the round, k in this lane's range [excl, excl + count)
     auto own_ref = [&](int k) -> uint32_t {
       int i = 0;
@@ -695,14 +708,27 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
           ra[u] = S.ref_a[ref[u]];
           rb[u] = S.ref_b[ref[u]];
         }
+        // the owners' rays (converged wave: every source lane is active)
+        float4 gx[kPairsInFlight], gy[kPairsInFlight];
+        float gs[kPairsInFlight];
+        if constexpr (DENSE) {
+#pragma unroll
+          for (int u = 0; u < kPairsInFlight; ++u) {
+            const int L = owner[u];
+            gx[u] = make_float4(lane_get(o.x, L), lane_get(o.y, L), lane_get(o.z, L), lane_get(d.x, L));
+            gy[u] = make_float4(lane_get(d.y, L), lane_get(d.z, L), lane_get(rtmin_v, L), lane_get(rtmax, L));
+            gs[u] = lane_get(screen0, L);
+          }
+        }
 #pragma unroll
         for (int u = 0; u < kPairsInFlight; ++u) {
           if (c0 + 64 * u >= nk) break;
           if (COUNT) ++ctr.tests;
           const int L = owner[u];
-          const float4 x = ray4[2 * L], y = ray4[2 * L + 1];
+          const float4 x = DENSE ? gx[u] : ray4[2 * L], y = DENSE ? gy[u] : ray4[2 * L + 1];
+          const float scr = DENSE ? gs[u] : rbest[L];
           const int prim = __float_as_int(rc[u].y);
-          const float t = pair_t(ra[u], rb[u], rc[u], v3(x.x, x.y, x.z), v3(x.w, y.x, y.y), y.z, y.w, rbest[L]);
+          const float t = pair_t(ra[u], rb[u], rc[u], v3(x.x, x.y, x.z), v3(x.w, y.x, y.y), y.z, y.w, scr);
           if (t == t) {  // t > EPS > 0: the order key is the float's bits
             const unsigned long long key = static_cast<uint32_t>(__float_as_int(t));
             const unsigned long long pr = static_cast<uint32_t>((!SPH || prim >= 0) ? prim : -prim - 1);
@@ -746,8 +772,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
             best = pmin;
           }
           if (!decided) {
-            const float screen = rbest[lane];
-            const float rtmin = ray4[2 * lane + 1].z;
+            const float screen = DENSE ? screen0 : rbest[lane];
+            const float rtmin = DENSE ? rtmin_v : ray4[2 * lane + 1].z;
             for (int k = k0; k < k1; ++k) {
               const uint32_t ref = own_ref(k);
               const float2 c = S.ref_c[ref];
