@@ -44,7 +44,20 @@ def normalize_f32(d):
                                         ("cbox64x48", lambda: _scenes.cbox(64, 48)),
                                         ("spheres64", lambda: _scenes.spheres(64, 64))])
 def test_trace_closest_bit_exact_vs_reference(name, maker):
-    c = ctx(maker())
+    _check_golden_corpus(ctx(maker()), name)
+
+
+@pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),
+                                        ("cbox64x48", lambda: _scenes.cbox(64, 48)),
+                                        ("spheres64", lambda: _scenes.spheres(64, 64))])
+def test_trace_dense_variant_bit_exact_vs_reference(name, maker, monkeypatch):
+    """TRACE_DENSE (PT's launches: owner rays by ds_bpermute, 20 waves/CU),
+    forced on the API: the reference's corpus, closest hits and occlusion."""
+    monkeypatch.setenv("WR_TRACE_DENSE", "1")
+    _check_golden_corpus(native.Context(native.Scene(maker()), 0), name)
+
+
+def _check_golden_corpus(c, name):
     rays = np.fromfile(os.path.join(GOLD, f"rays_{name}.f32"), np.float32).reshape(-1, 9)
     ref = parse_rays(os.path.join(GOLD, f"rays_{name}.txt"))
     r8 = native.rays_from_arrays(rays[:, 0:3], normalize_f32(rays[:, 3:6]))  # Ray ctor normalises
@@ -231,7 +244,7 @@ def test_trace_wide_stack_variant_bit_exact(monkeypatch):
     assert _check_trace_vs_oracle(c, _oracle.Scene(path), rays) > 500
 
 
-def test_trace_1m_triangle_scene_matches_oracle(tmp_path):
+def test_trace_1m_triangle_scene_matches_oracle(tmp_path, monkeypatch):
     """C4 scene (1,005,486 prims, 292,937 nodes: the wide-stack variant, depth 18)."""
     from winmad_rt import scenes
     obj = str(tmp_path / "torus_1m.obj")
@@ -246,7 +259,36 @@ def test_trace_1m_triangle_scene_matches_oracle(tmp_path):
     d = rng.normal(size=(n, 3))
     rays = np.zeros((n, 9), np.float32)
     rays[:, 0:3], rays[:, 3:6] = o, d
-    assert _check_trace_vs_oracle(c, _oracle.Scene(path), rays) > n // 4
+    orc = _oracle.Scene(path)
+    assert _check_trace_vs_oracle(c, orc, rays) > n // 4
+    monkeypatch.setenv("WR_TRACE_DENSE", "1")  # wide stack + TRACE_DENSE
+    assert _check_trace_vs_oracle(native.Context(s, 0), orc, rays) > n // 4
+
+
+def test_trace_large_batch_matches_oracle_and_small_batches():
+    """4M rays in one wr_trace_closest call (grid-stride refill, queue
+    reservations across many waves): a random sample of 4,096 equals the
+    oracle bit for bit and the same rays traced as a small batch."""
+    path = _scenes.torus(64, 64)
+    c = ctx(path)
+    rng = np.random.default_rng(5)
+    n = 1 << 22
+    o = rng.uniform([-250, -150, -120], [280, 350, 90], size=(n, 3)).astype(np.float32)
+    draw = rng.normal(size=(n, 3)).astype(np.float32)
+    d = normalize_f32(draw)  # as the Ray constructor the oracle runs
+    big = c.trace_closest(native.rays_from_arrays(o, d))
+    idx = np.sort(rng.choice(n, 4096, replace=False))
+    rays = np.zeros((idx.size, 9), np.float32)
+    rays[:, 0:3], rays[:, 3:6] = o[idx], draw[idx]
+    oi, of, _, _ = _oracle.Scene(path).trace(rays)
+    assert np.array_equal(big["prim"][idx], oi[:, 0])
+    m = oi[:, 0] >= 0
+    assert m.sum() > 500
+    got = np.concatenate([big["t"][idx][:, None], big["p"][idx], big["n"][idx]], axis=1).astype(np.float32)
+    assert np.array_equal(got[m], of[m])
+    small = c.trace_closest(native.rays_from_arrays(o[idx], d[idx]))
+    for k in ("prim", "t", "p", "n", "inside", "mat_id"):
+        assert np.array_equal(small[k], big[k][idx]), k
 
 
 @pytest.mark.parametrize("pipes", [1, 3, 8])

@@ -320,6 +320,7 @@ struct wr_context {
   bool stamps = false;  // WR_TRACE_STAMPS=1: diagnostic traversal with phase stamps
   int trace_blocks = 4096;        // resident one-wave workgroups of the traversal
   int trace_blocks_dense = 4096;  // the same for the TRACE_DENSE layout
+  bool api_dense = false;         // test knob WR_TRACE_DENSE=1: API launches in TRACE_DENSE
   bool timing = false;
 };
 
@@ -1006,6 +1007,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   for (const auto& p : s.prims) c->spheres |= p.type != wr::kTri;
   if (const char* e = std::getenv("WR_TRACE_STAMPS")) c->stamps = std::atoi(e) != 0 && !c->spheres;
   if (const char* e = std::getenv("WR_TRACE_LOG")) c->trace_log = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WR_TRACE_DENSE")) c->api_dense = std::atoi(e) != 0;
   if (const char* e = std::getenv("WR_VCM_CELL")) c->vcm_cell = std::min(8.f, std::max(0.25f, (float)std::atof(e)));
   {
     // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
@@ -1100,7 +1102,8 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   HIPCHK(hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream));
   QueueList ql;
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
-  trace_launch(c, c->stream, c->ctr, &c->ctr->fetch, tm, false, ql.Q, ql.max_rays, occ != nullptr ? TRACE_CUT : TRACE_PLAIN);
+  trace_launch(c, c->stream, c->ctr, &c->ctr->fetch, tm, false, ql.Q, ql.max_rays,
+               c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN));
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
   HIPCHK(hipGetLastError());
