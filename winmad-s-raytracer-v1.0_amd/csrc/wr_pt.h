@@ -227,7 +227,14 @@ __device__ __forceinline__ void pt_resolve_body(const PtArgs& A, int slot, int b
 // One PT step after its traversal: resolve the step's shadow rays (blocks
 // [0, nres)) and shade its vertices (the rest, `shade` = 0 after the last
 // bounce) -- they read and write different shadow-queue buffers.
-__global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_step(PtGroup G_, int slot, int nres, int shade) {
+// Register budget left to the compiler (106 VGPRs, 4 waves/SIMD).  Forcing more
+// waves spills and loses: C3 2,738 (free) vs 2,763 (5, within noise), 2,617 (6),
+// 2,603 (8) Mrays/s.
+#ifndef WR_PT_WAVES
+#define WR_PT_WAVES 1
+#endif
+__global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WR_PT_WAVES, 8))) WR_NO_PK_FP32
+k_pt_step(PtGroup G_, int slot, int nres, int shade) {
   const PtArgs& A = G_.a[blockIdx.y];
   if (static_cast<int>(blockIdx.x) < nres) pt_resolve_body(A, slot, blockIdx.x, nres);
   else if (shade) pt_shade_body(A, slot, blockIdx.x - nres, gridDim.x - nres);
