@@ -2331,19 +2331,28 @@ static c3 pt_trace(const cr_scene* s, rng_t* rng, ray_t r, int max_depth, cr_sta
     return res;
 }
 
-int cr_render_pt(const cr_scene* s, int W, int H, int spp, int max_depth, uint32_t seed, int rng_mode,
-                 int64_t pix_begin, int64_t pix_end, float* film, cr_stats* st) {
+/* Samples [k_begin, k_begin + k_count) of the spp-sample stratification grid,
+ * summed into film (no 1/spp scale): one rank's share of a sample-sharded PT
+ * render (winmad_rt.dist.pt_sample_range), surfaceIntegrator.cpp:14-46 */
+int cr_render_pt_samples(const cr_scene* s, int W, int H, int spp, int k_begin, int k_count, int max_depth,
+                         uint32_t seed, int rng_mode, int64_t pix_begin, int64_t pix_end, float* film,
+                         cr_stats* st) {
     init_consts();
     if (!s || s->nprims == 0 || s->nlights == 0) { set_err("scene has no geometry or lights", NULL); return -1; }
+    if (k_begin < 0 || k_count < 0 || k_begin + k_count > spp) { set_err("bad sample range", NULL); return -1; }
+    if (rng_mode != CR_RNG_COUNTER && (k_begin != 0 || k_count != spp)) {
+        set_err("sample ranges need the counter RNG", NULL);
+        return -1;
+    }
     const camera_t* cam = &s->cam;
     mt_state mt;
     mt_seed(&mt, seed);
     rng_t rng;
     if (pix_end > (int64_t)W * H) pix_end = (int64_t)W * H;
     double t0 = now_s();
-    for (int64_t pix = pix_begin; pix < pix_end; pix++) {  /* surfaceIntegrator.cpp:14-46 */
+    for (int64_t pix = pix_begin; pix < pix_end; pix++) {
         int i = (int)(pix / W), j = (int)(pix % W);
-        for (int k = 0; k < spp; k++) {
+        for (int k = k_begin; k < k_begin + k_count; k++) {
             rng_for(&rng, rng_mode, &mt, seed, (uint32_t)k, 2, (uint32_t)pix);
             v3 v0 = mk((float)j - 0.5f, (float)i - 0.5f, 0);
             v3 v1 = mk((float)j + 0.5f, (float)i - 0.5f, 0);
@@ -2355,10 +2364,18 @@ int cr_render_pt(const cr_scene* s, int W, int H, int spp, int max_depth, uint32
             film_add(film, H, W, i, j, v);
         }
     }
-    float inv = 1.f / (float)spp;
+    if (st) st->seconds += now_s() - t0;
+    return 0;
+}
+
+int cr_render_pt(const cr_scene* s, int W, int H, int spp, int max_depth, uint32_t seed, int rng_mode,
+                 int64_t pix_begin, int64_t pix_end, float* film, cr_stats* st) {
+    int rc = cr_render_pt_samples(s, W, H, spp, 0, spp, max_depth, seed, rng_mode, pix_begin, pix_end, film, st);
+    if (rc) return rc;
+    if (pix_end > (int64_t)W * H) pix_end = (int64_t)W * H;
+    float inv = 1.f / (float)spp;  /* film->scale(1.f / samplesPerPixel) */
     for (int64_t pix = pix_begin; pix < pix_end; pix++)
         for (int ch = 0; ch < 3; ch++) film[3 * pix + ch] = film[3 * pix + ch] * inv;
-    if (st) st->seconds += now_s() - t0;
     return 0;
 }
 

@@ -76,7 +76,13 @@ int cr_render_vcm(const cr_scene* s, int W, int H, int iter_begin, int iteration
                   int rng_mode, int min_path_length, int max_path_length, float radius_factor,
                   float radius_alpha, int64_t path_begin, int64_t path_end, float* film, cr_stats* st);
 
-/* PT (pathIntegrator.cpp:29-148 + surfaceIntegrator.cpp:14-46); film scaled by 1/spp. */
+/* PT (pathIntegrator.cpp:29-148 + surfaceIntegrator.cpp:14-46).  cr_render_pt:
+ * all spp samples, film scaled by 1/spp.  cr_render_pt_samples: samples
+ * [k_begin, k_begin + k_count) of the spp grid summed unscaled (one rank's
+ * share of a sample-sharded render; counter RNG only unless the range is all). */
+int cr_render_pt_samples(const cr_scene* s, int W, int H, int spp, int k_begin, int k_count, int max_depth,
+                         uint32_t seed, int rng_mode, int64_t pix_begin, int64_t pix_end, float* film,
+                         cr_stats* st);
 int cr_render_pt(const cr_scene* s, int W, int H, int spp, int max_depth, uint32_t seed,
                  int rng_mode, int64_t pix_begin, int64_t pix_end, float* film, cr_stats* st);
 

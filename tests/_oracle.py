@@ -46,6 +46,7 @@ def lib():
         L.cr_render_vcm.argtypes = [P, I, I, I, I, U32, I, I, I, C.c_float, C.c_float, I64, I64, F,
                                     C.POINTER(Stats)]
         L.cr_render_pt.argtypes = [P, I, I, I, I, U32, I, I64, I64, F, C.POINTER(Stats)]
+        L.cr_render_pt_samples.argtypes = [P, I, I, I, I, I, I, U32, I, I64, I64, F, C.POINTER(Stats)]
         L.cr_pt_radiance.argtypes = [P, F, I64, I, U32, U32, F, C.POINTER(Stats)]
         L.cr_stream_key.restype = C.c_uint64
         L.cr_stream_key.argtypes = [U32, U32, U32, U32]
@@ -143,6 +144,17 @@ class Scene:
         st = Stats()
         pb, pe = pix_range or (0, W * H)
         rc = self.L.cr_render_pt(self.h, W, H, spp, max_depth, seed, mode, pb, pe, fptr(film), C.byref(st))
+        if rc:
+            raise RuntimeError(self.L.cr_last_error().decode())
+        return film, st
+
+    def pt_samples(self, W, H, spp, k_begin, k_count, max_depth, seed, mode=1, pix_range=None):
+        """Samples [k_begin, k_begin + k_count) of the spp grid, summed (no 1/spp)."""
+        film = np.zeros((H, W, 3), np.float32)
+        st = Stats()
+        pb, pe = pix_range or (0, W * H)
+        rc = self.L.cr_render_pt_samples(self.h, W, H, spp, k_begin, k_count, max_depth, seed, mode, pb, pe,
+                                         fptr(film), C.byref(st))
         if rc:
             raise RuntimeError(self.L.cr_last_error().decode())
         return film, st

@@ -28,7 +28,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, scene, out_dir):
+PT_SPP = 5  # uneven split over 2 ranks: samples [0, 3) and [3, 5)
+
+
+def _render(kind, scene, iters, it0):
+    if kind == "pt":  # `iters` ranks' worth of samples: rank r's pt_sample_range
+        b, n = (0, PT_SPP) if iters == 2 * K else wdist.pt_sample_range(it0 // K, 2, PT_SPP)
+        return _oracle.Scene(scene).pt_samples(W, H, PT_SPP, b, n, 7, 5489)
+    if kind == "vcm":  # merge radius from the global iteration index (vertexcm.cpp)
+        return _oracle.Scene(scene).vcm(W, H, iters, 5489, mode=1, iter_begin=it0)
+    return _oracle.Scene(scene).bdpt(W, H, iters, 5489, mode=1, iter_begin=it0)
+
+
+def _rank_main(rank, world, port, scene, out_dir, kind="bdpt"):
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.join(os.path.dirname(here), "winmad-s-raytracer-v1.0_amd")):
         if p not in sys.path:
@@ -38,7 +50,7 @@ def _rank_main(rank, world, port, scene, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         it0 = wdist.bdpt_iteration_begin(rank, K)
-        film, st = _oracle.Scene(scene).bdpt(W, H, K, 5489, mode=1, iter_begin=it0)
+        film, st = _render(kind, scene, K, it0)
         t = torch.from_numpy(film)
         wdist.reduce_film(t, dist)
         elapsed, rays = wdist.job_totals(0.5 + rank, st.closest_rays + st.shadow_rays, dist)
@@ -50,11 +62,16 @@ def _rank_main(rank, world, port, scene, out_dir):
         dist.destroy_process_group()
 
 
-def test_bdpt_iteration_sharding_over_two_gloo_ranks(tmp_path):
+@pytest.mark.parametrize("kind", ["bdpt", "vcm", "pt"])
+def test_iteration_sharding_over_two_gloo_ranks(kind, tmp_path):
+    """BDPT and VCM: rank r renders iteration r; reduce(sum) on rank 0 equals
+    the single-process render of both iterations (VCM: each iteration's merge
+    radius and grid come from its global index, so no other exchange).  PT:
+    rank r renders its pt_sample_range share of the spp grid."""
     scene = _scenes.torus(W, H)
-    mp.spawn(_rank_main, args=(2, _free_port(), scene, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_rank_main, args=(2, _free_port(), scene, str(tmp_path), kind), nprocs=2, join=True)
     film = np.load(tmp_path / "film.npy")
-    ref, rst = _oracle.Scene(scene).bdpt(W, H, 2 * K, 5489, mode=1)
+    ref, rst = _render(kind, scene, 2 * K, 0)
     assert np.allclose(film, ref, rtol=1e-5, atol=1e-7)
     elapsed, rays = np.load(tmp_path / "totals.npy")
     assert elapsed == 1.5  # max over ranks

@@ -152,6 +152,17 @@ def test_pt_sample_sharding_is_additive():
     assert np.allclose(a + b, full, rtol=1e-5, atol=1e-6)
 
 
+def test_pt_sample_range_matches_oracle():
+    """One rank's share (samples [3, 8) of a 9-sample grid, stratified over the
+    whole grid) equals the oracle's cr_render_pt_samples of the same range."""
+    path = _scenes.cbox(64, 48)
+    film, st = ctx(path).render_path(64, 48, spp=9, max_depth=7, seed=8, sample_begin=3, sample_count=5)
+    ref, rst = _oracle.Scene(path).pt_samples(64, 48, 9, 3, 5, 7, 8)
+    rmse, rms, ch = film_err(film, ref)
+    assert rmse / rms < 1e-2, (rmse, rms)
+    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+
+
 def test_bdpt_1080p_properties_and_sharding():
     """Full C2 frame size: finite, non-negative, iteration-sharded renders sum
     to the unsharded one (multi-GPU invariance), identical ray sets."""
