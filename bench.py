@@ -191,7 +191,11 @@ def main():
     ap.add_argument("--cpu-paths", type=int, default=1000000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting replay")
+    ap.add_argument("--no-cut", action="store_true",
+                    help="c3/vcm: shadow rays run to the end of the walk (no occlusion cutoff)")
     args = ap.parse_args()
+    if args.no_cut:
+        os.environ["WR_TRACE_NO_CUT"] = "1"  # read by wr_create
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -310,6 +314,13 @@ def main():
             "rays_per_step": round(total_rays / (K * world)),
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if cfg["integrator"] in ("pt", "vcm"):
+            # dead-work elision is flagged; --no-cut measures without it
+            out["config"]["occlusion_cutoff"] = not args.no_cut
+            if not args.no_cut:
+                out["dead_work_elision"] = ("occlusion cutoff: a shadow ray ends once a hit below occl_cut "
+                                            "settles 'occluded' (exact, DESIGN.md section 4); every ray is "
+                                            "still traced and counted; bench.py --no-cut runs without it")
         if cfg["integrator"] == "vcm":
             out["merges_per_step"] = round(st.vm_merged / K)
             out["merge_queries_per_step"] = round(st.vm_queries / K)

@@ -321,6 +321,7 @@ struct wr_context {
   int trace_blocks = 4096;        // resident one-wave workgroups of the traversal
   int trace_blocks_dense = 4096;  // the same for the TRACE_DENSE layout
   bool api_dense = false;         // test knob WR_TRACE_DENSE=1: API launches in TRACE_DENSE
+  bool no_cut = false;            // WR_TRACE_NO_CUT=1: shadow rays run to the end (no occl_cut)
   bool timing = false;
 };
 
@@ -594,7 +595,10 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, int
 // One persistent traversal launch over qa then qb (max_rays bounds the grid).
 // `fetch` must be zero (the iteration's counter memset, or the caller).
 int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, int* fetch, Timer& tm, bool count,
-                 const TraceQueues& Q, int max_rays, int mode = TRACE_PLAIN) {
+                 const TraceQueues& Q_, int max_rays, int mode = TRACE_PLAIN) {
+  TraceQueues Q = Q_;
+  if (c->no_cut)  // measurement knob: the same launches without the dead-work elision
+    for (int i = 0; i < Q.n; ++i) Q.q[i].cut = nullptr;
   const bool dense = mode == TRACE_DENSE && !c->stamps;
   const size_t lds = trace_lds_bytes(c->ds.max_stack, c->narrow, dense);
   const int grid =
@@ -1008,6 +1012,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   if (const char* e = std::getenv("WR_TRACE_STAMPS")) c->stamps = std::atoi(e) != 0 && !c->spheres;
   if (const char* e = std::getenv("WR_TRACE_LOG")) c->trace_log = std::atoi(e) != 0;
   if (const char* e = std::getenv("WR_TRACE_DENSE")) c->api_dense = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WR_TRACE_NO_CUT")) c->no_cut = std::atoi(e) != 0;
   if (const char* e = std::getenv("WR_VCM_CELL")) c->vcm_cell = std::min(8.f, std::max(0.25f, (float)std::atof(e)));
   {
     // persistent traversal grid: the one-wave workgroups that fit at once (LDS stack
