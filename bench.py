@@ -232,7 +232,11 @@ def main():
     if pt and (world * K > args.spp or args.warmup > args.spp):
         raise SystemExit(f"c3: --steps x ranks ({world * K}) must not exceed --spp ({args.spp})")
     if args.warmup > 0:  # warm-up samples / iterations outside the timed ones
-        render((args.spp - args.warmup) if pt else (1 << 20), args.warmup, film_ptr=film.data_ptr())
+        # run as the counting build of the traversal (k_trace<true, ...>): the
+        # same caches and allocations warm up, and a rocprofv3 summary of this
+        # command then lists exactly the timed launches under k_trace<false, ...>
+        render((args.spp - args.warmup) if pt else (1 << 20), args.warmup, film_ptr=film.data_ptr(),
+               count_work=1)
     film.zero_()
     torch.cuda.synchronize()
     if dist:

@@ -69,6 +69,29 @@ def main():
         json.dump(out, fh, indent=1)
     print(json.dumps(out))
 
+    # the trace pass's bench line beside rocprof's own k_trace durations (the
+    # warm-up runs the counting build, so k_trace<false, ...> = the timed launches)
+    line = None
+    log = os.path.join(src, "trace.log")
+    if os.path.exists(log):
+        with open(log) as fh:
+            lines = [l for l in fh if l.startswith('{"metric"')]
+        line = json.loads(lines[-1]) if lines else None
+    if line and os.path.exists(stats):
+        with open(os.path.join(dst, "bench_c2_profiled_run.json"), "w") as fh:
+            fh.write(json.dumps(line) + "\n")
+        rows = [r for r in csv.DictReader(open(stats)) if short(r["Name"]).startswith(DOMINANT + "<false")]
+        calls = sum(int(r["Calls"]) for r in rows)
+        tot = sum(float(r["TotalDurationNs"]) for r in rows)
+        r = line["roofline"]
+        cmp_ = {"rocprof_kernel": [short(r_["Name"]) for r_ in rows],
+                "rocprof_calls": calls, "rocprof_avg_ms": round(tot / max(1, calls) / 1e6, 4),
+                "bench_launches": r["launches"], "bench_event_avg_ms": r["avg_launch_ms"],
+                "ratio_events_over_rocprof": round(r["avg_launch_ms"] / (tot / max(1, calls) / 1e6), 3)}
+        with open(os.path.join(dst, "duration_check.json"), "w") as fh:
+            json.dump(cmp_, fh, indent=1)
+        print(json.dumps(cmp_))
+
 
 if __name__ == "__main__":
     main()
