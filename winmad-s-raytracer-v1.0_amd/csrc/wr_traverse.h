@@ -268,6 +268,14 @@ __host__ __device__ constexpr size_t trace_lds_bytes(int depth, bool narrow, boo
          size_t(4) * ((dense ? 0 : 8 * 64 + 64) + kLeavesPerRound * 64 + kLeavesPerRound * (narrow ? 32 : 64) +
                       kPairBatch / 4 + 4 * 64 + 16 + kMail * 64 + (kMail > 0 ? kPairBatch / 2 : 0));
 }
+// Ray prefetch: a lane holds the record of its next ray in registers, loaded
+// one round ahead, so a refill does not wait on the queue load (never in the
+// DENSE layout: no register room at 96 VGPRs).  Exact, but OFF: it costs C2
+// 889 -> 828, VCM 796 -> 753, C4 41.4 -> 38.3 Mrays/s (127 VGPRs; vector
+// loads retire in order, so the walk's first wait also waits for the prefetch).
+#ifndef WR_RAY_PREFETCH
+#define WR_RAY_PREFETCH 0
+#endif
 // value of v in lane `src` (all lanes of the wave active)
 __device__ __forceinline__ float lane_get(float v, int src) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
@@ -379,13 +387,26 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
   }
   const int n = qend[kMaxQueues - 1];
   int qi = 0;            // queue of the lane's ray
-  // field of queue qi (selects, no dynamic indexing of the kernel argument)
-  auto sel = [&](auto field) {
+  // field of queue q (selects, no dynamic indexing of the kernel argument)
+  auto selq = [&](int q, auto field) {
     auto v = field(Q.q[0]);
 #pragma unroll
     for (int i = 1; i < kMaxQueues; ++i)
-      if (qi == i) v = field(Q.q[i]);
+      if (q == i) v = field(Q.q[i]);
     return v;
+  };
+  auto sel = [&](auto field) { return selq(qi, field); };
+  // queue and index within it of launch index idx
+  auto locate = [&](int idx, int& q, int& rr) {
+    q = 0;
+    int q0 = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxQueues - 1; ++i)
+      if (idx >= qend[i]) {
+        q = i + 1;
+        q0 = qend[i];
+      }
+    rr = idx - q0;
   };
   int r = -1;            // ray held by this lane (-1: none)
   bool pool = true;      // wave-uniform: queue not yet exhausted
@@ -396,6 +417,58 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
   float rtmin_v = 0.f, screen0 = WR_INF;  // the ray's tmin; its best at round start
   int best = -1, sp = 0;
   uint32_t node = 0;
+  constexpr bool PF = WR_RAY_PREFETCH != 0 && !DENSE;
+  int pidx = -1;  // PF: launch index of the prefetched ray (-1: none)
+  V3 po = v3(0.f, 0.f, 0.f), pd = po;
+  float ptn = 0.f, ptx = WR_INF, pcut = -WR_INF;
+  // queue indices come from the wave's reservation [pb, pe), topped up kRayGrab
+  // at a time (one global atomic per kRayGrab rays, not per refill)
+  auto reserve = [&](bool want) -> int {
+    const unsigned long long m = __ballot(want);
+    const int need = __popcll(m);
+    const int rank = __popcll(m & ((1ull << lane) - 1ull));
+    int idx = pb + rank;
+    if (need == 0) return idx;
+    if (pe - pb < need) {
+      int got = 0;
+      if (lane == 0) got = atomicAdd(fetch, kRayGrab);
+      got = __builtin_amdgcn_readlane(got, 0);
+      const int rem = pe - pb;
+      if (rank >= rem) idx = got + (rank - rem);
+      pb = got + (need - rem);
+      pe = got + kRayGrab;
+    } else {
+      pb += need;
+    }
+    return idx;
+  };
+  // PF: reserve the next ray of the lanes in `want` and issue its loads
+  auto prefetch = [&](bool want) {
+    const int idx = reserve(want);
+    if (want) {
+      pidx = -1;
+      if (idx < n) {
+        int q, rr;
+        locate(idx, q, rr);
+        pidx = idx;
+        const float* o3 = selq(q, [](const RayQueue& x) { return x.o3; });
+        const float* d3 = selq(q, [](const RayQueue& x) { return x.d3; });
+        const int cap = selq(q, [](const RayQueue& x) { return x.cap; });
+        const float* tmn = selq(q, [](const RayQueue& x) { return x.tmin; });
+        const float* tmx = selq(q, [](const RayQueue& x) { return x.tmax; });
+        po = v3(o3[rr], o3[cap + rr], o3[2 * cap + rr]);
+        pd = v3(d3[rr], d3[cap + rr], d3[2 * cap + rr]);
+        ptn = tmn ? tmn[rr] : 0.f;
+        ptx = tmx ? tmx[rr] : WR_INF;
+        if constexpr (CUT) {
+          const float* cutp = selq(q, [](const RayQueue& x) { return x.cut; });
+          pcut = cutp ? cutp[rr] : -WR_INF;
+        }
+      }
+    }
+    if (__ballot(want && idx >= n)) pool = false;
+  };
+  if constexpr (PF) prefetch(true);
   // one level of KDtreeAccelNode descent (:325-358) from inner node `at` (word w)
   auto step = [&](uint2 w, uint32_t at) -> uint32_t {
     if (COUNT) ++ctr.inner;
@@ -435,50 +508,42 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
   };
   for (;;) {
     // ---- refill idle lanes
-    if (pool) {
+    if (PF ? (pool || __ballot(pidx >= 0) != 0) : pool) {
       const bool idle = r < 0;
-      const unsigned long long m = __ballot(idle);
-      if (m) {
-        // queue indices come from the wave's reservation [pb, pe), topped up
-        // kRayGrab at a time (one global atomic per kRayGrab rays, not per refill)
-        const int need = __popcll(m);
-        const int rank = __popcll(m & ((1ull << lane) - 1ull));
-        int idx = pb + rank;
-        if (pe - pb < need) {
-          int got = 0;
-          if (lane == 0) got = atomicAdd(fetch, kRayGrab);
-          got = __builtin_amdgcn_readlane(got, 0);
-          const int rem = pe - pb;
-          if (rank >= rem) idx = got + (rank - rem);
-          pb = got + (need - rem);
-          pe = got + kRayGrab;
+      if (__ballot(idle)) {
+        int idx;
+        bool take;
+        if constexpr (PF) {  // the prefetched ray; the next one is requested below
+          idx = pidx;
+          take = idle && pidx >= 0;
         } else {
-          pb += need;
+          idx = reserve(idle);
+          take = idle && idx < n;
         }
-        if (idle && idx < n) {
-          qi = 0;
-          int q0 = 0;
-#pragma unroll
-          for (int i = 0; i < kMaxQueues - 1; ++i)
-            if (idx >= qend[i]) {
-              qi = i + 1;
-              q0 = qend[i];
+        if (take) {
+          locate(idx, qi, r);
+          if constexpr (PF) {
+            o = po;
+            d = pd;
+            rtmin_v = ptn;
+            rtmax = ptx;
+            if constexpr (CUT) rcut = pcut;
+          } else {
+            const float* o3 = sel([](const RayQueue& x) { return x.o3; });
+            const float* d3 = sel([](const RayQueue& x) { return x.d3; });
+            const int cap = sel([](const RayQueue& x) { return x.cap; });
+            const float* tmn = sel([](const RayQueue& x) { return x.tmin; });
+            const float* tmx = sel([](const RayQueue& x) { return x.tmax; });
+            o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
+            d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+            rtmin_v = tmn ? tmn[r] : 0.f;
+            rtmax = tmx ? tmx[r] : WR_INF;
+            if constexpr (CUT) {
+              const float* cutp = sel([](const RayQueue& x) { return x.cut; });
+              rcut = cutp ? cutp[r] : -WR_INF;
             }
-          r = idx - q0;
-          const float* o3 = sel([](const RayQueue& x) { return x.o3; });
-          const float* d3 = sel([](const RayQueue& x) { return x.d3; });
-          const int cap = sel([](const RayQueue& x) { return x.cap; });
-          const float* tmn = sel([](const RayQueue& x) { return x.tmin; });
-          const float* tmx = sel([](const RayQueue& x) { return x.tmax; });
-          o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
-          d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
-          const float rtmin = tmn ? tmn[r] : 0.f;
-          rtmin_v = rtmin;
-          rtmax = tmx ? tmx[r] : WR_INF;
-          if constexpr (CUT) {
-            const float* cutp = sel([](const RayQueue& x) { return x.cut; });
-            rcut = cutp ? cutp[r] : -WR_INF;
           }
+          const float rtmin = rtmin_v;
           t_best = WR_INF;
           best = -1;
           sp = 0;
@@ -501,13 +566,18 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
             for (int k = 0; k < kMail; ++k) mail[lane * kMail + k] = 0;
           }
         }
-        if (__ballot(idle && idx >= n)) pool = false;
+        if constexpr (PF) {
+          if (pool) prefetch(take);
+          else if (take) pidx = -1;
+        } else if (__ballot(idle && idx >= n)) {
+          pool = false;
+        }
       }
     }
     WR_STAMP(0)
     const bool act = r >= 0;
     if (!__ballot(act)) {
-      if (!pool) break;
+      if (!pool && !(PF && __ballot(pidx >= 0))) break;  // PF: prefetched rays still to take
       continue;
     }
     // ---- walk to the next leaves (:321-358, pops :375-383).  One record pair
