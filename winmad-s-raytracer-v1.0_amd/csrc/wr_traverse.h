@@ -235,7 +235,15 @@ static_assert(kPairBatch % 256 == 0, "the owner-table scan covers 4 bytes per la
 #ifndef WR_PAIRS_IN_FLIGHT
 #define WR_PAIRS_IN_FLIGHT 2
 #endif
-constexpr int kPairsInFlight = WR_PAIRS_IN_FLIGHT;     // (ray, triangle) records requested per lane per trip
+#ifndef WR_PAIRS_IN_FLIGHT_WIDE
+#define WR_PAIRS_IN_FLIGHT_WIDE 4  // 32-bit-index trees (> 65536 nodes): C4 +4 % over 2
+#endif
+// (ray, triangle) records requested per lane per trip; torus-sized trees: 4
+// costs C2 1.5 %
+constexpr int kPairsInFlight = WR_PAIRS_IN_FLIGHT;
+constexpr int kPairsInFlightWide = WR_PAIRS_IN_FLIGHT_WIDE;
+static_assert(kPairBatch % (64 * kPairsInFlight) == 0 && kPairBatch % (64 * kPairsInFlightWide) == 0,
+              "a batch is whole trips");
 constexpr int kLeavesPerRound = WR_LEAVES_PER_ROUND;
 #ifndef WR_RAY_GRAB
 #define WR_RAY_GRAB 128  // 64: C2 -0.8 %, 256: -1 %
@@ -422,6 +430,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
   int best = -1, sp = 0;
   uint32_t node = 0;
   constexpr bool PF = WR_RAY_PREFETCH != 0 && !DENSE;
+  constexpr int PIF = (NARROW || DENSE) ? kPairsInFlight : kPairsInFlightWide;  // DENSE: no room at 96 VGPRs
   int pidx = -1;  // PF: launch index of the prefetched ray (-1: none)
   V3 po = v3(0.f, 0.f, 0.f), pd = po;
   float ptn = 0.f, ptx = WR_INF, pcut = -WR_INF;
@@ -754,40 +763,40 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
         }
         __syncthreads();
       }
-      // kPairsInFlight pairs per lane per trip: c, c + 64, ... of the kept
+      // PIF pairs per lane per trip: c, c + 64, ... of the kept
       // slots; all their records are requested before the first test.  A lane
       // keeps the t of its own pairs ((c - lane) / 64) in registers.
       float tv[kPairBatch / 64];
 #pragma unroll
       for (int k = 0; k < kPairBatch / 64; ++k) tv[k] = __int_as_float(0x7fc00000);  // NaN: no hit
 #pragma unroll
-      for (int tr = 0; tr < kPairBatch / (64 * kPairsInFlight); ++tr) {
-        const int c0 = lane + 64 * kPairsInFlight * tr;
-        if (64 * kPairsInFlight * tr >= nk) break;  // wave-uniform
-        uint32_t ref[kPairsInFlight];
-        int owner[kPairsInFlight];
+      for (int tr = 0; tr < kPairBatch / (64 * PIF); ++tr) {
+        const int c0 = lane + 64 * PIF * tr;
+        if (64 * PIF * tr >= nk) break;  // wave-uniform
+        uint32_t ref[PIF];
+        int owner[PIF];
 #pragma unroll
-        for (int u = 0; u < kPairsInFlight; ++u) {
+        for (int u = 0; u < PIF; ++u) {
           const int c = min(c0 + 64 * u, max(nk - 1, 0));
           const int j = kMail > 0 ? static_cast<int>(cslot[c]) : c;
           const int id = own[j];
           owner[u] = id / kLeavesPerRound;
           ref[u] = leaf_first[id] + static_cast<uint32_t>(base + j - static_cast<int>(leaf_off[id]));
         }
-        float2 rc[kPairsInFlight];
-        float4 ra[kPairsInFlight], rb[kPairsInFlight];
+        float2 rc[PIF];
+        float4 ra[PIF], rb[PIF];
 #pragma unroll
-        for (int u = 0; u < kPairsInFlight; ++u) {
+        for (int u = 0; u < PIF; ++u) {
           rc[u] = S.ref_c[ref[u]];
           ra[u] = S.ref_a[ref[u]];
           rb[u] = S.ref_b[ref[u]];
         }
         // the owners' rays (converged wave: every source lane is active)
-        float4 gx[kPairsInFlight], gy[kPairsInFlight];
-        float gs[kPairsInFlight];
+        float4 gx[PIF], gy[PIF];
+        float gs[PIF];
         if constexpr (DENSE) {
 #pragma unroll
-          for (int u = 0; u < kPairsInFlight; ++u) {
+          for (int u = 0; u < PIF; ++u) {
             const int L = owner[u];
             gx[u] = make_float4(lane_get(o.x, L), lane_get(o.y, L), lane_get(o.z, L), lane_get(d.x, L));
             gy[u] = make_float4(lane_get(d.y, L), lane_get(d.z, L), lane_get(rtmin_v, L), lane_get(rtmax, L));
@@ -795,7 +804,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
           }
         }
 #pragma unroll
-        for (int u = 0; u < kPairsInFlight; ++u) {
+        for (int u = 0; u < PIF; ++u) {
           if (c0 + 64 * u >= nk) break;
           if (COUNT) ++ctr.tests;
           const int L = owner[u];
@@ -809,7 +818,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
             atomicMin(olo + L, (key << 32) | pr);
             atomicMax(ohi + L, ((0x7fffffffull - key) << 32) | pr);
           }
-          tv[tr * kPairsInFlight + u] = t;
+          tv[tr * PIF + u] = t;
         }
       }
       __syncthreads();
