@@ -275,7 +275,10 @@ size_t measure(Fn fn) {  // bytes an arena layout needs
 // launches (a launch lasts as long as its slowest ray) overlaps the full
 // launches of another.  The film is a sum, so the result does not depend on the
 // pipeline count (up to the order of float atomics).
-constexpr int kMaxPipes = 16;
+#ifndef WR_MAX_PIPES
+#define WR_MAX_PIPES 16
+#endif
+constexpr int kMaxPipes = WR_MAX_PIPES;
 // Each pipeline advances a group of up to kGroup iterations / samples in
 // lockstep: every traversal launch takes the queues of all of them, so the
 // launch tail (its slowest ray) is paid once per group.
@@ -1046,7 +1049,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
 }
 
 int wr_set_pipelines(wr_context* c, int n) {
-  if (!c || n < 1 || n > kMaxPipes) return fail(WR_E_ARG, "pipelines must be in 1..16");
+  if (!c || n < 1 || n > kMaxPipes) return fail(WR_E_ARG, "pipelines must be in 1.." + std::to_string(kMaxPipes));
   c->npipes = n;
   return WR_OK;
 }
