@@ -878,28 +878,28 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     }
     nrec[i] = make_uint4(self.x, self.y, l.x, l.y);
   }
-  // three-level records (WR_NODE_LEVELS = 3): self, children, grandchildren
-  std::vector<uint4> nrec3(4 * nn, make_uint4(0u, 0u, 0u, 0u));
+  // multi-level records (WR_NODE_LEVELS = 3 or 4): node i's subtree of
+  // kRecLevels levels in heap order (entry 0 = i, entries 2h+1 / 2h+2 = the
+  // children of entry h; 0 below a leaf), two entries per uint4
+  std::vector<uint4> nrec3(kRecU4 * nn, make_uint4(0u, 0u, 0u, 0u));
   {
-    auto word = [&](int64_t i) { return i >= 0 ? nodes[static_cast<size_t>(i)] : make_uint2(0u, 0u); };
-    auto kids = [&](int64_t i, int64_t& l, int64_t& r) {
-      l = r = -1;
-      if (i >= 0 && s.nodes[static_cast<size_t>(i)].axis >= 0) {
-        l = i + 1;
-        r = s.nodes[static_cast<size_t>(i)].right;
-      }
-    };
+    constexpr int kEnt = (1 << kRecLevels) - 1;
     for (size_t i = 0; i < nn; ++i) {
-      int64_t L, R, LL, LR, RL, RR;
-      kids(static_cast<int64_t>(i), L, R);
-      kids(L, LL, LR);
-      kids(R, RL, RR);
-      const uint2 w0 = word(static_cast<int64_t>(i)), wl = word(L), wr = word(R), wll = word(LL), wlr = word(LR),
-                  wrl = word(RL), wrr = word(RR);
-      nrec3[4 * i] = make_uint4(w0.x, w0.y, wl.x, wl.y);
-      nrec3[4 * i + 1] = make_uint4(wr.x, wr.y, wll.x, wll.y);
-      nrec3[4 * i + 2] = make_uint4(wlr.x, wlr.y, wrl.x, wrl.y);
-      nrec3[4 * i + 3] = make_uint4(wrr.x, wrr.y, 0u, 0u);
+      int64_t e[kEnt];
+      e[0] = static_cast<int64_t>(i);
+      for (int h = 0; 2 * h + 2 < kEnt; ++h) {
+        e[2 * h + 1] = e[2 * h + 2] = -1;
+        if (e[h] >= 0 && s.nodes[static_cast<size_t>(e[h])].axis >= 0) {
+          e[2 * h + 1] = e[h] + 1;
+          e[2 * h + 2] = s.nodes[static_cast<size_t>(e[h])].right;
+        }
+      }
+      uint32_t* w = reinterpret_cast<uint32_t*>(&nrec3[kRecU4 * i]);
+      for (int h = 0; h < kEnt; ++h) {
+        const uint2 v = e[h] >= 0 ? nodes[static_cast<size_t>(e[h])] : make_uint2(0u, 0u);
+        w[2 * h] = v.x;
+        w[2 * h + 1] = v.y;
+      }
     }
   }
   std::vector<float4> ra(nr), rb(nr);
@@ -949,7 +949,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                    v3(m.specular.x, m.specular.y, m.specular.z), m.phong_exp, m.index};
   }
   auto total = measure([&](Arena& a) {
-    a.take<uint4>(nn); a.take<uint2>(nn); a.take<uint4>(4 * nn); a.take<float4>(nr); a.take<float4>(nr);
+    a.take<uint4>(nn); a.take<uint2>(nn); a.take<uint4>(kRecU4 * nn); a.take<float4>(nr); a.take<float4>(nr);
     a.take<float2>(nr);
     a.take<int>(np); a.take<int>(np); a.take<float4>(np); a.take<float2>(np); a.take<float4>(np);
     a.take<float4>(np); a.take<float2>(np); a.take<DLight>(lights.size() + 1); a.take<DMat>(mats.size());
@@ -966,7 +966,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   DevScene& d = c->ds;
   uint4* dn = A.take<uint4>(nn);
   uint2* dnr = A.take<uint2>(nn);
-  uint4* dn3 = A.take<uint4>(4 * nn);
+  uint4* dn3 = A.take<uint4>(kRecU4 * nn);
   float4* dra = A.take<float4>(nr);
   float4* drb = A.take<float4>(nr);
   float2* drc = A.take<float2>(nr);

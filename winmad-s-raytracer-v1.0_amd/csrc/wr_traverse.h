@@ -219,9 +219,14 @@ struct TraceQueues {
 #endif
 constexpr int kPairBatch = WR_PAIR_BATCH;  // multiple of 256
 #ifndef WR_NODE_LEVELS
-#define WR_NODE_LEVELS 3  // tree levels resolved per dependent record load (2 or 3); 3: C2 892 -> 911 Mrays/s
+// tree levels resolved per dependent record load (2, 3 or 4); 3 over 2: C2
+// 892 -> 911 Mrays/s; 4 (128-byte records, exact) loses 13-16 % on C2/C3
+#define WR_NODE_LEVELS 3
 #endif
 static_assert(kPairBatch % 256 == 0, "the owner-table scan covers 4 bytes per lane per 256 slots");
+static_assert(WR_NODE_LEVELS >= 2 && WR_NODE_LEVELS <= 4, "node record levels: 2, 3 or 4");
+constexpr int kRecLevels = WR_NODE_LEVELS < 3 ? 3 : WR_NODE_LEVELS;  // nrec3 layout
+constexpr int kRecU4 = kRecLevels == 4 ? 8 : 4;                      // uint4 per record
 #ifndef WR_LEAVES_PER_ROUND
 #define WR_LEAVES_PER_ROUND 4
 #endif
@@ -600,7 +605,44 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
     int nl = 0, count = 0;
     while (__ballot(more && nl < kLeavesWait)) {
       if (more && nl < kLeavesPerRound) {
-#if WR_NODE_LEVELS == 3
+#if WR_NODE_LEVELS == 4
+        // 15 entries in 128 bytes: up to four descent steps per record
+        const uint4* rp = S.nrec3 + 8 * static_cast<size_t>(node);
+        const uint4 q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3], q4 = rp[4], q5 = rp[5], q6 = rp[6], q7 = rp[7];
+        asm volatile("" : : "v"(q0.y), "v"(q1.x), "v"(q2.x), "v"(q3.x), "v"(q4.x), "v"(q5.x), "v"(q6.x), "v"(q7.x));
+        uint2 nd = make_uint2(q0.x, q0.y);
+        bool leaf = (nd.y & 3u) == 3u;
+        if (!leaf) {
+          const uint32_t a0 = node;
+          node = step(nd, a0);
+          const bool b1 = node != a0 + 1;  // went right
+          nd = b1 ? make_uint2(q1.x, q1.y) : make_uint2(q0.z, q0.w);  // e2 : e1
+          leaf = (nd.y & 3u) == 3u;
+          if (!leaf) {
+            const uint32_t a1 = node;
+            node = step(nd, a1);
+            const bool b2 = node != a1 + 1;
+            // e3 = q1.zw, e4 = q2.xy, e5 = q2.zw, e6 = q3.xy
+            nd = b1 ? (b2 ? make_uint2(q3.x, q3.y) : make_uint2(q2.z, q2.w))
+                    : (b2 ? make_uint2(q2.x, q2.y) : make_uint2(q1.z, q1.w));
+            leaf = (nd.y & 3u) == 3u;
+            if (!leaf) {
+              const uint32_t a2 = node;
+              node = step(nd, a2);
+              const bool b3 = node != a2 + 1;
+              // e7 = q3.zw, e8 = q4.xy, e9 = q4.zw, e10 = q5.xy, e11 = q5.zw,
+              // e12 = q6.xy, e13 = q6.zw, e14 = q7.xy
+              const uint2 l0 = b3 ? make_uint2(q4.x, q4.y) : make_uint2(q3.z, q3.w);
+              const uint2 l1 = b3 ? make_uint2(q5.x, q5.y) : make_uint2(q4.z, q4.w);
+              const uint2 l2 = b3 ? make_uint2(q6.x, q6.y) : make_uint2(q5.z, q5.w);
+              const uint2 l3 = b3 ? make_uint2(q7.x, q7.y) : make_uint2(q6.z, q6.w);
+              nd = b1 ? (b2 ? l3 : l2) : (b2 ? l1 : l0);
+              leaf = (nd.y & 3u) == 3u;
+              if (!leaf) node = step(nd, node);
+            }
+          }
+        }
+#elif WR_NODE_LEVELS == 3
         const uint4* rp = S.nrec3 + 4 * static_cast<size_t>(node);
         const uint4 q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3];
         asm volatile("" : : "v"(q0.y), "v"(q1.x), "v"(q2.x), "v"(q3.x));
