@@ -180,6 +180,45 @@ def test_bdpt_1080p_properties_and_sharding():
     assert 3.5 < rpp < 4.8, rpp
 
 
+def test_4k_frames_properties_and_sharding():
+    """3840x2160 frames (4x BASELINE.json's) for BDPT, VCM and PT: the work
+    buffers scale with the frame (2 pipelines here, up to ~105 GB), renders
+    stay finite and non-negative, iteration / sample shards add up, and BDPT's
+    ray density per pixel is the 1080p frame's."""
+    W, H = 3840, 2160
+    s = native.Scene(_scenes.torus(W, H))
+    c = native.Context(s, 0)
+    try:
+        c.set_pipelines(2)
+        both, s2 = c.render_bdpt(W, H, iterations=2, seed=77)
+        a, sa = c.render_bdpt(W, H, iterations=1, seed=77, iter_begin=0)
+        b, sb = c.render_bdpt(W, H, iterations=1, seed=77, iter_begin=1)
+        assert np.all(np.isfinite(both)) and both.min() >= 0 and both.max() > 0
+        assert sa.closest_rays + sb.closest_rays == s2.closest_rays
+        assert sa.shadow_rays + sb.shadow_rays == s2.shadow_rays
+        assert np.allclose(a + b, both, rtol=1e-4, atol=1e-6)
+        rpp = (sa.closest_rays + sa.shadow_rays) / (W * H)
+        assert 3.5 < rpp < 4.8, rpp
+        # VCM and PT on the same frame: shards add up as well
+        vb, _ = c.render_vcm(W, H, iterations=2, seed=77)
+        va, _ = c.render_vcm(W, H, iterations=1, seed=77, iter_begin=0)
+        vc, _ = c.render_vcm(W, H, iterations=1, seed=77, iter_begin=1)
+        assert np.all(np.isfinite(vb)) and vb.min() >= 0 and vb.max() > 0
+        assert np.allclose(va + vc, vb, rtol=1e-4, atol=1e-6)
+    finally:
+        c.close()
+    cb = native.Context(native.Scene(_scenes.cbox(W, H)), 0)
+    try:
+        cb.set_pipelines(2)
+        full, _ = cb.render_path(W, H, spp=4, seed=7)
+        p0, _ = cb.render_path(W, H, spp=4, seed=7, sample_begin=0, sample_count=1)
+        p1, _ = cb.render_path(W, H, spp=4, seed=7, sample_begin=1, sample_count=3)
+        assert np.all(np.isfinite(full)) and full.min() >= 0 and full.max() > 0
+        assert np.allclose(p0 + p1, full, rtol=1e-4, atol=1e-6)
+    finally:
+        cb.close()
+
+
 def test_bdpt_1080p_matches_oracle_counter_rng():
     """BASELINE.json's own frame (torus.scene 1920x1080, C2), one iteration:
     the GPU film against the oracle's counter-RNG film -- the same gates as the
