@@ -566,18 +566,27 @@ using TraceKernel = void (*)(DevScene, TraceQueues, DevCounters*, int*);
 // the check costs C2 1.5 % (measured).  TRACE_DENSE: cut + the 20-waves/CU
 // layout (PT).
 enum TraceMode { TRACE_PLAIN = 0, TRACE_CUT = 1, TRACE_DENSE = 2 };
+#ifndef WR_BDPT_TRACE_MODE
+// BDPT light / camera passes.  TRACE_DENSE without the cutoff (WR_DENSE_CUT
+// false) measured C2 -2.5 % (-3.7 % with per-queue uniform branches)
+#define WR_BDPT_TRACE_MODE TRACE_PLAIN
+#endif
+#ifndef WR_DENSE_CUT
+#define WR_DENSE_CUT true  // TRACE_DENSE instances carry the occlusion cutoff
+#endif
 #ifndef WR_VCM_TRACE_MODE
 #define WR_VCM_TRACE_MODE TRACE_CUT  // camera pass of VCM (TRACE_DENSE: -1.3 %)
 #endif
 TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, int mode = TRACE_PLAIN) {
   if (stamps) return narrow ? k_trace<false, false, true, true> : k_trace<false, false, false, true>;
   if (mode == TRACE_DENSE) {
+    constexpr bool C = WR_DENSE_CUT;
     if (count) {
-      if (spheres) return narrow ? k_trace<true, true, true, false, true, true> : k_trace<true, true, false, false, true, true>;
-      return narrow ? k_trace<true, false, true, false, true, true> : k_trace<true, false, false, false, true, true>;
+      if (spheres) return narrow ? k_trace<true, true, true, false, C, true> : k_trace<true, true, false, false, C, true>;
+      return narrow ? k_trace<true, false, true, false, C, true> : k_trace<true, false, false, false, C, true>;
     }
-    if (spheres) return narrow ? k_trace<false, true, true, false, true, true> : k_trace<false, true, false, false, true, true>;
-    return narrow ? k_trace<false, false, true, false, true, true> : k_trace<false, false, false, false, true, true>;
+    if (spheres) return narrow ? k_trace<false, true, true, false, C, true> : k_trace<false, true, false, false, C, true>;
+    return narrow ? k_trace<false, false, true, false, C, true> : k_trace<false, false, false, false, C, true>;
   }
   if (mode == TRACE_CUT) {
     if (count) {
@@ -1229,7 +1238,7 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
     for (int b = 0; b < maxlen - 1; ++b) {
       QueueList ql;
       for (int m = 0; m < gn; ++m) ql.add(ext(m, b), P);
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
       hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
       tm.mark(WR_K_SHADE);
     }
@@ -1245,7 +1254,7 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
       for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), sq_max);
       if (more)
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays);
+      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
       // resolve this step's shadow / aux rays and shade its vertices in one launch
       const int nres = shade_grid(c, sq_max);
       hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot, nres,
