@@ -158,10 +158,13 @@ def cpu_reference(cfg_name, kind, W, H, tmp, shrink):
 
 # SURVEY.md 8(d) configurations a bench line can be quoted on
 CONFIGS = {
-    "c2": {"desc": "torus.scene BDPT", "integrator": "bdpt"},
-    "c3": {"desc": "cbox + dragon PT, 512 spp stratification, MAX_TRACING_DEPTH 7", "integrator": "pt"},
-    "c4": {"desc": "1M-triangle synthetic torus BDPT", "integrator": "bdpt"},
-    "vcm": {"desc": "torus.scene VertexCM", "integrator": "vcm"},
+    # steps: default iterations (spp) per GPU -- BASELINE.json configs[1] is 256
+    # spp BDPT, configs[3] 64 spp; c3's 512-spp grid is shared by the ranks
+    "c2": {"desc": "torus.scene BDPT", "integrator": "bdpt", "steps": 256},
+    "c3": {"desc": "cbox + dragon PT, 512 spp stratification, MAX_TRACING_DEPTH 7", "integrator": "pt",
+           "steps": 64},
+    "c4": {"desc": "1M-triangle synthetic torus BDPT", "integrator": "bdpt", "steps": 64},
+    "vcm": {"desc": "torus.scene VertexCM", "integrator": "vcm", "steps": 256},
 }
 METRIC = "Mrays/sec + spp/sec at 1920x1080, torus.scene BDPT, 1/2/4/8 MI355X"
 
@@ -181,7 +184,8 @@ def make_scene(cfg, W, H, tmp, obj=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="iterations (spp) per GPU; default per config: c2/vcm 256, c3/c4 64")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -210,8 +214,9 @@ def main():
     from winmad_rt import native
     from winmad_rt import dist as wdist
 
-    W, H, K = args.width, args.height, args.steps
     cfg = CONFIGS[args.config]
+    W, H = args.width, args.height
+    K = args.steps if args.steps is not None else cfg["steps"]
     pt = cfg["integrator"] == "pt"
     tmp = tempfile.mkdtemp(prefix=f"wr_bench_{rank}_")
     scene_path = make_scene(args.config, W, H, tmp)
