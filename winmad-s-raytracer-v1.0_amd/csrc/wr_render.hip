@@ -152,9 +152,16 @@ template <bool COUNT, bool SPH, bool NARROW, bool STAMP = false, bool CUT = fals
 #ifndef WR_TRACE_CUT_WAVES_PER_EU
 #define WR_TRACE_CUT_WAVES_PER_EU 4
 #endif
+// wave issue priority of the traversal (s_setprio 0-3); 0 = hardware default
+#ifndef WR_TRACE_PRIO
+#define WR_TRACE_PRIO 0
+#endif
 __global__ void __launch_bounds__(kTraceBlock)
 __attribute__((amdgpu_waves_per_eu(DENSE ? 5 : (CUT ? WR_TRACE_CUT_WAVES_PER_EU : WR_TRACE_WAVES_PER_EU), 8))) WR_NO_PK_FP32 k_trace(DevScene S, TraceQueues Q, DevCounters* ctr, int* fetch) {
   extern __shared__ uint32_t smem[];
+#if WR_TRACE_PRIO > 0
+  __builtin_amdgcn_s_setprio(WR_TRACE_PRIO);  // issue priority over co-resident vertex-kernel waves
+#endif
   TraceCounters tc{0, 0, 0, 0};
   trace_queue<COUNT, SPH, NARROW, STAMP, CUT, DENSE>(S, Q, fetch, smem, tc, ctr->stamps);
   if (COUNT) {
