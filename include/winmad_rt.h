@@ -86,8 +86,9 @@ typedef struct {
   int32_t width, height;
   int32_t spp;               /* SAMPLES_PER_PIXEL: the stratification grid (surfaceIntegrator.cpp:26-32) */
   int32_t max_depth;         /* MAX_TRACING_DEPTH                                          */
-  int32_t sample_begin;      /* first sample index k rendered (RNG key; sharding)          */
-  int32_t sample_count;      /* samples rendered by this call (<= 0: spp - sample_begin)   */
+  int32_t sample_begin;      /* first sample index k rendered (RNG key; sharding), >= 0    */
+  int32_t sample_count;      /* samples rendered by this call (0: spp - sample_begin);
+                                negative, or sample_begin + sample_count > spp: WR_E_ARG    */
   uint32_t seed;
   int32_t time_kernels;
   int32_t count_work;
@@ -163,7 +164,10 @@ int wr_occluded(wr_context* ctx, const wr_ray* rays, const float* targets, int64
  * runIteration :53-265).  film: height*width*3 floats in ImageFilm layout
  * film[x_raster][y_raster] (pre-transpose), accumulated (+=), NOT scaled by
  * 1/iterations.  film_on_device != 0: `film` is a device pointer on the
- * context's device. */
+ * context's device.  The render is ordered after all work submitted before the
+ * call on the legacy null stream (torch's default stream); work on another
+ * caller stream that writes the film must be synchronized by the caller first.
+ * The call returns once the film holds the result (all streams synchronized). */
 int wr_render_bdpt(wr_context* ctx, const wr_bdpt_params* p, float* film, int film_on_device, wr_stats* stats);
 /* SurfaceIntegrator::render (surfaceIntegrator.cpp:14-46) + PathIntegrator::raytracing
  * (pathIntegrator.cpp:29-148).  film[height][width][3] accumulates the per-sample

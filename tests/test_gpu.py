@@ -272,6 +272,39 @@ def test_film_on_device_pointer():
     assert np.allclose(dev.cpu().numpy(), host, rtol=1e-5, atol=1e-7)
 
 
+def test_device_film_is_ordered_after_pending_default_stream_work():
+    """A device film zeroed by torch on the default stream right before the
+    call (no synchronize) is zeroed before the render adds into it: the
+    library's non-blocking streams wait for the legacy null stream."""
+    torch = pytest.importorskip("torch")
+    path = _scenes.torus(64, 64)
+    c = ctx(path)
+    host, _ = c.render_bdpt(64, 64, iterations=1, seed=9)
+    a = torch.randn((4096, 4096), device="cuda:0")
+    dev = torch.full((64, 64, 3), 1e6, dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()
+    for _ in range(8):  # several ms of default-stream work ahead of the zeroing
+        a = a @ a
+        a = a / a.abs().max()
+    dev.zero_()
+    c.render_bdpt(64, 64, iterations=1, seed=9, film_ptr=dev.data_ptr())
+    torch.cuda.synchronize()
+    assert np.allclose(dev.cpu().numpy(), host, rtol=1e-5, atol=1e-7)
+
+
+def test_pt_sample_range_is_validated():
+    c = ctx(_scenes.cbox(16, 12))
+    for kw in ({"sample_begin": -1, "sample_count": 1}, {"sample_begin": 0, "sample_count": -2},
+               {"sample_begin": 3, "sample_count": 2}, {"sample_begin": 5, "sample_count": 0}):
+        with pytest.raises(native.WrError) as e:
+            c.render_path(16, 12, spp=4, **kw)
+        assert e.value.code == native.WR_E_ARG, kw
+    film, _ = c.render_path(16, 12, spp=4, sample_begin=4, sample_count=0)  # empty rest range
+    assert not film.any()
+    with pytest.raises(ValueError):  # host film of the wrong shape / dtype: refused before the call
+        c.render_path(16, 12, spp=4, film=np.zeros((12, 16, 3), np.float64))
+
+
 def _check_trace_vs_oracle(c, oracle_scene, rays9):
     """GPU closest hit (wr_trace_closest) == the oracle's Scene::intersect, bit for bit."""
     oi, of, _, _ = oracle_scene.trace(rays9)

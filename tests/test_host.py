@@ -46,6 +46,28 @@ def test_product_loader_and_kdtree_match_reference(name, maker, tmp_path):
     assert 1 <= info["kd_max_stack"] <= m["depmax"]
 
 
+def test_host_buffers_are_validated_before_the_library_sees_them():
+    """Host films are accumulated in place and rays / targets are read by
+    hipMemcpy: a wrong shape, dtype or layout raises instead of reaching C."""
+    f = np.zeros((4, 5, 3), np.float32)
+    assert native._host_film(f, 4, 5) is f
+    assert native._host_film(None, 4, 5).shape == (4, 5, 3)
+    for bad in (np.zeros((4, 5, 3), np.float64), np.zeros((5, 4, 3), np.float32), np.zeros((4, 4, 3), np.float32),
+                np.zeros((4, 10, 3), np.float32)[:, ::2], np.zeros(60, np.float32), [[0.0] * 3] * 20):
+        with pytest.raises(ValueError):
+            native._host_film(bad, 4, 5)
+    ro = np.zeros((4, 5, 3), np.float32)
+    ro.setflags(write=False)
+    with pytest.raises(ValueError):
+        native._host_film(ro, 4, 5)
+    assert native._rays8(np.zeros((3, 8), np.float64)).dtype == np.float32
+    for bad in (np.zeros((3, 7)), np.zeros(8), np.zeros((2, 3, 8))):
+        with pytest.raises(ValueError):
+            native._rays8(bad)
+    with pytest.raises(ValueError):
+        native.write_image(np.zeros((4, 5), np.float32), "x.ppm")
+
+
 def test_missing_obj_is_skipped_like_the_reference():
     # torus.scene names torus_mirror.obj, absent in the reference's ObjFiles too
     info = native.Scene(_scenes.torus(64, 64)).info()

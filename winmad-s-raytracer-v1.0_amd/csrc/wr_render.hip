@@ -314,12 +314,15 @@ struct wr_context {
   // 8 / 8 -> 864, 16 / 16 -> 894 (twice the memory of 8: ~5 GB per buffer set)
   int npipes = 4;
   hipEvent_t t_ref = nullptr;  // start of the current render (pipelines wait on it)
+  hipEvent_t t_null = nullptr;  // the caller's legacy-stream work before a render
   DevScene ds{};
   Arena scene_mem;
   int64_t scene_bytes = 0;
   DevCounters* ctr = nullptr;  // API traversal
   float* film_tmp = nullptr;
   size_t film_tmp_n = 0;
+  char* api_tmp = nullptr;  // wr_trace_closest / wr_occluded / wr_path_radiance scratch, grown on demand
+  size_t api_tmp_n = 0;
   int grid = 2048;
   int cus = 256;
   float sph_r = 0.f;  // sceneSphere.sceneRadius (scene.cpp:483-487): VCM base radius
@@ -659,6 +662,11 @@ double host_now() {
 // (film clear) and clear their counters.
 void begin_render(wr_context* c, int n, const int time_kernels) {
   c->timing = time_kernels != 0;
+  // a device film may still be written by the caller's work on the legacy
+  // null stream (e.g. torch's default stream zeroing it): the render's streams
+  // are non-blocking, so order them after that work explicitly
+  (void)hipEventRecord(c->t_null, hipStreamLegacy);
+  (void)hipStreamWaitEvent(c->stream, c->t_null, 0);
   (void)hipEventRecord(c->t_ref, c->stream);
   for (int i = 0; i < n; ++i) {
     Pipe& p = c->pipes[i];
@@ -825,7 +833,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   auto* c = new wr_context();
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->t_ref, hipEventDefault) != hipSuccess) {
+      hipEventCreateWithFlags(&c->t_ref, hipEventDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&c->t_null, hipEventDisableTiming) != hipSuccess) {
     wr_destroy(c);
     return fail(WR_E_HIP, "hipStreamCreate failed");
   }
@@ -1091,10 +1100,24 @@ void wr_destroy(wr_context* c) {
     if (p.stream && p.stream != c->stream) (void)hipStreamDestroy(p.stream);
   }
   if (c->t_ref) (void)hipEventDestroy(c->t_ref);
+  if (c->t_null) (void)hipEventDestroy(c->t_null);
   if (c->film_tmp) (void)hipFree(c->film_tmp);
+  if (c->api_tmp) (void)hipFree(c->api_tmp);
   c->scene_mem.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+// the context's API scratch block, at least `bytes` (the stream is idle
+// between API calls: every call ends with a stream synchronize)
+static int api_scratch(wr_context* c, size_t bytes) {
+  if (c->api_tmp_n >= bytes) return WR_OK;
+  if (c->api_tmp) (void)hipFree(c->api_tmp);
+  c->api_tmp = nullptr;
+  c->api_tmp_n = 0;
+  HIPCHK(hipMalloc(&c->api_tmp, bytes));
+  c->api_tmp_n = bytes;
+  return WR_OK;
 }
 
 static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, int64_t n64, wr_hit* hits,
@@ -1104,12 +1127,12 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   if (n64 > (1 << 28)) return fail(WR_E_ARG, "at most 2^28 rays per call");
   const int n = static_cast<int>(n64);
   HIPCHK(hipSetDevice(c->device));
-  // one scratch block: rays, SoA queue, results, counters
-  char* buf = nullptr;
+  // one scratch block: rays, SoA queue, results, counters (kept on the
+  // context: no allocation per call, nothing to free on an error return)
   const size_t nb = size_t(n);
   const size_t bytes = nb * (sizeof(wr_ray) + 4 * 14 + sizeof(wr_hit) + 1) + 16 * 256;
-  HIPCHK(hipMalloc(&buf, bytes));
-  char* q = buf;
+  if (int rc = api_scratch(c, bytes)) return rc;
+  char* q = c->api_tmp;
   auto take = [&](size_t sz) { char* r = q; q += (sz + 255) & ~size_t(255); return r; };
   wr_ray* dr = reinterpret_cast<wr_ray*>(take(nb * sizeof(wr_ray)));
   float* o3 = reinterpret_cast<float*>(take(nb * 12));
@@ -1141,7 +1164,6 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   if (occ) HIPCHK(hipMemcpyAsync(occ, dox, nb, hipMemcpyDeviceToHost, c->stream));
   else HIPCHK(hipMemcpyAsync(hits, dh, nb * sizeof(wr_hit), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  (void)hipFree(buf);
   return WR_OK;
 }
 
@@ -1421,8 +1443,8 @@ int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max
   std::memset(rgb, 0, nf * sizeof(float));
   float* dfilm = nullptr;
   if (int rc = film_target(c, rgb, 0, nf, &dfilm)) return rc;
-  wr_ray* drays = nullptr;
-  HIPCHK(hipMalloc(&drays, size_t(P) * sizeof(wr_ray)));
+  if (int rc = api_scratch(c, size_t(P) * sizeof(wr_ray))) return rc;
+  wr_ray* drays = reinterpret_cast<wr_ray*>(c->api_tmp);
   HIPCHK(hipMemcpyAsync(drays, rays, size_t(P) * sizeof(wr_ray), hipMemcpyHostToDevice, pp.stream));
   begin_render(c, 1, 0);
   PtGroup GA;
@@ -1459,16 +1481,22 @@ int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max
     if (!more) break;
   }
   HIPCHK(hipGetLastError());
-  const int rc = finish_render(c, 1, st, t0);
-  (void)hipFree(drays);
-  if (rc) return rc;
+  if (int rc = finish_render(c, 1, st, t0)) return rc;
   return film_return(c, rgb, 0, nf);
 }
 
 int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int film_on_device, wr_stats* st) {
   if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
   if (prm->width <= 0 || prm->height <= 0 || prm->spp <= 0) return fail(WR_E_ARG, "bad film size / spp");
+  // path-state arrays are indexed up to 3 * P in 32-bit ints
+  if (static_cast<int64_t>(prm->width) * prm->height >= (int64_t(1) << 31) / 4)
+    return fail(WR_E_ARG, "film too large for one context");
   if (prm->max_depth < 0 || prm->max_depth > kSlots - 3) return fail(WR_E_ARG, "max_depth must be in 0..61");
+  // sample k of the spp grid (surfaceIntegrator.cpp:26-32): only 0 <= k < spp exist
+  if (prm->sample_begin < 0 || prm->sample_count < 0 ||
+      static_cast<int64_t>(prm->sample_begin) + prm->sample_count > prm->spp ||
+      prm->sample_begin > prm->spp)
+    return fail(WR_E_ARG, "samples [sample_begin, sample_begin + sample_count) must lie in [0, spp)");
   if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "path tracing needs at least one area light");
   HIPCHK(hipSetDevice(c->device));
   const double t0 = host_now();

@@ -165,6 +165,29 @@ class Scene:
             return f.read()
 
 
+def _rays8(rays8):
+    """(n, 8) float32 C-contiguous rays (o, d, tmin, tmax); anything else raises."""
+    rays8 = np.ascontiguousarray(rays8, np.float32)
+    if rays8.ndim != 2 or rays8.shape[1] != 8:
+        raise ValueError(f"rays8 must have shape (n, 8), got {rays8.shape}")
+    return rays8
+
+
+def _host_film(film, height, width):
+    """The caller's accumulating host film: the library adds height*width*3
+    floats into it in place, so it must be exactly a C-contiguous float32
+    (height, width, 3) array -- no silent conversion (a copy would drop the
+    result, a smaller buffer would be overrun)."""
+    if film is None:
+        return np.zeros((height, width, 3), np.float32)
+    if not isinstance(film, np.ndarray) or film.dtype != np.float32 or film.shape != (height, width, 3) \
+            or not film.flags["C_CONTIGUOUS"] or not film.flags["WRITEABLE"]:
+        raise ValueError(f"film must be a writeable C-contiguous float32 array of shape ({height}, {width}, 3), "
+                         f"got {type(film).__name__} "
+                         f"{getattr(film, 'dtype', None)} {getattr(film, 'shape', None)}")
+    return film
+
+
 def rays_from_arrays(o, d, tmin=0.0, tmax=1e7):
     n = o.shape[0]
     arr = np.zeros((n, 8), np.float32)
@@ -197,7 +220,7 @@ class Context:
 
     def trace_closest(self, rays8):
         """rays8: (n, 8) float32 = o, d, tmin, tmax (d used as given)."""
-        rays8 = np.ascontiguousarray(rays8, np.float32)
+        rays8 = _rays8(rays8)
         n = rays8.shape[0]
         hits = np.zeros(n, dtype=np.dtype([("t", "f4"), ("p", "f4", 3), ("n", "f4", 3), ("prim", "i4"),
                                            ("inside", "i4"), ("mat_id", "i4")]))
@@ -206,9 +229,11 @@ class Context:
         return hits
 
     def occluded(self, rays8, targets):
-        rays8 = np.ascontiguousarray(rays8, np.float32)
+        rays8 = _rays8(rays8)
         targets = np.ascontiguousarray(targets, np.float32)
         n = rays8.shape[0]
+        if targets.shape != (n, 3):
+            raise ValueError(f"targets must have shape ({n}, 3), got {targets.shape}")
         out = np.zeros(n, np.uint8)
         check(lib().wr_occluded(self.h, rays8.ctypes.data_as(C.POINTER(WrRay)),
                                 targets.ctypes.data_as(C.POINTER(C.c_float)), n,
@@ -225,8 +250,7 @@ class Context:
         if film_ptr is not None:
             check(lib().wr_render_bdpt(self.h, C.byref(p), C.c_void_p(film_ptr), 1, C.byref(st)))
             return None, st
-        if film is None:
-            film = np.zeros((height, width, 3), np.float32)
+        film = _host_film(film, height, width)
         check(lib().wr_render_bdpt(self.h, C.byref(p), film.ctypes.data_as(C.c_void_p), 0, C.byref(st)))
         return film, st
 
@@ -240,15 +264,14 @@ class Context:
         if film_ptr is not None:
             check(lib().wr_render_vcm(self.h, C.byref(p), C.c_void_p(film_ptr), 1, C.byref(st)))
             return None, st
-        if film is None:
-            film = np.zeros((height, width, 3), np.float32)
+        film = _host_film(film, height, width)
         check(lib().wr_render_vcm(self.h, C.byref(p), film.ctypes.data_as(C.c_void_p), 0, C.byref(st)))
         return film, st
 
     def path_radiance(self, rays8, max_depth=7, seed=5489, sample=0):
         """PathIntegrator::raytracing for each ray of rays8 ((n, 8) float32:
         o, d, tmin, tmax; d used as given).  Returns (n, 3) radiance, stats."""
-        rays8 = np.ascontiguousarray(rays8, np.float32)
+        rays8 = _rays8(rays8)
         n = rays8.shape[0]
         out = np.zeros((n, 3), np.float32)
         st = WrStats()
@@ -265,8 +288,7 @@ class Context:
         if film_ptr is not None:
             check(lib().wr_render_path(self.h, C.byref(p), C.c_void_p(film_ptr), 1, C.byref(st)))
             return None, st
-        if film is None:
-            film = np.zeros((height, width, 3), np.float32)
+        film = _host_film(film, height, width)
         check(lib().wr_render_path(self.h, C.byref(p), film.ctypes.data_as(C.c_void_p), 0, C.byref(st)))
         return film, st
 
@@ -274,6 +296,8 @@ class Context:
 def write_ppm(film, path, scale=1.0, gamma=2.2, transpose=False):
     """ImageFilm::outputImage pipeline (film.cpp:39-64) to a binary PPM."""
     film = np.ascontiguousarray(film, np.float32)
+    if film.ndim != 3 or film.shape[2] != 3:
+        raise ValueError(f"film must have shape (height, width, 3), got {film.shape}")
     h, w = film.shape[:2]
     check(lib().wr_film_write_ppm(film.ctypes.data_as(C.POINTER(C.c_float)), h, w, scale, gamma,
                                   1 if transpose else 0, os.fsencode(path)))
@@ -282,6 +306,8 @@ def write_ppm(film, path, scale=1.0, gamma=2.2, transpose=False):
 def write_image(film, path, scale=1.0, gamma=2.2, transpose=False):
     """ImageFilm::outputImage into .ppm / .bmp / .png, or linear .pfm."""
     film = np.ascontiguousarray(film, np.float32)
+    if film.ndim != 3 or film.shape[2] != 3:
+        raise ValueError(f"film must have shape (height, width, 3), got {film.shape}")
     h, w = film.shape[:2]
     check(lib().wr_film_write_image(film.ctypes.data_as(C.POINTER(C.c_float)), h, w, scale, gamma,
                                     1 if transpose else 0, os.fsencode(path)))
