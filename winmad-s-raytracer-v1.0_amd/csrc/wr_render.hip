@@ -664,8 +664,10 @@ void begin_render(wr_context* c, int n, const int time_kernels) {
   c->timing = time_kernels != 0;
   // a device film may still be written by the caller's work on the legacy
   // null stream (e.g. torch's default stream zeroing it): the render's streams
-  // are non-blocking, so order them after that work explicitly
-  (void)hipEventRecord(c->t_null, hipStreamLegacy);
+  // are non-blocking, so order them after that work explicitly.  The null
+  // stream is named as 0: the hipStreamLegacy handle ((hipStream_t)1) is not
+  // understood by the older HIP runtime PyTorch loads first (segfault)
+  (void)hipEventRecord(c->t_null, nullptr);
   (void)hipStreamWaitEvent(c->stream, c->t_null, 0);
   (void)hipEventRecord(c->t_ref, c->stream);
   for (int i = 0; i < n; ++i) {
