@@ -197,6 +197,9 @@ def main():
     ap.add_argument("--cpu-paths", type=int, default=1000000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting replay")
+    ap.add_argument("--trace", choices=["reference", "bvh"], default="reference",
+                    help="traversal: the reference's KD walk, or the verified BVH search with KD "
+                         "fallback (same answers, DESIGN.md section 4b)")
     ap.add_argument("--no-cut", action="store_true",
                     help="c3/vcm: shadow rays run to the end of the walk (no occlusion cutoff)")
     args = ap.parse_args()
@@ -224,6 +227,8 @@ def main():
     scene_path = make_scene(args.config, W, H, tmp)
     sc = native.Scene(scene_path)
     ctx = native.Context(sc, local)
+    if args.trace == "bvh":
+        ctx.set_trace_mode(native.TRACE_BVH)
     film = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
 
     # one step = one iteration (BDPT) / one sample index of the spp grid (PT);
@@ -271,6 +276,18 @@ def main():
         _, cst = render(it0, K, count_work=1, film=None)
         assert cst.closest_rays == st.closest_rays and cst.shadow_rays == st.shadow_rays
         total_bytes = algorithmic_bytes(rays, cst.inner_visits, cst.leaf_visits, cst.prim_refs, cst.prim_tests)
+        bvh = None
+        if args.trace == "bvh":
+            # the KD counters cover only the fallback rays (their own B_ray terms
+            # minus the ray load / hit store, which every ray pays once here):
+            # + 64 B per BVH node record, 48 B per triangle record, 8 B per KD
+            # path entry replayed
+            total_bytes += 64.0 * cst.bvh_nodes + 48.0 * cst.bvh_tests + 8.0 * cst.kd_replay_steps \
+                - 48.0 * cst.fallback_rays
+            bvh = {"nodes_per_ray": round(cst.bvh_nodes / rays, 2), "tests_per_ray": round(cst.bvh_tests / rays, 2),
+                   "replay_steps_per_ray": round(cst.kd_replay_steps / rays, 2),
+                   "fallback_frac": round(cst.fallback_rays / rays, 5),
+                   "kd_tests_per_fallback_ray": round(cst.prim_tests / max(1, cst.fallback_rays), 1)}
         per_launch = total_bytes / max(1, trace_launches)
         # launches of the concurrent pipelines overlap: the rate is the bytes over
         # the union of the traversal launch intervals (HIP events on each stream);
@@ -306,6 +323,11 @@ def main():
                     "tests_per_ray": round(cst.prim_tests / rays, 2),
                     "nodes_per_ray": round((cst.inner_visits + cst.leaf_visits) / rays, 2),
                     "trace_share_of_wall": round(st.trace_wall_ms / 1e3 / max(1e-9, elapsed), 3)}
+        if bvh:
+            roofline["kernel"] = "k_trace_fast (verified BVH closest hit) + k_trace over its fallback rays"
+            roofline["algorithmic_bytes"] = ("BVH: 48 B per ray + 64 B per node + 48 B per triangle test + 8 B per "
+                                             "KD path entry replayed; fallback rays: SURVEY.md 8(d) B_ray")
+            roofline["bvh"] = bvh
 
     cpu = port = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -331,7 +353,7 @@ def main():
                                    + ("" if pt else ", maxPathLength 10" if cfg["integrator"] == "vcm"
                                       else ", controlLength 3, maxPathLength 10"),
                        "scene_config": args.config.upper(), "width": W, "height": H,
-                       "steps_per_gpu": K, "parallelism": f"sample-batch x{world}",
+                       "steps_per_gpu": K, "parallelism": f"sample-batch x{world}", "trace": args.trace,
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
             "spp_per_sec": round(W * H * K * world / elapsed, 1),
             "rays_per_step": round(total_rays / (K * world)),

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define WR_API_VERSION 3
+#define WR_API_VERSION 4
 
 enum {
   WR_OK = 0,
@@ -128,6 +128,12 @@ typedef struct {
   int64_t vm_merged;         /* VCM: RangeQuery::process merges (non-black BSDF)   */
   int64_t prim_tests;        /* count_work only: primitive tests run; < prim_refs
                                 by the (ray, primitive) repeats skipped            */
+  /* WR_TRACE_BVH only (wr_set_trace_mode), count_work: verified-BVH work.  The
+   * KD counters above then cover only the fallback rays.                       */
+  int64_t bvh_nodes;         /* BVH nodes visited (64-byte records)             */
+  int64_t bvh_tests;         /* triangle tests of the BVH search                */
+  int64_t kd_replay_steps;   /* KD path entries replayed (membership checks)    */
+  int64_t fallback_rays;     /* rays handed to the faithful KD traversal        */
 } wr_stats;
 
 /* ---- scene (Scene::init, scene/scene.cpp:469-489 + loadScene :259-467) ---- */
@@ -148,6 +154,18 @@ void wr_destroy(wr_context* ctx);
  * (GPU_MAX_HW_QUEUES, HIP default 4) up to 16, or env WR_PIPES.
  * GPU-specific scheduling; no reference counterpart. */
 int wr_set_pipelines(wr_context* ctx, int n);
+
+/* Traversal mode of every later call on the context.
+ *   WR_TRACE_REFERENCE (default): the reference's KD tree, walked exactly as
+ *     KDtreeAccel::traverse (scene/KDtreeAccel.cpp:309-388) walks it.
+ *   WR_TRACE_BVH: a BVH search for the smallest hit, accepted only when the
+ *     winner is provably the reference's (unique within EPS, and in a KD leaf
+ *     the reference's traversal reaches); every other ray is traced in the
+ *     reference mode.  Same rays, same (t, primitive) answers; see DESIGN.md 4b.
+ * Env WR_TRACE_BVH=1 selects the BVH mode at wr_create.  WR_E_SCENE if the
+ * scene cannot use it (spheres). */
+enum { WR_TRACE_REFERENCE = 0, WR_TRACE_BVH = 1 };
+int wr_set_trace_mode(wr_context* ctx, int mode);
 
 /* ---- traversal ---- */
 /* Scene::intersect (scene/scene.cpp:21-43) -> KDtreeAccel::traverse

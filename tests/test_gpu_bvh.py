@@ -1,0 +1,163 @@
+"""GPU parity of the verified-BVH traversal mode (WR_TRACE_BVH).
+
+The BVH mode must return exactly what the reference's KD walk returns: the same
+winning primitive and the same float t for every ray (bit-exact), the same
+occlusion answers, and therefore renders with the same ray set.  Checked
+against the reference mode of the same library (itself bit-exact against the
+reference's own golden corpus, tests/test_gpu.py) on
+  * the golden corpus (reference outputs, tests/golden/rays_*.txt);
+  * large ray corpora built like the renderer's rays: camera rays, random rays,
+    extension rays leaving surface hits (origin + EPS along d, the BDPT / PT
+    extension rule) in every direction including grazing ones, and shadow rays
+    from hit points (no offset, BDPT's connections) to points on other surfaces;
+  * full BDPT / VCM / PT renders: identical ray counts, films equal up to the
+    order of float atomics.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _scenes
+from test_gpu import _check_golden_corpus, normalize_f32
+from winmad_rt import native, scenes
+
+pytestmark = pytest.mark.gpu
+EPS = np.float32(1e-3)
+
+_cache = {}
+
+
+def pair(path):
+    """(reference-mode context, BVH-mode context) on one scene."""
+    if path not in _cache:
+        s = native.Scene(path)
+        a = native.Context(s, 0)
+        b = native.Context(s, 0)
+        b.set_trace_mode(native.TRACE_BVH)
+        _cache[path] = (s, a, b)
+    return _cache[path][1], _cache[path][2]
+
+
+def big_torus(W, H):
+    p = os.path.join(_scenes._DIR, "torus1m.obj")
+    if not os.path.exists(p):
+        scenes.synth_torus_obj(p)
+    return _scenes.path(f"torus1m_{W}x{H}.scene", scenes.torus_scene(W, H, "bdpt", torus_obj=p))
+
+
+SCENES = [("torus", lambda: _scenes.torus(256, 256)), ("cbox", lambda: _scenes.cbox(256, 192))]
+
+
+@pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),
+                                        ("cbox64x48", lambda: _scenes.cbox(64, 48))])
+def test_bvh_golden_corpus_bit_exact(name, maker):
+    _check_golden_corpus(pair(maker())[1], name)
+
+
+def test_bvh_mode_refused_with_spheres():
+    c = native.Context(native.Scene(_scenes.spheres(64, 64)), 0)
+    with pytest.raises(native.WrError) as e:
+        c.set_trace_mode(native.TRACE_BVH)
+    assert e.value.code == native.WR_E_SCENE
+
+
+def _unit(v):
+    return normalize_f32(v.astype(np.float32))
+
+
+def _corpus(ref, n, seed):
+    """Rays shaped like the renderer's: camera / random rays, then extension
+    and shadow rays spawned from their hits."""
+    rng = np.random.default_rng(seed)
+    # first generation: random origins inside a big box around the scene, random dirs
+    info_o = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    hits0 = None
+    for scale in (2000.0, 400.0, 60.0, 3.0):
+        o = (info_o * scale).astype(np.float32)
+        d = _unit(rng.normal(size=(n, 3)))
+        h = ref.trace_closest(native.rays_from_arrays(o, d))
+        if hits0 is None or (h["prim"] >= 0).mean() > (hits0[2]["prim"] >= 0).mean():
+            hits0 = (o, d, h)
+    o0, d0, h0 = hits0
+    hit = h0["prim"] >= 0
+    p = h0["p"][hit].astype(np.float32)
+    nn = h0["n"][hit].astype(np.float32)
+    m = p.shape[0]
+    # extension rays: cosine-ish around +-n, a quarter of them grazing
+    side = np.where(rng.random(m) < 0.5, 1.0, -1.0).astype(np.float32)[:, None]
+    dd = _unit(nn * side + rng.normal(size=(m, 3)).astype(np.float32))
+    g = rng.random(m) < 0.25
+    t = np.cross(nn[g], rng.normal(size=(g.sum(), 3)).astype(np.float32))
+    dd[g] = _unit(t + nn[g] * side[g] * rng.uniform(-1e-3, 1e-3, (g.sum(), 1)).astype(np.float32))
+    ext_o = (p + dd * EPS).astype(np.float32)
+    # shadow rays: hit point -> another hit point, no offset (BDPT connections)
+    q = p[rng.permutation(m)]
+    sd = _unit(q - p)
+    ok = np.isfinite(sd).all(axis=1)
+    rays = [native.rays_from_arrays(o0, d0), native.rays_from_arrays(ext_o, dd),
+            native.rays_from_arrays(p[ok], sd[ok])]
+    return np.concatenate(rays), (p[ok], sd[ok], q[ok])
+
+
+def _same_hits(a, b):
+    same_prim = a["prim"] == b["prim"]
+    same_t = (a["t"].view(np.int32) == b["t"].view(np.int32)) | (a["prim"] < 0)
+    return same_prim & same_t
+
+
+@pytest.mark.parametrize("name,maker", SCENES + [("torus1m", lambda: big_torus(64, 64))])
+def test_bvh_matches_reference_mode_on_ray_corpus(name, maker):
+    ref, fast = pair(maker())
+    n = 400_000 if name != "torus1m" else 150_000
+    rays, (p, sd, q) = _corpus(ref, n, 1234)
+    a = ref.trace_closest(rays)
+    b = fast.trace_closest(rays)
+    ok = _same_hits(a, b)
+    assert ok.all(), (name, int((~ok).sum()), rays.shape[0], np.nonzero(~ok)[0][:8])
+    for fld in ("p", "n", "inside", "mat_id"):
+        assert np.array_equal(a[fld], b[fld]), fld
+    r8 = native.rays_from_arrays(p, sd)
+    assert np.array_equal(ref.occluded(r8, q), fast.occluded(r8, q))
+
+
+def _film_close(fa, fb):
+    fa = fa.astype(np.float64)
+    fb = fb.astype(np.float64)
+    rms = np.sqrt((fa ** 2).mean())
+    return np.sqrt(((fa - fb) ** 2).mean()) <= 1e-5 * max(rms, 1e-30)
+
+
+def test_bvh_bdpt_render_same_rays_and_film():
+    ref, fast = pair(_scenes.torus(256, 256))
+    fa, sa = ref.render_bdpt(256, 256, iterations=4, seed=5489, count_work=True)
+    fb, sb = fast.render_bdpt(256, 256, iterations=4, seed=5489, count_work=True)
+    assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
+    assert _film_close(fa, fb)
+    rays = sb.closest_rays + sb.shadow_rays
+    assert sb.bvh_nodes > 0 and sb.bvh_tests > 0
+    assert sb.fallback_rays < 0.1 * rays, (sb.fallback_rays, rays)
+    # the BVH search does far less work than the reference's walk
+    assert sb.bvh_tests + sb.prim_tests < 0.5 * sa.prim_tests
+
+
+def test_bvh_vcm_and_pt_renders_same_rays_and_film():
+    ref, fast = pair(_scenes.torus(128, 128))
+    fa, sa = ref.render_vcm(128, 128, iterations=2, seed=7)
+    fb, sb = fast.render_vcm(128, 128, iterations=2, seed=7)
+    assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
+    assert sa.vm_merged == sb.vm_merged
+    assert _film_close(fa, fb)
+    ref, fast = pair(_scenes.cbox(128, 96))
+    fa, sa = ref.render_path(128, 96, spp=4, max_depth=7, seed=11)
+    fb, sb = fast.render_path(128, 96, spp=4, max_depth=7, seed=11)
+    assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
+    assert _film_close(fa, fb)
+
+
+def test_bvh_bdpt_render_1m_triangles():
+    ref, fast = pair(big_torus(192, 108))
+    fa, sa = ref.render_bdpt(192, 108, iterations=2, seed=3)
+    fb, sb = fast.render_bdpt(192, 108, iterations=2, seed=3, count_work=True)
+    assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
+    assert _film_close(fa, fb)

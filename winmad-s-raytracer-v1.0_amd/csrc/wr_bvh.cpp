@@ -1,0 +1,299 @@
+// Host build of the verified-BVH fast path (wr_bvh.h): a binned-SAH BVH over the
+// scene's triangles, and for every triangle the root-to-leaf paths of the
+// reference KD leaves that hold it (KDtreeAccel::buildTree,
+// src/scene/KDtreeAccel.cpp:118-307, as restated in wr_scene.cpp).
+#include "wr_bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "wr_scene.h"
+
+namespace wrf {
+namespace {
+
+struct Box {
+  float lo[3] = {INFINITY, INFINITY, INFINITY};
+  float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], b.lo[k]);
+      hi[k] = std::max(hi[k], b.hi[k]);
+    }
+  }
+  void grow(const float* p) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], p[k]);
+      hi[k] = std::max(hi[k], p[k]);
+    }
+  }
+  bool empty() const { return !(lo[0] <= hi[0]); }
+  double area() const {
+    if (empty()) return 0.0;
+    const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+    return 2.0 * (x * y + x * z + y * z);
+  }
+};
+
+constexpr int kBins = 16;
+
+struct Builder {
+  const std::vector<Box>& box;
+  const std::vector<float>& cen;  // 3 per triangle
+  std::vector<int>& idx;
+  FastHost& out;
+  const wr::Scene& s;
+  const std::vector<int>& tri_prim;
+
+  int leaf_link(int b, int e) {
+    const int first = static_cast<int>(out.tris.size());
+    for (int i = b; i < e; ++i) {
+      const wr::Prim& p = s.prims[tri_prim[idx[i]]];
+      TriRec r;
+      // A..F exactly as Triangle::hit forms them (triangle.cpp:24-30)
+      r.a[0] = p.p0.x;
+      r.a[1] = p.p0.y;
+      r.a[2] = p.p0.z;
+      r.a[3] = p.p0.x - p.p1.x;
+      r.b[0] = p.p0.y - p.p1.y;
+      r.b[1] = p.p0.z - p.p1.z;
+      r.b[2] = p.p0.x - p.p2.x;
+      r.b[3] = p.p0.y - p.p2.y;
+      r.c[0] = p.p0.z - p.p2.z;
+      const int32_t prim = tri_prim[idx[i]];
+      std::memcpy(&r.c[1], &prim, 4);
+      // the primitive's KD leaf list (prim_leaf range): no extra lookup when it wins
+      const int32_t lb = out.prim_leaf_off[static_cast<size_t>(prim)];
+      const int32_t ln = out.prim_leaf_off[static_cast<size_t>(prim) + 1] - lb;
+      std::memcpy(&r.c[2], &lb, 4);
+      std::memcpy(&r.c[3], &ln, 4);
+      out.tris.push_back(r);
+    }
+    ++out.leaves;
+    return ~((first << 3) | (e - b - 1));
+  }
+
+  Box bounds(int b, int e) const {
+    Box r;
+    for (int i = b; i < e; ++i) r.grow(box[idx[i]]);
+    return r;
+  }
+
+  // split [b, e) by binned SAH over the centroids; returns the split position
+  // (b < m < e) or -1 when a leaf is cheaper (only allowed for e - b <= kMaxLeaf)
+  int split(int b, int e, const Box& nb) {
+    const int n = e - b;
+    Box cb;
+    for (int i = b; i < e; ++i) cb.grow(&cen[3 * idx[i]]);
+    double best = INFINITY;
+    int bax = -1, bbin = 0;
+    for (int ax = 0; ax < 3; ++ax) {
+      const float ext = cb.hi[ax] - cb.lo[ax];
+      if (!(ext > 0.f)) continue;
+      Box bb[kBins];
+      int bc[kBins] = {0};
+      const float sc = kBins / ext;
+      for (int i = b; i < e; ++i) {
+        int k = static_cast<int>((cen[3 * idx[i] + ax] - cb.lo[ax]) * sc);
+        k = std::min(kBins - 1, std::max(0, k));
+        bb[k].grow(box[idx[i]]);
+        ++bc[k];
+      }
+      Box rb[kBins];
+      int rc[kBins];
+      Box acc;
+      int an = 0;
+      for (int k = kBins - 1; k > 0; --k) {
+        acc.grow(bb[k]);
+        an += bc[k];
+        rb[k] = acc;
+        rc[k] = an;
+      }
+      Box la;
+      int ln = 0;
+      for (int k = 0; k < kBins - 1; ++k) {
+        la.grow(bb[k]);
+        ln += bc[k];
+        if (ln == 0 || rc[k + 1] == 0) continue;
+        const double cost = la.area() * ln + rb[k + 1].area() * rc[k + 1];
+        if (cost < best) {
+          best = cost;
+          bax = ax;
+          bbin = k + 1;
+        }
+      }
+    }
+    if (n <= kMaxLeaf) {
+      // leaf cost n tests vs 1 node + the children's tests
+      const double leaf = nb.area() * n;
+      if (bax < 0 || best + 0.5 * nb.area() >= leaf) return -1;
+    }
+    if (bax < 0) return b + n / 2;  // all centroids equal: split by index
+    const float ext = cb.hi[bax] - cb.lo[bax];
+    const float sc = kBins / ext;
+    auto mid = std::partition(idx.begin() + b, idx.begin() + e, [&](int t) {
+      int k = static_cast<int>((cen[3 * t + bax] - cb.lo[bax]) * sc);
+      k = std::min(kBins - 1, std::max(0, k));
+      return k < bbin;
+    });
+    int m = static_cast<int>(mid - idx.begin());
+    if (m <= b || m >= e) m = b + n / 2;
+    return m;
+  }
+
+  // child link for [b, e) with bounds cb
+  int child(int b, int e, const Box& cb, int depth) {
+    if (e - b <= kMaxLeaf) {
+      const int m = split(b, e, cb);
+      if (m < 0) return leaf_link(b, e);
+      return inner(b, e, m, depth);
+    }
+    return inner(b, e, split(b, e, cb), depth);
+  }
+
+  int inner(int b, int e, int m, int depth) {
+    out.depth = std::max(out.depth, depth);
+    if (depth > kMaxBvhDepth) {
+      out.ok = false;
+      out.why = "BVH deeper than the traversal stack";
+      return leaf_link(b, std::min(e, b + kMaxLeaf));
+    }
+    const int at = static_cast<int>(out.nodes.size());
+    out.nodes.emplace_back();
+    const Box l = bounds(b, m), r = bounds(m, e);
+    const int cl = child(b, m, l, depth + 1);
+    const int cr = child(m, e, r, depth + 1);
+    BNode& nd = out.nodes[static_cast<size_t>(at)];
+    for (int k = 0; k < 3; ++k) {
+      nd.b[k] = l.lo[k];
+      nd.b[3 + k] = l.hi[k];
+      nd.b[6 + k] = r.lo[k];
+      nd.b[9 + k] = r.hi[k];
+    }
+    nd.c[0] = cl;
+    nd.c[1] = cr;
+    nd.c[2] = nd.c[3] = 0;
+    return at;
+  }
+};
+
+void kd_paths(const wr::Scene& s, FastHost& out) {
+  const size_t np = s.prims.size();
+  std::vector<std::vector<int32_t>> per(np);
+  std::vector<uint32_t> cur;  // entries of the current path
+  struct Item {
+    int node;
+    int depth;            // entries on the path to this node
+    uint32_t e0, e1;      // the entry that led here (valid if depth > 0)
+  };
+  std::vector<Item> st;
+  st.push_back({0, 0, 0u, 0u});
+  while (!st.empty()) {
+    const Item it = st.back();
+    st.pop_back();
+    cur.resize(2 * static_cast<size_t>(it.depth));
+    if (it.depth > 0) {
+      cur[2 * (it.depth - 1)] = it.e0;
+      cur[2 * (it.depth - 1) + 1] = it.e1;
+    }
+    const wr::KdNode& k = s.nodes[static_cast<size_t>(it.node)];
+    if (k.axis >= 0) {
+      uint32_t bits;
+      std::memcpy(&bits, &k.split, 4);
+      st.push_back({k.right, it.depth + 1, bits, static_cast<uint32_t>(k.axis) | 4u});
+      st.push_back({it.node + 1, it.depth + 1, bits, static_cast<uint32_t>(k.axis)});
+    } else {
+      // records start on 16-byte boundaries (even entries): read as uint4
+      if ((out.path.size() / 2) & 1) {
+        out.path.push_back(0u);
+        out.path.push_back(0u);
+      }
+      const int32_t off = static_cast<int32_t>(out.path.size() / 2);
+      out.path.push_back(static_cast<uint32_t>(it.depth));
+      out.path.push_back(0u);
+      out.path.insert(out.path.end(), cur.begin(), cur.end());
+      for (int i = 0; i < k.count; ++i) {
+        const int p = s.refs[static_cast<size_t>(k.first + i)];
+        if (per[static_cast<size_t>(p)].empty() || per[static_cast<size_t>(p)].back() != off)
+          per[static_cast<size_t>(p)].push_back(off);
+      }
+    }
+  }
+  out.prim_leaf_off.assign(np + 1, 0);
+  for (size_t p = 0; p < np; ++p) out.prim_leaf_off[p + 1] = out.prim_leaf_off[p] + static_cast<int32_t>(per[p].size());
+  out.prim_leaf.reserve(static_cast<size_t>(out.prim_leaf_off[np]));
+  for (size_t p = 0; p < np; ++p) out.prim_leaf.insert(out.prim_leaf.end(), per[p].begin(), per[p].end());
+  // the replay reads 8 entries at a time: pad past the last record
+  out.path.resize(out.path.size() + 2 * 8, 0u);
+}
+
+}  // namespace
+
+void build_fast(const wr::Scene& s, FastHost& out) {
+  out = FastHost();
+  for (const auto& p : s.prims)
+    if (p.type != wr::kTri) {
+      out.why = "scene has spheres (the fast path covers triangles only)";
+      return;
+    }
+  if (s.prims.empty() || s.nodes.empty()) {
+    out.why = "empty scene";
+    return;
+  }
+  const size_t n = s.prims.size();
+  std::vector<Box> box(n);
+  std::vector<float> cen(3 * n);
+  std::vector<int> tri_prim(n), idx(n);
+  for (size_t i = 0; i < n; ++i) {
+    const wr::Prim& p = s.prims[i];
+    const float v[3][3] = {{p.p0.x, p.p0.y, p.p0.z}, {p.p1.x, p.p1.y, p.p1.z}, {p.p2.x, p.p2.y, p.p2.z}};
+    Box b;
+    for (auto& q : v) b.grow(q);
+    // the EPS-fattened triangle of Triangle::hit, with a tenfold margin
+    auto len = [](const float* a, const float* c) {
+      const double x = a[0] - c[0], y = a[1] - c[1], z = a[2] - c[2];
+      return std::sqrt(x * x + y * y + z * z);
+    };
+    const double m = kBoxGrow * (len(v[0], v[1]) + len(v[0], v[2])) + 1e-6 * (1.0 + std::max({std::fabs(b.lo[0]),
+        std::fabs(b.lo[1]), std::fabs(b.lo[2]), std::fabs(b.hi[0]), std::fabs(b.hi[1]), std::fabs(b.hi[2])}));
+    for (int k = 0; k < 3; ++k) {
+      b.lo[k] = std::nextafter(static_cast<float>(b.lo[k] - m), -INFINITY);
+      b.hi[k] = std::nextafter(static_cast<float>(b.hi[k] + m), INFINITY);
+      cen[3 * i + k] = 0.5f * (b.lo[k] + b.hi[k]);
+    }
+    box[i] = b;
+    tri_prim[i] = static_cast<int>(i);
+    idx[i] = static_cast<int>(i);
+  }
+  out.ok = true;
+  kd_paths(s, out);  // first: the triangle records carry their prim_leaf range
+  out.tris.reserve(n);
+  out.nodes.reserve(2 * n / kMaxLeaf + 8);
+  Builder B{box, cen, idx, out, s, tri_prim};
+  // node 0 is always inner (the traversal starts from its two children)
+  const int nn = static_cast<int>(n);
+  if (nn <= kMaxLeaf) {
+    out.nodes.emplace_back();
+    Box all = B.bounds(0, nn);
+    const int l = B.leaf_link(0, nn);
+    BNode& nd = out.nodes[0];
+    for (int k = 0; k < 3; ++k) {
+      nd.b[k] = all.lo[k];
+      nd.b[3 + k] = all.hi[k];
+      nd.b[6 + k] = INFINITY;
+      nd.b[9 + k] = -INFINITY;
+    }
+    nd.c[0] = l;
+    nd.c[1] = ~0;  // never reached: empty box
+    nd.c[2] = nd.c[3] = 0;
+    out.depth = 1;
+  } else {
+    const Box all = B.bounds(0, nn);
+    int m = B.split(0, nn, all);
+    if (m < 0) m = nn / 2;
+    B.inner(0, nn, m, 1);
+  }
+}
+
+}  // namespace wrf

@@ -1,0 +1,89 @@
+// Verified BVH closest hit: a second acceleration structure that finds the
+// same winner as the reference's KD traversal (KDtreeAccel::traverse,
+// src/scene/KDtreeAccel.cpp:309-388) with far less work, or hands the ray to
+// the faithful KD kernel (wr_traverse.h) when it cannot prove that.
+//
+// Why the winner can be found without the reference's tree.  The reference
+// tests, in leaf order, every triangle of every leaf its ray crosses (no early
+// exit) and keeps a hit iff `cmp(t - best) < 0` (first found wins within EPS).
+// Triangle::hit (triangle.cpp:22-87) depends only on (ray, triangle).  Let m be
+// the hit with the smallest t over ALL triangles of the scene.  If
+//   (1) m is in a leaf the reference visits (checked by replaying the
+//       reference's near/far decisions down the root-to-leaf path of m's
+//       leaves with the same float operations), and
+//   (2) every other triangle's hit t_h has fl(t_h - t_m) > EPS,
+// then m is taken whenever the reference reaches it (every earlier best is an
+// accepted hit of another triangle, so cmp(t_m - best) < 0) and nothing after
+// it can replace it (t_h >= t_m gives cmp(t_h - t_m) >= 0).  So the reference
+// returns exactly (t_m, m).  A miss everywhere is a miss for the reference.
+// Any ray failing (1) or (2) -- near-ties (e.g. hits on a shared mesh edge,
+// where the EPS-fattened barycentrics of both triangles accept), or a smallest
+// hit in a leaf the reference never reaches -- is traced by the faithful kernel.
+//
+// The BVH search must report every hit with t <= t_m + 2 EPS.  Its boxes are
+// the triangles' boxes grown by the EPS fattening of Triangle::hit
+// (barycentrics down to -EPS, so hits lie up to ~EPS x edge outside the
+// triangle) with a tenfold margin, and each ray widens them further by
+// 1e-4 x (its distance + 1) for the float error of the Cramer solve.  That
+// covers every test whose barycentric error is below ~9 EPS, i.e. every ray not
+// within ~1e-3 rad of grazing the triangle's plane; a test closer to
+// degenerate (denominator at the rounding noise of the Cramer sums) yields a
+// t the reference itself only gets by rounding, and is the documented residual
+// (measured 0 mismatches against the faithful kernel).
+#pragma once
+#include <stdint.h>
+
+namespace wrf {
+
+// 64 bytes: the two children's boxes and links.
+//   b[0..5]  child 0 box (lo.xyz, hi.xyz), b[6..11] child 1 box
+//   c[0], c[1] links: >= 0 inner node index; < 0 leaf, ~link = first << 3 | (count - 1)
+//   (an empty child has an inverted box and never hits)
+struct BNode {
+  float b[12];
+  int32_t c[4];
+};
+static_assert(sizeof(BNode) == 64, "BVH node record is 64 bytes");
+
+// 48 bytes per triangle, in BVH leaf order, laid out as the KD refs
+// (wr_traverse.h): (p0.xyz, A), (B, C, D, E), (F, prim, lb, ln) with A..F =
+// p0 - p1, p0 - p2 exactly as Triangle::hit forms them and [lb, lb + ln) the
+// primitive's range of prim_leaf.
+struct TriRec {
+  float a[4], b[4], c[4];
+};
+static_assert(sizeof(TriRec) == 48, "BVH triangle record is 48 bytes");
+
+// KD membership data.  Leaf path record at path[off] (off even: 16-byte
+// aligned): (n, 0) then n entries (split bits, axis | went_right << 2) from the
+// root down; 8 zero entries pad the array's end.  prim_leaf[
+// prim_leaf_off[p] .. prim_leaf_off[p+1]) = path offsets of the KD leaves that
+// hold primitive p.
+constexpr int kMaxLeaf = 4;      // triangles per BVH leaf
+constexpr int kMaxBvhDepth = 62;  // deeper builds disable the fast path
+constexpr float kBoxGrow = 0.01f;  // x (|p0 - p1| + |p0 - p2|): 10x the EPS fattening
+constexpr float kRayGrow = 1e-4f;  // x (ray length to the search bound + 1), per ray
+
+}  // namespace wrf
+
+// host build (declared in both HIP compile passes; defined in wr_bvh.cpp)
+#include <string>
+#include <vector>
+namespace wr {
+struct Scene;
+}
+namespace wrf {
+struct FastHost {
+  std::vector<BNode> nodes;
+  std::vector<TriRec> tris;
+  std::vector<int32_t> prim_leaf_off, prim_leaf;
+  std::vector<uint32_t> path;  // pairs
+  int depth = 0;               // deepest node chain (stack bound)
+  int leaves = 0;
+  bool ok = false;
+  std::string why;  // when !ok: why the fast path is off for this scene
+};
+// Build the BVH over the scene's triangles and the KD membership data.  Scenes
+// with spheres keep the faithful traversal only (ok = false).
+void build_fast(const wr::Scene& s, FastHost& out);
+}  // namespace wrf

@@ -1,0 +1,443 @@
+// Verified-BVH closest hit on gfx950 (see wr_bvh.h for why its answers equal the
+// reference's KDtreeAccel::traverse, src/scene/KDtreeAccel.cpp:309-388).
+//
+// Two launches over the same ray queues as k_trace:
+//   k_trace_fast  every ray gets a closest-hit search over a binary BVH
+//                 (64-byte nodes holding both children's boxes, 48-byte
+//                 triangle records).  It keeps the smallest hit (t1, p1) --
+//                 written as the ray's result -- and the smallest hit of any
+//                 other triangle, t2, when within t1 + 2 EPS (per launch index
+//                 into a scratch array).
+//   k_fast_resolve one ray per lane, all lanes on the same code path:
+//                 * no hit anywhere -> miss (the reference tests a subset);
+//                 * cmp(t2 - t1) > 0 and p1 lies in a KD leaf the reference's
+//                   traversal reaches (replay of its near / far rule down the
+//                   leaf's root path, kd_member) -> (t1, p1) stands;
+//                 * otherwise the lane walks the reference's KD tree for the
+//                   ray (kd_walk: KDtreeAccel::traverse statement for
+//                   statement) and overwrites the result.
+// Triangle tests are Triangle::hit exactly (tri_test: the rcp screen only skips
+// tests whose exact outcome is a reject or a t beyond the window), so t1 is the
+// reference's float.  The membership replay runs in its own launch because at
+// the end of a lane's search it ran with a handful of lanes active (measured:
+// 13 % VALU lane utilisation, most of it there).
+#pragma once
+#include "wr_bvh.h"
+
+namespace wrd {
+
+struct FastScene {
+  const float4* nodes;  // 4 per wrf::BNode
+  const float4* tris;   // 3 per wrf::TriRec
+  const int* prim_leaf_off;
+  const int* prim_leaf;
+  const uint2* path;
+  V3 lo, hi;  // union of the (grown) triangle boxes
+  int depth;  // stack entries (BVH search and KD fallback walk)
+};
+
+struct FastCounters {  // algorithmic work (count_work)
+  uint32_t nodes, tests, replay, fallback;
+  uint32_t kinner, kleaves, krefs;           // KD walks of the fallback rays
+  uint32_t max_nodes, max_tests, long_rays;  // per-ray tail: max visits, rays > 256 nodes
+};
+
+// Per wave: the stack columns, 8 bytes per entry and lane (BVH: link + entry t;
+// KD walk: node + tmin).
+__host__ __device__ constexpr size_t fast_lds_bytes(int depth) { return size_t(depth) * 64 * 8; }
+
+// KDtreeAccel::traverse reaches the leaf whose root path is rec[1..n]: the
+// near / far rule (:331-357) and the `ray.tmax < tmin` stop (:323), evaluated
+// with the reference's floats along that one path.  (tmin, tmax) = root clip.
+// The record is read 8 entries (4 x 16 bytes) per round trip.
+__device__ __forceinline__ bool kd_reaches(const uint2* rec, V3 o, V3 d, V3 inv, float tmin, float tmax, float rtmax,
+                                           uint32_t& steps) {
+  const uint4* R = reinterpret_cast<const uint4*>(rec);
+  int n = 0;
+  for (int base = 0;; base += 8) {
+    uint4 q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) q[u] = R[base / 2 + u];
+    if (base == 0) n = static_cast<int>(q[0].x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = base + j;
+      if (k == 0) continue;
+      if (k > n) return true;
+      const uint2 e = (j & 1) ? make_uint2(q[j / 2].z, q[j / 2].w) : make_uint2(q[j / 2].x, q[j / 2].y);
+      ++steps;
+      const uint32_t axis = e.y & 3u;
+      const bool right = (e.y & 4u) != 0u;
+      const float split = __uint_as_float(e.x);
+      const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+      const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+      const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
+      const float t = (split - oa) * ia;
+      const bool below = (oa < split) | ((oa == split) & (da <= 0));
+      const bool is_near = right != below;  // near = left iff below
+      const bool go_near = (t > tmax) | (t <= 0);
+      const bool go_far = !go_near & (t < tmin);
+      if (go_near) {
+        if (!is_near) return false;
+      } else if (go_far) {
+        if (is_near) return false;
+      } else if (is_near) {
+        tmax = t;
+      } else {
+        tmin = t;  // popped later with tmin = t: the :323 check
+        if (rtmax < tmin) return false;
+      }
+    }
+    if (base + 8 > n) return true;
+  }
+}
+
+// Is the primitive whose KD leaves are prim_leaf[lb, lb + ln) tested by the
+// reference's traversal of this ray?
+__device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F, int lb, int ln, V3 o, V3 d,
+                                          float rtmax, uint32_t& steps) {
+  float tmin, tmax;
+  if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) return false;  // :312-313, :323
+  const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+  for (int k = lb; k < lb + ln; ++k)
+    if (kd_reaches(F.path + F.prim_leaf[k], o, d, inv, tmin, tmax, rtmax, steps)) return true;
+  return false;
+}
+
+// KDtreeAccel::traverse (KDtreeAccel.cpp:309-388) for one ray on one lane:
+// root-box clip, the belowFirst near / far rule, the `ray.tmax < tmin` stop, no
+// early exit, and `cmp(t - best) < 0` over every leaf's references in order.
+// The stack holds (node, tmin) in LDS columns of stride 64; an entry's tmax is
+// the previous entry's tmin (the root tmax for entry 0), the floats the
+// reference's todo[] holds.
+template <bool COUNT>
+__device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtmin, float rtmax, int* stk_node,
+                                        float* stk_tmin, float& t_best, int& best, FastCounters& ctr) {
+  t_best = WR_INF;
+  best = -1;
+  float tmin, tmax;
+  if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) return;  // :312-313, :323
+  const float root_tmax = tmax;
+  const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+  uint32_t node = 0;
+  int sp = 0;
+  for (;;) {
+    const uint4 w = S.nrec[node];  // (self, left child)
+    if ((w.y & 3u) != 3u) {        // inner (:325-358)
+      if (COUNT) ++ctr.kinner;
+      const uint32_t axis = w.y & 3u;
+      const float split = __uint_as_float(w.x);
+      const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+      const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+      const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
+      const float t = (split - oa) * ia;
+      const bool below = (oa < split) | ((oa == split) & (da <= 0));
+      const uint32_t left = node + 1, right = w.y >> 2;
+      const uint32_t nearc = below ? left : right, farc = below ? right : left;
+      if ((t > tmax) | (t <= 0)) {
+        node = nearc;
+      } else if (t < tmin) {
+        node = farc;
+      } else {
+        stk_node[sp * 64] = static_cast<int>(farc);
+        stk_tmin[sp * 64] = t;
+        ++sp;
+        node = nearc;
+        tmax = t;
+      }
+      continue;
+    }
+    // leaf (:359-373): references in order, four records in flight
+    const uint32_t first = w.x, cnt = w.y >> 2;
+    if (COUNT) {
+      ++ctr.kleaves;
+      ctr.krefs += cnt;
+    }
+    for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
+      float4 ra[4], rb[4];
+      float2 rc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t ref = first + min(k0 + u, cnt - 1);
+        ra[u] = S.ref_a[ref];
+        rb[u] = S.ref_b[ref];
+        rc[u] = S.ref_c[ref];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (k0 + u >= cnt) break;
+        float t;
+        if (tri_test(ra[u], rb[u], rc[u].x, o, d, rtmin, rtmax, t_best, t) && cmpf(t - t_best) < 0) {
+          t_best = t;
+          best = __float_as_int(rc[u].y);
+        }
+      }
+    }
+    if (sp == 0) return;  // :375-383
+    --sp;
+    node = static_cast<uint32_t>(stk_node[sp * 64]);
+    tmin = stk_tmin[sp * 64];
+    tmax = sp > 0 ? stk_tmin[(sp - 1) * 64] : root_tmax;
+    if (rtmax < tmin) return;  // :323
+  }
+}
+
+__device__ __forceinline__ float clamp_inv(float x) { return fminf(fmaxf(1.f / x, -1e30f), 1e30f); }
+
+// launch index -> (queue, index in it), as k_trace numbers a launch's rays
+struct QueueIndex {
+  int qend[kMaxQueues];
+  int n;
+  __device__ __forceinline__ explicit QueueIndex(const TraceQueues& Q) {
+    int acc = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxQueues; ++i) {
+      if (i < Q.n && Q.q[i].count) acc += *Q.q[i].count;
+      qend[i] = acc;
+    }
+    n = acc;
+  }
+  __device__ __forceinline__ void locate(int idx, int& q, int& r) const {
+    q = 0;
+    int q0 = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxQueues - 1; ++i)
+      if (idx >= qend[i]) {
+        q = i + 1;
+        q0 = qend[i];
+      }
+    r = idx - q0;
+  }
+};
+template <class Fn>
+__device__ __forceinline__ auto qfield(const TraceQueues& Q, int q, Fn field) {
+  auto v = field(Q.q[0]);
+#pragma unroll
+  for (int i = 1; i < kMaxQueues; ++i)
+    if (q == i) v = field(Q.q[i]);
+  return v;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, int* fetch,
+                                           float* t2buf, uint32_t* lds, FastCounters& ctr) {
+  const int lane = __lane_id();
+  int* stk_link = reinterpret_cast<int*>(lds) + lane;
+  float* stk_t = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
+  const QueueIndex QI(Q);
+  const int n = QI.n;
+  int r = -1, qi = 0, lidx = 0;
+  bool pool = true;
+  int pb = 0, pe = 0;
+  V3 o = v3(0.f, 0.f, 0.f), d = o, binv = o;
+  float rtmin = 0.f, rtmax = WR_INF, t1 = WR_INF, t2 = WR_INF, tcap = 0.f, dlen = 1.f;
+  int p1 = -1, sp = 0;
+  uint32_t rn = 0, rt = 0;  // COUNT: this ray's node visits / tests
+  int cur = 0;  // >= 0 inner node to visit; < 0 leaf link to test; kDone when finished
+  constexpr int kDone = 0x7fffffff;
+  auto reserve = [&](bool want) -> int {
+    const unsigned long long m = __ballot(want);
+    const int need = __popcll(m);
+    const int rank = __popcll(m & ((1ull << lane) - 1ull));
+    int idx = pb + rank;
+    if (need == 0) return idx;
+    if (pe - pb < need) {
+      int got = 0;
+      if (lane == 0) got = atomicAdd(fetch, kRayGrab);
+      got = __builtin_amdgcn_readlane(got, 0);
+      const int rem = pe - pb;
+      if (rank >= rem) idx = got + (rank - rem);
+      pb = got + (need - rem);
+      pe = got + kRayGrab;
+    } else {
+      pb += need;
+    }
+    return idx;
+  };
+  // the search window: hits up to t1 + 2 EPS, and rtmax
+  auto bound = [&]() { return fminf(rtmax, t1 + 2.f * WR_EPS); };
+  auto pop = [&]() {
+    const float thi = bound();
+    const float tc = fminf(thi, tcap);
+    const float gt = (wrf::kRayGrow * (tc * dlen + 1.f)) / dlen;
+    cur = kDone;
+    while (sp > 0) {
+      --sp;
+      if (stk_t[sp * 64] <= thi + gt) {
+        cur = stk_link[sp * 64];
+        break;
+      }
+    }
+  };
+  for (;;) {
+    // ---- refill idle lanes
+    if (pool) {
+      const bool idle = r < 0;
+      if (__ballot(idle)) {
+        const int idx = reserve(idle);
+        const bool take = idle && idx < n;
+        if (take) {
+          lidx = idx;
+          QI.locate(idx, qi, r);
+          const float* o3 = qfield(Q, qi, [](const RayQueue& x) { return x.o3; });
+          const float* d3 = qfield(Q, qi, [](const RayQueue& x) { return x.d3; });
+          const int cap = qfield(Q, qi, [](const RayQueue& x) { return x.cap; });
+          const float* tmn = qfield(Q, qi, [](const RayQueue& x) { return x.tmin; });
+          const float* tmx = qfield(Q, qi, [](const RayQueue& x) { return x.tmax; });
+          o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
+          d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+          rtmin = tmn ? tmn[r] : 0.f;
+          rtmax = tmx ? tmx[r] : WR_INF;
+          binv = v3(clamp_inv(d.x), clamp_inv(d.y), clamp_inv(d.z));
+          dlen = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+          if (!(dlen > 0.f)) dlen = 1.f;
+          t1 = WR_INF;
+          t2 = WR_INF;
+          p1 = -1;
+          sp = 0;
+          cur = 0;
+          rn = rt = 0;
+          // exit of the union box: caps the search margin before the first hit
+          const float ax = (F.lo.x - o.x) * binv.x, bx = (F.hi.x - o.x) * binv.x;
+          const float ay = (F.lo.y - o.y) * binv.y, by = (F.hi.y - o.y) * binv.y;
+          const float az = (F.lo.z - o.z) * binv.z, bz = (F.hi.z - o.z) * binv.z;
+          tcap = fmaxf(0.f, fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)));
+        }
+        if (__ballot(idle && idx >= n)) pool = false;
+      }
+    }
+    const bool act = r >= 0;
+    if (!__ballot(act)) {
+      if (!pool) break;
+      continue;
+    }
+    // ---- inner nodes until this lane has a leaf (or is done)
+    while (__ballot(act && cur >= 0 && cur != kDone)) {
+      if (act && cur >= 0 && cur != kDone) {
+        if (COUNT) {
+          ++ctr.nodes;
+          ++rn;
+        }
+        const float4* np = F.nodes + 4 * static_cast<size_t>(cur);
+        const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+        const int4 lk = *reinterpret_cast<const int4*>(np + 3);
+        const float thi = bound();
+        const float tc = fminf(thi, tcap);
+        const float g = wrf::kRayGrow * (tc * dlen + 1.f);  // spatial margin for this ray
+        const float gt = g / dlen;
+        const float lo_t = rtmin - gt, hi_t = thi + gt;
+        auto slab = [&](float lx, float ly, float lz, float hx, float hy, float hz, float& tn) {
+          const float x0 = (lx - g - o.x) * binv.x, x1 = (hx + g - o.x) * binv.x;
+          const float y0 = (ly - g - o.y) * binv.y, y1 = (hy + g - o.y) * binv.y;
+          const float z0 = (lz - g - o.z) * binv.z, z1 = (hz + g - o.z) * binv.z;
+          tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), lo_t));
+          const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), hi_t));
+          return tn <= tf;
+        };
+        float ta, tb;
+        const bool ha = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, ta);
+        const bool hb = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tb);
+        if (ha && hb) {
+          const bool af = ta <= tb;
+          stk_link[sp * 64] = af ? lk.y : lk.x;
+          stk_t[sp * 64] = af ? tb : ta;
+          ++sp;
+          cur = af ? lk.x : lk.y;
+        } else if (ha) {
+          cur = lk.x;
+        } else if (hb) {
+          cur = lk.y;
+        } else {
+          pop();
+        }
+      }
+    }
+    // ---- leaf: test its triangles (Triangle::hit), keep (t1, p1) and t2
+    if (act && cur < 0) {
+      const int l = ~cur;
+      const int first = l >> 3, cnt = (l & 7) + 1;
+      // all records of the leaf requested before the first test
+      float4 ta[wrf::kMaxLeaf], tb[wrf::kMaxLeaf], tc[wrf::kMaxLeaf];
+#pragma unroll
+      for (int j = 0; j < wrf::kMaxLeaf; ++j) {
+        const float4* tp = F.tris + 3 * static_cast<size_t>(first + min(j, cnt - 1));
+        ta[j] = tp[0];
+        tb[j] = tp[1];
+        tc[j] = tp[2];
+      }
+#pragma unroll
+      for (int j = 0; j < wrf::kMaxLeaf; ++j) {
+        if (j >= cnt) break;
+        if (COUNT) {
+          ++ctr.tests;
+          ++rt;
+        }
+        float t;
+        // screen against t1 + 3 EPS: every hit with t <= t1 + 2 EPS survives
+        if (tri_test(ta[j], tb[j], tc[j].x, o, d, rtmin, rtmax, t1 + 3.f * WR_EPS, t)) {
+          if (t < t1) {
+            t2 = t1;
+            t1 = t;
+            p1 = __float_as_int(tc[j].y);
+          } else if (t < t2) {
+            t2 = t;
+          }
+        }
+      }
+      pop();
+    }
+    // ---- finished rays: the candidate goes to k_fast_resolve
+    if (act && cur == kDone) {
+      if (COUNT) {
+        ctr.max_nodes = max(ctr.max_nodes, rn);
+        ctr.max_tests = max(ctr.max_tests, rt);
+        ctr.long_rays += rn > 256u ? 1u : 0u;
+      }
+      qfield(Q, qi, [](const RayQueue& x) { return x.out_t; })[r] = p1 >= 0 ? t1 : WR_INF;
+      qfield(Q, qi, [](const RayQueue& x) { return x.out_prim; })[r] = p1;
+      t2buf[lidx] = t2;
+      r = -1;
+    }
+  }
+}
+
+// k_fast_resolve: one ray per lane (grid-stride over the launch's indices).
+template <bool COUNT>
+__device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
+                                             const float* t2buf, uint32_t* lds, FastCounters& ctr) {
+  const int lane = __lane_id();
+  int* stk_node = reinterpret_cast<int*>(lds) + lane;
+  float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
+  const QueueIndex QI(Q);
+  for (int idx = blockIdx.x * 64 + lane; idx < QI.n; idx += gridDim.x * 64) {
+    int q, r;
+    QI.locate(idx, q, r);
+    int* outp = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; });
+    const int p1 = outp[r];
+    if (p1 < 0) continue;  // no hit anywhere: a miss for the reference too
+    float* outt = qfield(Q, q, [](const RayQueue& x) { return x.out_t; });
+    const float t1 = outt[r], t2 = t2buf[idx];
+    const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
+    const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
+    const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
+    const float* tmn = qfield(Q, q, [](const RayQueue& x) { return x.tmin; });
+    const float* tmx = qfield(Q, q, [](const RayQueue& x) { return x.tmax; });
+    const V3 o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
+    const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+    const float rtmax = tmx ? tmx[r] : WR_INF;
+    uint32_t steps = 0;
+    const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
+    const bool ok = cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0 && kd_member(S, F, lb, ln, o, d, rtmax, steps);
+    if (COUNT) ctr.replay += steps;
+    if (ok) continue;
+    // near-tie or not reached by the reference's walk: the walk itself decides
+    if (COUNT) ++ctr.fallback;
+    float tb;
+    int pb;
+    kd_walk<COUNT>(S, o, d, tmn ? tmn[r] : 0.f, rtmax, stk_node, stk_tmin, tb, pb, ctr);
+    outt[r] = tb;
+    outp[r] = pb;
+  }
+}
+
+}  // namespace wrd

@@ -29,6 +29,7 @@
 #include "winmad_rt.h"
 #include "wr_scene.h"
 #include "wr_traverse.h"
+#include "wr_fast.h"
 
 using namespace wrd;
 
@@ -93,6 +94,7 @@ struct DevCounters {
   unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
   unsigned long long closest, shadow, inner, leaves, refs, tests;
   unsigned long long vm_queries, vm_found, vm_merged;  // VCM range queries / vertices in radius / merges
+  unsigned long long bvh_nodes, bvh_tests, kd_replay, fallback;  // WR_TRACE_BVH work (count_work)
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -174,6 +176,47 @@ __attribute__((amdgpu_waves_per_eu(DENSE ? 5 : (CUT ? WR_TRACE_CUT_WAVES_PER_EU 
       atomicAdd(&ctr->tests, e);
     }
   }
+}
+
+// Verified-BVH closest hit over the same queues (wr_fast.h): the search, then
+// the one-ray-per-lane resolve (membership replay, KD walk of undecided rays).
+// 4 waves/SIMD like k_trace.
+template <bool COUNT>
+__device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters& fc) {
+  unsigned long long a = wave_sum(fc.nodes), b = wave_sum(fc.tests), c = wave_sum(fc.replay),
+                     e = wave_sum(fc.fallback), ki = wave_sum(fc.kinner), kl = wave_sum(fc.kleaves),
+                     kr = wave_sum(fc.krefs);
+  if (lane_id() == 0) {
+    atomicAdd(&ctr->bvh_nodes, a);
+    atomicAdd(&ctr->bvh_tests, b);
+    atomicAdd(&ctr->kd_replay, c);
+    atomicAdd(&ctr->fallback, e);
+    // the KD walks of undecided rays count as the reference traversal's work
+    atomicAdd(&ctr->inner, ki);
+    atomicAdd(&ctr->leaves, kl);
+    atomicAdd(&ctr->refs, kr);
+    atomicAdd(&ctr->tests, kr);
+  }
+  // diagnostic tail (stamps[5..7], WR_TRACE_LOG): max nodes / tests per ray, rays > 256 nodes
+  atomicMax(&ctr->stamps[5], static_cast<unsigned long long>(fc.max_nodes));
+  atomicMax(&ctr->stamps[6], static_cast<unsigned long long>(fc.max_tests));
+  atomicAdd(&ctr->stamps[7], static_cast<unsigned long long>(fc.long_rays));
+}
+template <bool COUNT>
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32
+k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf) {
+  extern __shared__ uint32_t smem[];
+  FastCounters fc{};
+  trace_fast<COUNT>(S, F, Q, fetch, t2buf, smem, fc);
+  if (COUNT) fast_counts<COUNT>(ctr, fc);
+}
+template <bool COUNT>
+__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
+k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf) {
+  extern __shared__ uint32_t smem[];
+  FastCounters fc{};
+  resolve_fast<COUNT>(S, F, Q, t2buf, smem, fc);
+  if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 
 // C-ABI traversal, before: AoS wr_ray -> SoA queue (occlusion rays re-normalised
@@ -300,6 +343,8 @@ struct Pipe {
   BdptBuf bb[kGroup]{};
   PtBuf pb[kGroup]{};
   VcmBuf vb[kGroup]{};
+  float* t2buf = nullptr;  // WR_TRACE_BVH: per-ray t2 of the BVH search (launch index)
+  size_t t2_cap = 0;
   std::vector<hipEvent_t> events;  // Timer marks (time_kernels)
   std::vector<int> ev_cat;
   size_t ev_used = 0;
@@ -336,6 +381,14 @@ struct wr_context {
   bool api_dense = false;         // test knob WR_TRACE_DENSE=1: API launches in TRACE_DENSE
   bool no_cut = false;            // WR_TRACE_NO_CUT=1: shadow rays run to the end (no occl_cut)
   bool timing = false;
+  // verified-BVH traversal (wr_fast.h): built at wr_create for triangle scenes
+  FastScene fs{};
+  Arena fast_mem;
+  bool fast_ok = false;   // scene supports it
+  bool fast_on = false;   // WR_TRACE_BVH mode selected
+  int fast_blocks = 4096; // resident one-wave workgroups of k_trace_fast
+  float* api_t2 = nullptr;  // t2 scratch of the API path
+  size_t api_t2_cap = 0;
 };
 
 namespace {
@@ -614,13 +667,67 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, int
   return narrow ? k_trace<false, false, true> : k_trace<false, false, false>;
 }
 
-// One persistent traversal launch over qa then qb (max_rays bounds the grid).
-// `fetch` must be zero (the iteration's counter memset, or the caller).
-int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, int* fetch, Timer& tm, bool count,
+// The device counters of one traversal step: the persistent cursor (zero at
+// the step's start: the iteration's counter memset, or the caller), and in
+// WR_TRACE_BVH mode the per-ray t2 scratch of the BVH search (>= the launch's rays).
+struct TraceSlot {
+  int* fetch;
+  float* t2;
+  size_t t2_cap;
+};
+TraceSlot tslot(Pipe& p, int slot) { return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap}; }
+// t2 scratch of a pipeline for launches of up to `rays` rays
+int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
+  if (!c->fast_on || p.t2_cap >= rays) return WR_OK;
+  if (p.t2buf) (void)hipFree(p.t2buf);
+  p.t2buf = nullptr;
+  p.t2_cap = 0;
+  HIPCHK(hipMalloc(&p.t2buf, rays * sizeof(float)));
+  p.t2_cap = rays;
+  return WR_OK;
+}
+
+// One persistent traversal launch over the queues of Q (max_rays bounds the
+// grid).  WR_TRACE_BVH: the verified-BVH search + its resolve launch instead.
+int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const TraceSlot& ts, Timer& tm, bool count,
                  const TraceQueues& Q_, int max_rays, int mode = TRACE_PLAIN) {
+  int* fetch = ts.fetch;
   TraceQueues Q = Q_;
   if (c->no_cut)  // measurement knob: the same launches without the dead-work elision
     for (int i = 0; i < Q.n; ++i) Q.q[i].cut = nullptr;
+  if (c->fast_on && !c->stamps && ts.t2 && static_cast<size_t>(max_rays) <= ts.t2_cap) {
+    const int blocks = (max_rays + kTraceBlock - 1) / kTraceBlock;
+    const int fgrid = std::max(1, std::min(c->fast_blocks, blocks));
+    const size_t lds = fast_lds_bytes(c->fs.depth);
+    hipEvent_t f0 = nullptr, f1 = nullptr;
+    if (c->trace_log) {
+      (void)hipEventCreate(&f0);
+      (void)hipEventCreate(&f1);
+      (void)hipEventRecord(f0, stream);
+    }
+    hipLaunchKernelGGL(count ? k_trace_fast<true> : k_trace_fast<false>, dim3(fgrid), dim3(kTraceBlock), lds, stream,
+                       c->ds, c->fs, Q, ctr, fetch, ts.t2);
+    hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
+                       dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), lds, stream, c->ds,
+                       c->fs, Q, ctr, ts.t2);
+    tm.mark(WR_K_TRACE);
+    if (c->trace_log) {
+      (void)hipEventRecord(f1, stream);
+      (void)hipEventSynchronize(f1);
+      int tot = 0;
+      for (int i = 0; i < Q.n; ++i) {
+        int k = 0;
+        if (Q.q[i].count) (void)hipMemcpy(&k, Q.q[i].count, sizeof(int), hipMemcpyDeviceToHost);
+        tot += k;
+      }
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, f0, f1);
+      std::fprintf(stderr, "[wr bvh] %d rays  %.1f us  grid %d\n", tot, ms * 1e3f, fgrid);
+      (void)hipEventDestroy(f0);
+      (void)hipEventDestroy(f1);
+    }
+    return WR_OK;
+  }
   const bool dense = mode == TRACE_DENSE && !c->stamps;
   const size_t lds = trace_lds_bytes(c->ds.max_stack, c->narrow, dense);
   const int grid =
@@ -703,6 +810,10 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
     sum.vm_queries += h.vm_queries;
     sum.vm_found += h.vm_found;
     sum.vm_merged += h.vm_merged;
+    sum.bvh_nodes += h.bvh_nodes;
+    sum.bvh_tests += h.bvh_tests;
+    sum.kd_replay += h.kd_replay;
+    sum.fallback += h.fallback;
     for (int k = 0; k < 8; ++k) sum.stamps[k] += h.stamps[k];
   }
   st->closest_rays += static_cast<int64_t>(sum.closest);
@@ -714,6 +825,22 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
   st->vm_queries += static_cast<int64_t>(sum.vm_queries);
   st->vm_found += static_cast<int64_t>(sum.vm_found);
   st->vm_merged += static_cast<int64_t>(sum.vm_merged);
+  st->bvh_nodes += static_cast<int64_t>(sum.bvh_nodes);
+  st->bvh_tests += static_cast<int64_t>(sum.bvh_tests);
+  st->kd_replay_steps += static_cast<int64_t>(sum.kd_replay);
+  st->fallback_rays += static_cast<int64_t>(sum.fallback);
+  if (c->trace_log && c->fast_on) {
+    unsigned long long mx[3] = {0, 0, 0};
+    for (int i = 0; i < n; ++i) {
+      DevCounters h;
+      HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
+      mx[0] = std::max(mx[0], h.stamps[5]);
+      mx[1] = std::max(mx[1], h.stamps[6]);
+      mx[2] += h.stamps[7];
+    }
+    std::fprintf(stderr, "[wr bvh tail] max nodes/ray %llu, max tests/ray %llu, rays > 256 nodes %llu\n", mx[0], mx[1],
+                 mx[2]);
+  }
   if (c->stamps) {
     static const char* names[6] = {"refill", "walk", "leaf-setup", "pair-tests", "decision", "write"};
     double tot = 0;
@@ -1078,7 +1205,74 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     c->trace_blocks = c->cus * resident(TRACE_PLAIN);
     c->trace_blocks_dense = c->cus * resident(TRACE_DENSE);
   }
+  // ---- verified-BVH traversal data (wr_bvh.h): BVH nodes, triangle records
+  // in leaf order, and the KD root paths of every primitive's leaves
+  {
+    wrf::FastHost fh;
+    wrf::build_fast(s, fh);
+    if (fh.ok) {
+      const size_t fbn = fh.nodes.size(), ftr = fh.tris.size(), fpo = fh.prim_leaf_off.size(),
+                   fpl = std::max<size_t>(1, fh.prim_leaf.size()), fpa = fh.path.size() / 2;
+      const size_t fbytes = measure([&](Arena& a) {
+        a.take<wrf::BNode>(fbn); a.take<wrf::TriRec>(ftr); a.take<int>(fpo); a.take<int>(fpl); a.take<uint2>(fpa);
+      });
+      if (int rc = c->fast_mem.reserve(fbytes)) {
+        wr_destroy(c);
+        return rc;
+      }
+      Arena& F = c->fast_mem;
+      auto* dno = F.take<wrf::BNode>(fbn);
+      auto* dtr = F.take<wrf::TriRec>(ftr);
+      int* dpo = F.take<int>(fpo);
+      int* dpl = F.take<int>(fpl);
+      uint2* dpa = F.take<uint2>(fpa);
+      hipError_t fe = hipSuccess;
+      for (hipError_t x : {hipMemcpy(dno, fh.nodes.data(), fbn * sizeof(wrf::BNode), hipMemcpyHostToDevice),
+                           hipMemcpy(dtr, fh.tris.data(), ftr * sizeof(wrf::TriRec), hipMemcpyHostToDevice),
+                           hipMemcpy(dpo, fh.prim_leaf_off.data(), fpo * sizeof(int), hipMemcpyHostToDevice),
+                           hipMemcpy(dpl, fh.prim_leaf.data(), fh.prim_leaf.size() * sizeof(int), hipMemcpyHostToDevice),
+                           hipMemcpy(dpa, fh.path.data(), fpa * sizeof(uint2), hipMemcpyHostToDevice)})
+        if (x != hipSuccess) fe = x;
+      if (fe != hipSuccess) {
+        wr_destroy(c);
+        return fail(WR_E_HIP, std::string("BVH upload: ") + hipGetErrorString(fe));
+      }
+      FastScene& fs = c->fs;
+      fs.nodes = reinterpret_cast<const float4*>(dno);
+      fs.tris = reinterpret_cast<const float4*>(dtr);
+      fs.prim_leaf_off = dpo;
+      fs.prim_leaf = dpl;
+      fs.path = dpa;
+      float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int k = 0; k < 3; ++k) {
+        lo[k] = std::min(fh.nodes[0].b[k], fh.nodes[0].b[6 + k]);
+        hi[k] = std::max(fh.nodes[0].b[3 + k], fh.nodes[0].b[9 + k]);
+      }
+      fs.lo = v3(lo[0], lo[1], lo[2]);
+      fs.hi = v3(hi[0], hi[1], hi[2]);
+      // one stack serves the BVH search and the lane's KD fallback walk
+      fs.depth = std::max(fh.depth + 1, d.max_stack + 1);
+      c->fast_ok = true;
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_fast<false>, kTraceBlock,
+                                                       fast_lds_bytes(fs.depth)) != hipSuccess ||
+          per_cu <= 0)
+        per_cu = 8;
+      c->fast_blocks = c->cus * per_cu;
+      if (const char* e = std::getenv("WR_TRACE_BVH")) c->fast_on = std::atoi(e) != 0;
+      if (c->trace_log)
+        std::fprintf(stderr, "[wr bvh] nodes %zu tris %zu depth %d lds %zu B/wave, %d waves/CU -> grid %d; kd grid %d\n",
+                     fbn, ftr, fs.depth, fast_lds_bytes(fs.depth), per_cu, c->fast_blocks, c->trace_blocks);
+    }
+  }
   *out = c;
+  return WR_OK;
+}
+
+int wr_set_trace_mode(wr_context* c, int mode) {
+  if (!c || (mode != WR_TRACE_REFERENCE && mode != WR_TRACE_BVH)) return fail(WR_E_ARG, "bad trace mode");
+  if (mode == WR_TRACE_BVH && !c->fast_ok) return fail(WR_E_SCENE, "the BVH mode covers triangle scenes only");
+  c->fast_on = mode == WR_TRACE_BVH;
   return WR_OK;
 }
 
@@ -1105,6 +1299,10 @@ void wr_destroy(wr_context* c) {
   if (c->t_null) (void)hipEventDestroy(c->t_null);
   if (c->film_tmp) (void)hipFree(c->film_tmp);
   if (c->api_tmp) (void)hipFree(c->api_tmp);
+  if (c->api_t2) (void)hipFree(c->api_t2);
+  for (Pipe& p : c->pipes)
+    if (p.t2buf) (void)hipFree(p.t2buf);
+  c->fast_mem.release();
   c->scene_mem.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1155,10 +1353,18 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   hipLaunchKernelGGL(k_api_prep, dim3(g), dim3(256), 0, c->stream, dr, n, occ ? 1 : 0, o3, d3, tmn, tmx, dtg, dcut);
   c->timing = false;
   Timer tm(c, nullptr);
-  HIPCHK(hipMemsetAsync(&c->ctr->fetch, 0, sizeof(int), c->stream));
+  HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(DevCounters), c->stream));
+  if (c->fast_on && c->api_t2_cap < nb) {
+    if (c->api_t2) (void)hipFree(c->api_t2);
+    c->api_t2 = nullptr;
+    c->api_t2_cap = 0;
+    HIPCHK(hipMalloc(&c->api_t2, nb * sizeof(float)));
+    c->api_t2_cap = nb;
+  }
   QueueList ql;
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
-  trace_launch(c, c->stream, c->ctr, &c->ctr->fetch, tm, false, ql.Q, ql.max_rays,
+  const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap};
+  trace_launch(c, c->stream, c->ctr, ts, tm, false, ql.Q, ql.max_rays,
                c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN));
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
@@ -1220,6 +1426,12 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
   const int fit = pipelines_that_fit(c, 1, P, kGroup, c->npipes);
   if (fit < 1) return WR_E_HIP;  // message set by the allocation
   const int np = std::max(1, std::min(fit, ngroups));
+  {  // WR_TRACE_BVH t2 scratch: a launch takes <= kGroup x (shadow / aux + extension) queues
+    const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
+    const size_t per = kGroup * (std::max(cap_sq, size_t(P)) + size_t(P));
+    for (int i = 0; i < np; ++i)
+      if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
+  }
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
@@ -1269,7 +1481,7 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
     for (int b = 0; b < maxlen - 1; ++b) {
       QueueList ql;
       for (int m = 0; m < gn; ++m) ql.add(ext(m, b), P);
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
+      trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
       hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
       tm.mark(WR_K_SHADE);
     }
@@ -1285,7 +1497,7 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
       for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), sq_max);
       if (more)
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
+      trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
       // resolve this step's shadow / aux rays and shade its vertices in one launch
       const int nres = shade_grid(c, sq_max);
       hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot, nres,
@@ -1315,6 +1527,12 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
   const int fit = pipelines_that_fit(c, 3, P, kGroup, c->npipes);
   if (fit < 1) return WR_E_HIP;  // message set by the allocation
   const int np = std::max(1, std::min(fit, ngroups));
+  {  // WR_TRACE_BVH t2 scratch: a launch takes <= kGroup x (shadow / aux + extension) queues
+    const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
+    const size_t per = kGroup * (std::max(cap_sq, size_t(P)) + size_t(P));
+    for (int i = 0; i < np; ++i)
+      if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
+  }
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
@@ -1390,7 +1608,7 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
     for (int b = 0; b < maxlen - 1; ++b) {
       QueueList ql;
       for (int m = 0; m < gn; ++m) ql.add(ext(m, b), P);
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays);
+      trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays);
       hipLaunchKernelGGL(k_vcm_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
       tm.mark(WR_K_SHADE);
     }
@@ -1415,7 +1633,7 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
       for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), sq_max);
       if (more)
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[slot], tm, count, ql.Q, ql.max_rays, WR_VCM_TRACE_MODE);
+      trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_VCM_TRACE_MODE);
       const int nres = shade_grid(c, sq_max);
       // + the merge queries of the previous step (none before the first)
       const int nsh = more ? g : 0, nmg = b > 0 ? g : 0;
@@ -1440,6 +1658,7 @@ int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max
   const double t0 = host_now();
   const int P = static_cast<int>(n64);
   if (pipelines_that_fit(c, 2, P, 1, 1) < 1) return WR_E_HIP;
+  if (int rc = ensure_t2(c, c->pipes[0], 2 * size_t(P))) return rc;
   Pipe& pp = c->pipes[0];  // the context stream
   const size_t nf = size_t(P) * 3;
   std::memset(rgb, 0, nf * sizeof(float));
@@ -1476,7 +1695,7 @@ int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max
     QueueList ql;
     ql.add(rq(Q.o, Q.d, P, &pp.sc[0].sq[b], Q.t, Q.prim, nullptr, nullptr, Q.cut), P);
     if (more) ql.add(rq(T.q_o[b & 1], T.q_d[b & 1], P, &pp.sc[0].ext[b], T.q_t[b & 1], T.q_prim[b & 1]), P);
-    trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, false, ql.Q, ql.max_rays, TRACE_DENSE);
+    trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, false, ql.Q, ql.max_rays, TRACE_DENSE);
     const int nres = shade_grid(c, P);
     hipLaunchKernelGGL(k_pt_step, dim3(nres + (more ? g : 0), 1), dim3(kShadeBlock), 0, sm, GA, b, nres,
                        more ? 1 : 0);
@@ -1510,6 +1729,12 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
   const int fit = pipelines_that_fit(c, 2, P, kGroup, c->npipes);
   if (fit < 1) return WR_E_HIP;  // message set by the allocation
   const int np = std::max(1, std::min(fit, ngroups));
+  {  // WR_TRACE_BVH t2 scratch: a launch takes <= kGroup x (shadow / aux + extension) queues
+    const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
+    const size_t per = kGroup * (std::max(cap_sq, size_t(P)) + size_t(P));
+    for (int i = 0; i < np; ++i)
+      if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
+  }
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
@@ -1559,7 +1784,7 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
           const PtBuf& T = pp.pb[m];
           ql.add(rq(T.q_o[q], T.q_d[q], P, &pp.sc[m].ext[b], T.q_t[q], T.q_prim[q]), P);
         }
-      trace_launch(c, sm, pp.ctr, &pp.sc[0].fetch[b], tm, count, ql.Q, ql.max_rays, TRACE_DENSE);
+      trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays, TRACE_DENSE);
       // resolve this step's shadow rays and shade its vertices in one launch
       const int nres = shade_grid(c, P);
       hipLaunchKernelGGL(k_pt_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, b, nres,

@@ -15,10 +15,11 @@ LIB_PATH = os.environ.get("WR_LIB") or os.path.join(PKG_DIR, "libwinmad_rt.so")
 
 WR_OK, WR_E_ARG, WR_E_IO, WR_E_HIP, WR_E_SCENE, WR_E_NODEVICE = 0, -1, -2, -3, -4, -5
 K_TRACE, K_SHADE, K_RESOLVE, K_GEN, K_OTHER = 0, 1, 2, 3, 4
+TRACE_REFERENCE, TRACE_BVH = 0, 1
 
 # every entry point declared in include/winmad_rt.h
 EXPORTS = ["wr_scene_load", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free", "wr_device_count",
-           "wr_create", "wr_destroy", "wr_set_pipelines", "wr_trace_closest", "wr_occluded", "wr_render_bdpt", "wr_render_path",
+           "wr_create", "wr_destroy", "wr_set_pipelines", "wr_set_trace_mode", "wr_trace_closest", "wr_occluded", "wr_render_bdpt", "wr_render_path",
            "wr_render_vcm", "wr_path_radiance",
            "wr_film_write_ppm", "wr_film_write_image", "wr_last_error", "wr_api_version"]
 
@@ -65,7 +66,8 @@ class WrStats(C.Structure):
                 ("leaf_visits", C.c_int64), ("prim_refs", C.c_int64), ("seconds", C.c_double),
                 ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8), ("trace_wall_ms", C.c_double),
                 ("vm_queries", C.c_int64), ("vm_found", C.c_int64), ("vm_merged", C.c_int64),
-                ("prim_tests", C.c_int64)]
+                ("prim_tests", C.c_int64), ("bvh_nodes", C.c_int64), ("bvh_tests", C.c_int64),
+                ("kd_replay_steps", C.c_int64), ("fallback_rays", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
@@ -115,6 +117,7 @@ def lib():
         L.wr_destroy.argtypes = [P]
         L.wr_destroy.restype = None
         L.wr_set_pipelines.argtypes = [P, I]
+        L.wr_set_trace_mode.argtypes = [P, I]
         L.wr_trace_closest.argtypes = [P, C.POINTER(WrRay), I64, C.POINTER(WrHit)]
         L.wr_occluded.argtypes = [P, C.POINTER(WrRay), C.POINTER(C.c_float), I64, C.POINTER(C.c_uint8)]
         L.wr_render_bdpt.argtypes = [P, C.POINTER(WrBdptParams), P, I, C.POINTER(WrStats)]
@@ -210,6 +213,11 @@ class Context:
     def set_pipelines(self, n):
         """Concurrent render pipelines (streams) for render_bdpt / render_path."""
         check(lib().wr_set_pipelines(self.h, n))
+
+    def set_trace_mode(self, mode):
+        """TRACE_REFERENCE (the reference's KD walk) or TRACE_BVH (verified BVH
+        search + KD fallback, same answers): include/winmad_rt.h."""
+        check(lib().wr_set_trace_mode(self.h, mode))
 
     def close(self):
         if getattr(self, "h", None):
