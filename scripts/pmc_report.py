@@ -15,7 +15,7 @@ for f in sorted(glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv
         k = row["Kernel_Name"]
         if want and want not in k:
             continue
-        key = k.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:48]
+        key = k.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:48]
         tot[key][row["Counter_Name"]] += float(row["Counter_Value"])
 for k, c in tot.items():
     print(k)

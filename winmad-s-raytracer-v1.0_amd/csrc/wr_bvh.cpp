@@ -186,9 +186,10 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
     int node;
     int depth;            // entries on the path to this node
     uint32_t e0, e1;      // the entry that led here (valid if depth > 0)
+    float lo[3], hi[3];   // the node's cell: the root box cut by the splits above
   };
   std::vector<Item> st;
-  st.push_back({0, 0, 0u, 0u});
+  st.push_back({0, 0, 0u, 0u, {s.root_l.x, s.root_l.y, s.root_l.z}, {s.root_r.x, s.root_r.y, s.root_r.z}});
   while (!st.empty()) {
     const Item it = st.back();
     st.pop_back();
@@ -201,8 +202,16 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
     if (k.axis >= 0) {
       uint32_t bits;
       std::memcpy(&bits, &k.split, 4);
-      st.push_back({k.right, it.depth + 1, bits, static_cast<uint32_t>(k.axis) | 4u});
-      st.push_back({it.node + 1, it.depth + 1, bits, static_cast<uint32_t>(k.axis)});
+      Item r = {k.right, it.depth + 1, bits, static_cast<uint32_t>(k.axis) | 4u, {}, {}};
+      Item l = {it.node + 1, it.depth + 1, bits, static_cast<uint32_t>(k.axis), {}, {}};
+      for (int a = 0; a < 3; ++a) {
+        l.lo[a] = r.lo[a] = it.lo[a];
+        l.hi[a] = r.hi[a] = it.hi[a];
+      }
+      l.hi[k.axis] = std::min(l.hi[k.axis], k.split);
+      r.lo[k.axis] = std::max(r.lo[k.axis], k.split);
+      st.push_back(r);
+      st.push_back(l);
     } else {
       // records start on 16-byte boundaries (even entries): read as uint4
       if ((out.path.size() / 2) & 1) {
@@ -212,6 +221,16 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
       const int32_t off = static_cast<int32_t>(out.path.size() / 2);
       out.path.push_back(static_cast<uint32_t>(it.depth));
       out.path.push_back(0u);
+      for (int a = 0; a < 3; ++a) {  // the leaf's cell (orders the replays)
+        uint32_t b;
+        std::memcpy(&b, &it.lo[a], 4);
+        out.path.push_back(b);
+      }
+      for (int a = 0; a < 3; ++a) {
+        uint32_t b;
+        std::memcpy(&b, &it.hi[a], 4);
+        out.path.push_back(b);
+      }
       out.path.insert(out.path.end(), cur.begin(), cur.end());
       for (int i = 0; i < k.count; ++i) {
         const int p = s.refs[static_cast<size_t>(k.first + i)];

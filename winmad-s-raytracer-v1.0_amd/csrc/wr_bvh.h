@@ -55,8 +55,9 @@ struct TriRec {
 static_assert(sizeof(TriRec) == 48, "BVH triangle record is 48 bytes");
 
 // KD membership data.  Leaf path record at path[off] (off even: 16-byte
-// aligned): (n, 0) then n entries (split bits, axis | went_right << 2) from the
-// root down; 8 zero entries pad the array's end.  prim_leaf[
+// aligned): header (n, 0), (cell lo.x, lo.y), (lo.z, hi.x), (hi.y, hi.z) -- the
+// leaf's cell, which orders the replays -- then n entries (split bits,
+// axis | went_right << 2) from the root down; 8 zero entries pad the array's end.  prim_leaf[
 // prim_leaf_off[p] .. prim_leaf_off[p+1]) = path offsets of the KD leaves that
 // hold primitive p.
 constexpr int kMaxLeaf = 4;      // triangles per BVH leaf

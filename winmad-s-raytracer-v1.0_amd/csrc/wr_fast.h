@@ -34,12 +34,14 @@ struct FastScene {
   const uint2* path;
   V3 lo, hi;  // union of the (grown) triangle boxes
   int depth;  // stack entries (BVH search and KD fallback walk)
+  int diag;   // WR_BVH_DIAG (measurement only): 1 = skip the KD walks (wrong answers)
 };
 
 struct FastCounters {  // algorithmic work (count_work)
   uint32_t nodes, tests, replay, fallback;
   uint32_t kinner, kleaves, krefs;           // KD walks of the fallback rays
   uint32_t max_nodes, max_tests, long_rays;  // per-ray tail: max visits, rays > 256 nodes
+  uint32_t fb_tie;                            // fallbacks for a near-tie (the rest: not reached)
 };
 
 // Per wave: the stack columns, 8 bytes per entry and lane (BVH: link + entry t;
@@ -52,17 +54,15 @@ __host__ __device__ constexpr size_t fast_lds_bytes(int depth) { return size_t(d
 // The record is read 8 entries (4 x 16 bytes) per round trip.
 __device__ __forceinline__ bool kd_reaches(const uint2* rec, V3 o, V3 d, V3 inv, float tmin, float tmax, float rtmax,
                                            uint32_t& steps) {
-  const uint4* R = reinterpret_cast<const uint4*>(rec);
-  int n = 0;
+  const int n = static_cast<int>(rec[0].x);
+  const uint4* R = reinterpret_cast<const uint4*>(rec + 4);  // after the header
   for (int base = 0;; base += 8) {
     uint4 q[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) q[u] = R[base / 2 + u];
-    if (base == 0) n = static_cast<int>(q[0].x);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = base + j;
-      if (k == 0) continue;
+      const int k = base + j + 1;
       if (k > n) return true;
       const uint2 e = (j & 1) ? make_uint2(q[j / 2].z, q[j / 2].w) : make_uint2(q[j / 2].x, q[j / 2].y);
       ++steps;
@@ -88,19 +88,30 @@ __device__ __forceinline__ bool kd_reaches(const uint2* rec, V3 o, V3 d, V3 inv,
         if (rtmax < tmin) return false;
       }
     }
-    if (base + 8 > n) return true;
+    if (base + 8 >= n) return true;
   }
 }
 
 // Is the primitive whose KD leaves are prim_leaf[lb, lb + ln) tested by the
 // reference's traversal of this ray?
 __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F, int lb, int ln, V3 o, V3 d,
-                                          float rtmax, uint32_t& steps) {
+                                          float rtmax, float t_hit, uint32_t& steps) {
   float tmin, tmax;
   if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) return false;  // :312-313, :323
   const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-  for (int k = lb; k < lb + ln; ++k)
-    if (kd_reaches(F.path + F.prim_leaf[k], o, d, inv, tmin, tmax, rtmax, steps)) return true;
+  // the leaves whose cell holds the hit point first (usually the one reached),
+  // then the others
+  const V3 p = o + d * t_hit;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int k = lb; k < lb + ln; ++k) {
+      const uint2* rec = F.path + F.prim_leaf[k];
+      const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
+      const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
+      const bool in = p.x >= __uint_as_float(h0.z) && p.y >= __uint_as_float(h0.w) && p.z >= __uint_as_float(h1.x) &&
+                      p.x <= __uint_as_float(h1.y) && p.y <= __uint_as_float(h1.z) && p.z <= __uint_as_float(h1.w);
+      if (in == (pass == 0) && kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps)) return true;
+    }
+  }
   return false;
 }
 
@@ -427,11 +438,16 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
     const float rtmax = tmx ? tmx[r] : WR_INF;
     uint32_t steps = 0;
     const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
-    const bool ok = cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0 && kd_member(S, F, lb, ln, o, d, rtmax, steps);
+    const bool tie = !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0);
+    const bool ok = !tie && kd_member(S, F, lb, ln, o, d, rtmax, t1, steps);
     if (COUNT) ctr.replay += steps;
     if (ok) continue;
     // near-tie or not reached by the reference's walk: the walk itself decides
-    if (COUNT) ++ctr.fallback;
+    if (COUNT) {
+      ++ctr.fallback;
+      ctr.fb_tie += tie ? 1u : 0u;
+    }
+    if (F.diag & 1) continue;
     float tb;
     int pb;
     kd_walk<COUNT>(S, o, d, tmn ? tmn[r] : 0.f, rtmax, stk_node, stk_tmin, tb, pb, ctr);

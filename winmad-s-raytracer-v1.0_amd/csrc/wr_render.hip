@@ -201,6 +201,7 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
   atomicMax(&ctr->stamps[5], static_cast<unsigned long long>(fc.max_nodes));
   atomicMax(&ctr->stamps[6], static_cast<unsigned long long>(fc.max_tests));
   atomicAdd(&ctr->stamps[7], static_cast<unsigned long long>(fc.long_rays));
+  atomicAdd(&ctr->stamps[4], static_cast<unsigned long long>(fc.fb_tie));
 }
 template <bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32
@@ -838,8 +839,14 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
       mx[1] = std::max(mx[1], h.stamps[6]);
       mx[2] += h.stamps[7];
     }
-    std::fprintf(stderr, "[wr bvh tail] max nodes/ray %llu, max tests/ray %llu, rays > 256 nodes %llu\n", mx[0], mx[1],
-                 mx[2]);
+    unsigned long long ties = 0;
+    for (int i = 0; i < n; ++i) {
+      DevCounters h;
+      HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
+      ties += h.stamps[4];
+    }
+    std::fprintf(stderr, "[wr bvh tail] max nodes/ray %llu, max tests/ray %llu, rays > 256 nodes %llu, tie fallbacks %llu\n",
+                 mx[0], mx[1], mx[2], ties);
   }
   if (c->stamps) {
     static const char* names[6] = {"refill", "walk", "leaf-setup", "pair-tests", "decision", "write"};
@@ -1260,6 +1267,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
         per_cu = 8;
       c->fast_blocks = c->cus * per_cu;
       if (const char* e = std::getenv("WR_TRACE_BVH")) c->fast_on = std::atoi(e) != 0;
+      if (const char* e = std::getenv("WR_BVH_DIAG")) fs.diag = std::atoi(e);
       if (c->trace_log)
         std::fprintf(stderr, "[wr bvh] nodes %zu tris %zu depth %d lds %zu B/wave, %d waves/CU -> grid %d; kd grid %d\n",
                      fbn, ftr, fs.depth, fast_lds_bytes(fs.depth), per_cu, c->fast_blocks, c->trace_blocks);
