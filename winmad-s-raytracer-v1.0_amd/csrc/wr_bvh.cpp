@@ -180,7 +180,7 @@ struct Builder {
 
 void kd_paths(const wr::Scene& s, FastHost& out) {
   const size_t np = s.prims.size();
-  std::vector<std::vector<int32_t>> per(np);
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> per(np);  // (path offset, position in the leaf)
   std::vector<uint32_t> cur;  // entries of the current path
   struct Item {
     int node;
@@ -234,15 +234,20 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
       out.path.insert(out.path.end(), cur.begin(), cur.end());
       for (int i = 0; i < k.count; ++i) {
         const int p = s.refs[static_cast<size_t>(k.first + i)];
-        if (per[static_cast<size_t>(p)].empty() || per[static_cast<size_t>(p)].back() != off)
-          per[static_cast<size_t>(p)].push_back(off);
+        if (per[static_cast<size_t>(p)].empty() || per[static_cast<size_t>(p)].back().first != off)
+          per[static_cast<size_t>(p)].emplace_back(off, i);
       }
     }
   }
   out.prim_leaf_off.assign(np + 1, 0);
   for (size_t p = 0; p < np; ++p) out.prim_leaf_off[p + 1] = out.prim_leaf_off[p] + static_cast<int32_t>(per[p].size());
   out.prim_leaf.reserve(static_cast<size_t>(out.prim_leaf_off[np]));
-  for (size_t p = 0; p < np; ++p) out.prim_leaf.insert(out.prim_leaf.end(), per[p].begin(), per[p].end());
+  out.prim_leaf_pos.reserve(static_cast<size_t>(out.prim_leaf_off[np]));
+  for (size_t p = 0; p < np; ++p)
+    for (const auto& e : per[p]) {
+      out.prim_leaf.push_back(e.first);
+      out.prim_leaf_pos.push_back(e.second);
+    }
   // the replay reads 8 entries at a time: pad past the last record
   out.path.resize(out.path.size() + 2 * 8, 0u);
 }
@@ -269,7 +274,8 @@ void build_fast(const wr::Scene& s, FastHost& out) {
     const float v[3][3] = {{p.p0.x, p.p0.y, p.p0.z}, {p.p1.x, p.p1.y, p.p1.z}, {p.p2.x, p.p2.y, p.p2.z}};
     Box b;
     for (auto& q : v) b.grow(q);
-    // the EPS-fattened triangle of Triangle::hit, with a tenfold margin
+    // the EPS-fattened triangle of Triangle::hit (hits lie within EPS x (|e1| + |e2|)
+    // of it), twice over; the float error of the solve is the per-ray margin's
     auto len = [](const float* a, const float* c) {
       const double x = a[0] - c[0], y = a[1] - c[1], z = a[2] - c[2];
       return std::sqrt(x * x + y * y + z * z);

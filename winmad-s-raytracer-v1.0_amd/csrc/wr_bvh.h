@@ -57,13 +57,23 @@ static_assert(sizeof(TriRec) == 48, "BVH triangle record is 48 bytes");
 // KD membership data.  Leaf path record at path[off] (off even: 16-byte
 // aligned): header (n, 0), (cell lo.x, lo.y), (lo.z, hi.x), (hi.y, hi.z) -- the
 // leaf's cell, which orders the replays -- then n entries (split bits,
-// axis | went_right << 2) from the root down; 8 zero entries pad the array's end.  prim_leaf[
-// prim_leaf_off[p] .. prim_leaf_off[p+1]) = path offsets of the KD leaves that
-// hold primitive p.
-constexpr int kMaxLeaf = 4;      // triangles per BVH leaf
-constexpr int kMaxBvhDepth = 62;  // deeper builds disable the fast path
-constexpr float kBoxGrow = 0.01f;  // x (|p0 - p1| + |p0 - p2|): 10x the EPS fattening
-constexpr float kRayGrow = 1e-4f;  // x (ray length to the search bound + 1), per ray
+// axis | went_right << 2) from the root down; 8 zero entries pad the array's end.
+// prim_leaf[prim_leaf_off[p] .. prim_leaf_off[p+1]) = path offsets of the KD
+// leaves that hold primitive p, prim_leaf_pos = its index in each leaf's list.
+#ifndef WR_BVH_LEAF
+#define WR_BVH_LEAF 4
+#endif
+#ifndef WR_BVH_BOX_GROW
+#define WR_BVH_BOX_GROW 0.002f
+#endif
+#ifndef WR_BVH_RAY_GROW
+#define WR_BVH_RAY_GROW 1e-4f
+#endif
+constexpr int kMaxLeaf = WR_BVH_LEAF;  // triangles per BVH leaf (<= 8)
+constexpr int kMaxBvhDepth = 62;       // deeper builds disable the fast path
+constexpr float kBoxGrow = WR_BVH_BOX_GROW;  // x (|p0 - p1| + |p0 - p2|): 2x the EPS fattening (0.01: C2 -6 %)
+constexpr float kRayGrow = WR_BVH_RAY_GROW;  // x (ray length to the search bound + 1), per ray
+static_assert(kMaxLeaf >= 1 && kMaxLeaf <= 8, "leaf links hold count - 1 in 3 bits");
 
 }  // namespace wrf
 
@@ -77,7 +87,7 @@ namespace wrf {
 struct FastHost {
   std::vector<BNode> nodes;
   std::vector<TriRec> tris;
-  std::vector<int32_t> prim_leaf_off, prim_leaf;
+  std::vector<int32_t> prim_leaf_off, prim_leaf, prim_leaf_pos;
   std::vector<uint32_t> path;  // pairs
   int depth = 0;               // deepest node chain (stack bound)
   int leaves = 0;

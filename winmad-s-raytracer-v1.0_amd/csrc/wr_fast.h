@@ -8,12 +8,21 @@
 //                 written as the ray's result -- and the smallest hit of any
 //                 other triangle, t2, when within t1 + 2 EPS (per launch index
 //                 into a scratch array).
-//   k_fast_resolve one ray per lane, all lanes on the same code path:
+//   k_fast_resolve one ray per lane, all lanes on the same code path
+//                 (the rare cases below the first are listed and finished by a
+//                 third launch, k_fast_hard):
 //                 * no hit anywhere -> miss (the reference tests a subset);
 //                 * cmp(t2 - t1) > 0 and p1 lies in a KD leaf the reference's
 //                   traversal reaches (replay of its near / far rule down the
 //                   leaf's root path, kd_member) -> (t1, p1) stands;
-//                 * otherwise the lane walks the reference's KD tree for the
+//                 * a near-tie (another hit within EPS of t1): every hit up to
+//                   t1 + 3 EPS is collected by a second BVH search
+//                   (bvh_collect), and the reference's first-found-wins rule is
+//                   run over those it reaches, in the order it reaches them
+//                   (resolve_tie);
+//                 * otherwise (t1's triangle not reached, more near hits than
+//                   the list holds, or hits in the band where unseen hits could
+//                   interfere) the lane walks the reference's KD tree for the
 //                   ray (kd_walk: KDtreeAccel::traverse statement for
 //                   statement) and overwrites the result.
 // Triangle tests are Triangle::hit exactly (tri_test: the rcp screen only skips
@@ -31,17 +40,18 @@ struct FastScene {
   const float4* tris;   // 3 per wrf::TriRec
   const int* prim_leaf_off;
   const int* prim_leaf;
+  const int* prim_leaf_pos;
   const uint2* path;
   V3 lo, hi;  // union of the (grown) triangle boxes
   int depth;  // stack entries (BVH search and KD fallback walk)
-  int diag;   // WR_BVH_DIAG (measurement only): 1 = skip the KD walks (wrong answers)
+  int diag;   // WR_BVH_DIAG: 1 = skip the KD walks (wrong answers, measurement only); 2 = KD walk for every tie
 };
 
 struct FastCounters {  // algorithmic work (count_work)
   uint32_t nodes, tests, replay, fallback;
   uint32_t kinner, kleaves, krefs;           // KD walks of the fallback rays
   uint32_t max_nodes, max_tests, long_rays;  // per-ray tail: max visits, rays > 256 nodes
-  uint32_t fb_tie;                            // fallbacks for a near-tie (the rest: not reached)
+  uint32_t fb_tie;                            // near-ties resolved by visit order
 };
 
 // Per wave: the stack columns, 8 bytes per entry and lane (BVH: link + entry t;
@@ -194,6 +204,227 @@ __device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtm
 }
 
 __device__ __forceinline__ float clamp_inv(float x) { return fminf(fmaxf(1.f / x, -1e30f), 1e30f); }
+
+// The kTie smallest triangle hits (Triangle::hit) with t <= cap of the ray over
+// the BVH, as (t, prim) sorted by t: a search whose bound is the kTie-th
+// smallest hit so far (and cap), with the main search's box margins.  Returns
+// the number of hits <= cap found (> kTie: more exist beyond ct[kTie - 1]).
+constexpr int kTie = 8;
+__device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float rtmin, float rtmax, float cap,
+                                           int* stk_link, float* stk_t, float (&ct)[kTie], int (&cp)[kTie]) {
+  rtmax = fminf(rtmax, cap);
+#pragma unroll
+  for (int j = 0; j < kTie; ++j) {
+    ct[j] = WR_INF;
+    cp[j] = -1;
+  }
+  const V3 binv = v3(clamp_inv(d.x), clamp_inv(d.y), clamp_inv(d.z));
+  float dlen = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+  if (!(dlen > 0.f)) dlen = 1.f;
+  float tcap;
+  {
+    const float ax = (F.lo.x - o.x) * binv.x, bx = (F.hi.x - o.x) * binv.x;
+    const float ay = (F.lo.y - o.y) * binv.y, by = (F.hi.y - o.y) * binv.y;
+    const float az = (F.lo.z - o.z) * binv.z, bz = (F.hi.z - o.z) * binv.z;
+    tcap = fmaxf(0.f, fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)));
+  }
+  int found = 0, sp = 0, cur = 0;
+  for (;;) {
+    const float thi = fminf(rtmax, ct[kTie - 1]);
+    const float g = wrf::kRayGrow * (fminf(thi, tcap) * dlen + 1.f);
+    const float gt = g / dlen;
+    if (cur >= 0) {
+      const float4* np = F.nodes + 4 * static_cast<size_t>(cur);
+      const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+      const int4 lk = *reinterpret_cast<const int4*>(np + 3);
+      const float lo_t = rtmin - gt, hi_t = thi + gt;
+      auto slab = [&](float lx, float ly, float lz, float hx, float hy, float hz, float& tn) {
+        const float x0 = (lx - g - o.x) * binv.x, x1 = (hx + g - o.x) * binv.x;
+        const float y0 = (ly - g - o.y) * binv.y, y1 = (hy + g - o.y) * binv.y;
+        const float z0 = (lz - g - o.z) * binv.z, z1 = (hz + g - o.z) * binv.z;
+        tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), lo_t));
+        const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), hi_t));
+        return tn <= tf;
+      };
+      float ta, tb;
+      const bool ha = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, ta);
+      const bool hb = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tb);
+      if (ha && hb) {
+        const bool af = ta <= tb;
+        stk_link[sp * 64] = af ? lk.y : lk.x;
+        stk_t[sp * 64] = af ? tb : ta;
+        ++sp;
+        cur = af ? lk.x : lk.y;
+        continue;
+      }
+      if (ha || hb) {
+        cur = ha ? lk.x : lk.y;
+        continue;
+      }
+    } else {
+      const int l = ~cur;
+      const int first = l >> 3, cnt = (l & 7) + 1;
+      for (int j = 0; j < cnt; ++j) {
+        const float4* tp = F.tris + 3 * static_cast<size_t>(first + j);
+        float t;
+        // screen: only hits below the current kTie-th can enter the list
+        if (tri_test(tp[0], tp[1], tp[2].x, o, d, rtmin, rtmax, fminf(ct[kTie - 1], rtmax) + WR_EPS + WR_EPS, t) &&
+            t <= rtmax) {
+          ++found;
+          float nt = t;
+          int npr = __float_as_int(tp[2].y);
+#pragma unroll
+          for (int k = 0; k < kTie; ++k) {  // insertion, sorted by t
+            const bool sw = nt < ct[k];
+            const float tt = sw ? ct[k] : nt;
+            const int pp = sw ? cp[k] : npr;
+            if (sw) {
+              ct[k] = nt;
+              cp[k] = npr;
+            }
+            nt = tt;
+            npr = pp;
+          }
+        }
+      }
+    }
+    // pop the next subtree that can still hold one of the kTie smallest hits
+    const float thi2 = fminf(rtmax, ct[kTie - 1]);
+    const float gt2 = (wrf::kRayGrow * (fminf(thi2, tcap) * dlen + 1.f)) / dlen;
+    cur = 0x7fffffff;
+    while (sp > 0) {
+      --sp;
+      if (stk_t[sp * 64] <= thi2 + gt2) {
+        cur = stk_link[sp * 64];
+        break;
+      }
+    }
+    if (cur == 0x7fffffff) return found;
+  }
+}
+
+// Does the reference's traversal visit leaf A (path record offset oa, the
+// primitive at position pa of its list) before leaf B?  Same leaf: list order.
+// Otherwise both paths agree down to their last common node, where the one that
+// goes to the near child (belowFirst, :331-343) is visited first -- the far
+// child waits on the stack until the near subtree is done.
+__device__ __forceinline__ bool visits_before(const FastScene& F, int oa, int pa, int ob, int pb, V3 o, V3 d) {
+  if (oa == ob) return pa < pb;
+  const uint2* ra = F.path + oa + 4;
+  const uint2* rb = F.path + ob + 4;
+  const int n = min(static_cast<int>(F.path[oa].x), static_cast<int>(F.path[ob].x));
+  for (int k = 0; k < n; ++k) {
+    const uint2 ea = ra[k], eb = rb[k];
+    if (ea.x == eb.x && ea.y == eb.y) continue;
+    const uint32_t axis = ea.y & 3u;
+    const float split = __uint_as_float(ea.x);
+    const float oa_ = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+    const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+    const bool below = (oa_ < split) | ((oa_ == split) & (da <= 0));
+    return ((ea.y & 4u) != 0u) != below;  // A took the near child
+  }
+  return false;  // distinct leaves always diverge; not reached
+}
+
+// The first leaf of primitive p that the reference's traversal visits: its
+// path offset and p's position in its list (off = -1: p is not visited).
+__device__ __noinline__ void first_leaf(const FastScene& F, int p, V3 o, V3 d, V3 inv, float tmin0, float tmax0,
+                                        float rtmax, int& off, int& pos, uint32_t& steps) {
+  off = -1;
+  pos = 0;
+  const int lb = F.prim_leaf_off[p], le = F.prim_leaf_off[p + 1];
+  for (int k = lb; k < le; ++k) {
+    const int ok = F.prim_leaf[k], pk = F.prim_leaf_pos[k];
+    if (!kd_reaches(F.path + ok, o, d, inv, tmin0, tmax0, rtmax, steps)) continue;
+    if (off < 0 || visits_before(F, ok, pk, off, pos, o, d)) {
+      off = ok;
+      pos = pk;
+    }
+  }
+}
+
+// Resolution by visit order.  The reference's answer is first-found-wins
+// (cmp(t - best) < 0) over the hits it visits, in visit order.  Let m be the
+// smallest hit it visits.  Its winner lies within EPS of m (once m is reached
+// either m is taken or best is already within EPS of it, and afterwards only t
+// < best - EPS <= m could be taken).  A visited hit beyond m + 3 EPS, whenever
+// it is the best, lets every hit up to m + 2 EPS through (their difference
+// exceeds EPS), so with every hit up to m + 3 EPS known and no visited one
+// between m + 1.5 EPS and m + 3 EPS, the rule run over the visited hits up to
+// m + 1.5 EPS in visit order gives the reference's answer.  The kTie smallest
+// hits of the scene (bvh_collect) hold all hits up to m + 3 EPS when fewer
+// were found or the last one lies beyond.  Returns false when a condition
+// fails (the caller walks the KD tree).
+__device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin,
+                                            float rtmax, float t1, int* stk_link, float* stk_t, float& t_out,
+                                            int& p_out, uint32_t& steps, int& dbg) {
+  float tmin0, tmax0;
+  if (!box_hit(S.root_l, S.root_r, o, d, tmin0, tmax0) || rtmax < tmin0) return false;
+  const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+  float ct[kTie];
+  int cp[kTie];
+  int off[kTie], pos[kTie];
+  float m = WR_INF;
+  int n = 0;
+  // first the hits up to t1 + 3 EPS (t1 = the scene's smallest); if t1's
+  // triangle is not visited, the kTie smallest hits without a bound
+  for (int pass = 0; pass < 2; ++pass) {
+    const float cap = pass == 0 ? t1 + 3.f * WR_EPS : WR_INF;
+    n = bvh_collect(F, o, d, rtmin, rtmax, cap, stk_link, stk_t, ct, cp);
+    m = WR_INF;
+#pragma unroll
+    for (int c = 0; c < kTie; ++c) {  // per candidate: its first visited leaf (-1: none)
+      off[c] = -1;
+      pos[c] = 0;
+      if (c < min(n, kTie)) {
+        first_leaf(F, cp[c], o, d, inv, tmin0, tmax0, rtmax, off[c], pos[c], steps);
+        if (off[c] >= 0 && m == WR_INF) m = ct[c];  // sorted by t: the first visited one
+      }
+    }
+    if (pass == 0 && m == t1) break;  // the window t1 + 3 EPS is complete when n <= kTie
+  }
+  dbg = n;
+  const int nc = min(n, kTie);
+  // m < 4096: fl(m + 3 EPS) is within EPS / 4 of m + 3 EPS
+  if (!(m < 4096.f)) return false;
+  const float lim = m + 3.f * WR_EPS;
+  if (n > kTie && !(ct[kTie - 1] > lim)) return false;  // hits up to m + 3 EPS may be missing
+  bool band = false;
+#pragma unroll
+  for (int c = 0; c < kTie; ++c)
+    if (c < nc && off[c] >= 0 && ct[c] <= lim && ct[c] - m > 1.5f * WR_EPS) band = true;  // exact difference
+  if (band) return false;
+  // first-found-wins over the visited candidates up to m + 1.5 EPS, in visit
+  // order: each candidate's rank, then the rule rank by rank (compile-time
+  // indices only: the lists stay in registers)
+  bool use[kTie];
+#pragma unroll
+  for (int c = 0; c < kTie; ++c) use[c] = c < nc && off[c] >= 0 && ct[c] - m <= 1.5f * WR_EPS;
+  int rank[kTie];
+#pragma unroll
+  for (int c = 0; c < kTie; ++c) {
+    rank[c] = 0;
+#pragma unroll
+    for (int e = 0; e < kTie; ++e)
+      if (e != c && use[c] && use[e] && visits_before(F, off[e], pos[e], off[c], pos[c], o, d)) ++rank[c];
+  }
+  float best = WR_INF;
+  int win = -1;
+#pragma unroll
+  for (int k = 0; k < kTie; ++k) {
+#pragma unroll
+    for (int c = 0; c < kTie; ++c) {
+      if (use[c] && rank[c] == k && cmpf(ct[c] - best) < 0) {
+        best = ct[c];
+        win = cp[c];
+      }
+    }
+  }
+  dbg |= 1 << 8;
+  t_out = best;
+  p_out = win;
+  return true;
+}
 
 // launch index -> (queue, index in it), as k_trace numbers a launch's rays
 struct QueueIndex {
@@ -412,20 +643,74 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   }
 }
 
+// one atomic per wave: this lane's slot in a list (or -1 if !want)
+__device__ __forceinline__ int fast_append(int* counter, bool want) {
+  const unsigned long long m = __ballot(want);
+  if (m == 0ull) return -1;
+  const int lane = __lane_id();
+  const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader);
+  return want ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
 // k_fast_resolve: one ray per lane (grid-stride over the launch's indices).
+// The rare rays it cannot settle (near-ties, t1 not reached) go to `hard` for
+// k_fast_hard, so that their register-hungry code does not lower this
+// kernel's occupancy.
 template <bool COUNT>
 __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
-                                             const float* t2buf, uint32_t* lds, FastCounters& ctr) {
+                                             const float* t2buf, int* hard, int* hard_n, FastCounters& ctr) {
+  const int lane = __lane_id();
+  const QueueIndex QI(Q);
+  // every lane of the wave takes part in each list append (whole iterations)
+  for (int base = blockIdx.x * 64; base < QI.n; base += gridDim.x * 64) {
+    const int idx = base + lane;
+    bool need = false;
+    if (idx < QI.n) {
+      int q, r;
+      QI.locate(idx, q, r);
+      const int p1 = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r];
+      if (p1 >= 0) {  // (no hit anywhere: a miss for the reference too)
+        const float t1 = qfield(Q, q, [](const RayQueue& x) { return x.out_t; })[r], t2 = t2buf[idx];
+        const bool tie = !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0);
+        if (tie) {
+          need = true;
+        } else {
+          const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
+          const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
+          const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
+          const float* tmx = qfield(Q, q, [](const RayQueue& x) { return x.tmax; });
+          const V3 o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
+          const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+          uint32_t steps = 0;
+          const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
+          need = !kd_member(S, F, lb, ln, o, d, tmx ? tmx[r] : WR_INF, t1, steps);
+          if (COUNT) ctr.replay += steps;
+        }
+      }
+    }
+    const int slot = fast_append(hard_n, need);
+    if (need) hard[slot] = idx;
+  }
+}
+
+// k_fast_hard: the rays k_fast_resolve listed, one per lane.
+template <bool COUNT>
+__device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
+                                          const float* t2buf, const int* hard, const int* hard_n, uint32_t* lds,
+                                          FastCounters& ctr) {
   const int lane = __lane_id();
   int* stk_node = reinterpret_cast<int*>(lds) + lane;
   float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
   const QueueIndex QI(Q);
-  for (int idx = blockIdx.x * 64 + lane; idx < QI.n; idx += gridDim.x * 64) {
+  const int nh = *hard_n;
+  for (int i = blockIdx.x * 64 + lane; i < nh; i += gridDim.x * 64) {
+    const int idx = hard[i];
     int q, r;
     QI.locate(idx, q, r);
     int* outp = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; });
-    const int p1 = outp[r];
-    if (p1 < 0) continue;  // no hit anywhere: a miss for the reference too
     float* outt = qfield(Q, q, [](const RayQueue& x) { return x.out_t; });
     const float t1 = outt[r], t2 = t2buf[idx];
     const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
@@ -435,22 +720,32 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
     const float* tmx = qfield(Q, q, [](const RayQueue& x) { return x.tmax; });
     const V3 o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
     const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
-    const float rtmax = tmx ? tmx[r] : WR_INF;
-    uint32_t steps = 0;
-    const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
-    const bool tie = !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0);
-    const bool ok = !tie && kd_member(S, F, lb, ln, o, d, rtmax, t1, steps);
-    if (COUNT) ctr.replay += steps;
-    if (ok) continue;
-    // near-tie or not reached by the reference's walk: the walk itself decides
-    if (COUNT) {
-      ++ctr.fallback;
-      ctr.fb_tie += tie ? 1u : 0u;
-    }
-    if (F.diag & 1) continue;
+    const float rtmin = tmn ? tmn[r] : 0.f, rtmax = tmx ? tmx[r] : WR_INF;
+    (void)t2;
     float tb;
     int pb;
-    kd_walk<COUNT>(S, o, d, tmn ? tmn[r] : 0.f, rtmax, stk_node, stk_tmin, tb, pb, ctr);
+    if (!(F.diag & 2)) {
+      uint32_t steps = 0;
+      int dbg = 0;
+      const bool done = resolve_tie(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, dbg);
+      if (F.diag & 4) {  // debug: the resolution record instead of the answer
+        outp[r] = -2 - dbg;
+        continue;
+      }
+      if (COUNT) {
+        ctr.replay += steps;
+        ctr.fb_tie += done ? 1u : 0u;
+      }
+      if (done) {
+        outt[r] = tb;
+        outp[r] = pb;
+        continue;
+      }
+    }
+    // unresolved (a crowd of hits near m, or visited hits in the band): the walk decides
+    if (COUNT) ++ctr.fallback;
+    if (F.diag & 1) continue;
+    kd_walk<COUNT>(S, o, d, rtmin, rtmax, stk_node, stk_tmin, tb, pb, ctr);
     outt[r] = tb;
     outp[r] = pb;
   }

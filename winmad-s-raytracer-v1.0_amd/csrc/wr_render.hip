@@ -88,9 +88,11 @@ struct StepCounters {
   int vcm_pending;    // VCM: light paths whose first vertex is an emitter (k_vcm_fixup)
   int vcm_nverts;     // VCM: light vertices in the merge grid
   int mq[kSlots];     // VCM: merge queries queued at step `slot`
+  int hard[kSlots];   // WR_TRACE_BVH: rays of step `slot` left to k_fast_hard
 };
 struct DevCounters {
   int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
+  int hard;   // API path: rays left to k_fast_hard
   unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
   unsigned long long closest, shadow, inner, leaves, refs, tests;
   unsigned long long vm_queries, vm_found, vm_merged;  // VCM range queries / vertices in radius / merges
@@ -213,10 +215,18 @@ k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetc
 }
 template <bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
-k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf) {
+k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf, int* hard, int* hard_n) {
+  FastCounters fc{};
+  resolve_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, fc);
+  if (COUNT) fast_counts<COUNT>(ctr, fc);
+}
+template <bool COUNT>
+__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
+k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf, const int* hard,
+            const int* hard_n) {
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
-  resolve_fast<COUNT>(S, F, Q, t2buf, smem, fc);
+  hard_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, smem, fc);
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 
@@ -673,17 +683,20 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, int
 // WR_TRACE_BVH mode the per-ray t2 scratch of the BVH search (>= the launch's rays).
 struct TraceSlot {
   int* fetch;
-  float* t2;
+  float* t2;      // [t2_cap] t2 per launch index, then [t2_cap] the hard-ray list
   size_t t2_cap;
+  int* hard_n;
 };
-TraceSlot tslot(Pipe& p, int slot) { return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap}; }
-// t2 scratch of a pipeline for launches of up to `rays` rays
+TraceSlot tslot(Pipe& p, int slot) {
+  return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap, &p.sc[0].hard[slot]};
+}
+// t2 scratch + hard-ray list of a pipeline for launches of up to `rays` rays
 int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
   if (!c->fast_on || p.t2_cap >= rays) return WR_OK;
   if (p.t2buf) (void)hipFree(p.t2buf);
   p.t2buf = nullptr;
   p.t2_cap = 0;
-  HIPCHK(hipMalloc(&p.t2buf, rays * sizeof(float)));
+  HIPCHK(hipMalloc(&p.t2buf, 2 * rays * sizeof(float)));
   p.t2_cap = rays;
   return WR_OK;
 }
@@ -708,9 +721,13 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     }
     hipLaunchKernelGGL(count ? k_trace_fast<true> : k_trace_fast<false>, dim3(fgrid), dim3(kTraceBlock), lds, stream,
                        c->ds, c->fs, Q, ctr, fetch, ts.t2);
+    int* hard = reinterpret_cast<int*>(ts.t2 + ts.t2_cap);
     hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
-                       dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), lds, stream, c->ds,
-                       c->fs, Q, ctr, ts.t2);
+                       dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), 0, stream, c->ds, c->fs,
+                       Q, ctr, ts.t2, hard, ts.hard_n);
+    // the hard rays are a few in 10^4: a small grid drains any count
+    hipLaunchKernelGGL(count ? k_fast_hard<true> : k_fast_hard<false>, dim3(std::max(1, std::min(256, blocks))),
+                       dim3(kTraceBlock), lds, stream, c->ds, c->fs, Q, ctr, ts.t2, hard, ts.hard_n);
     tm.mark(WR_K_TRACE);
     if (c->trace_log) {
       (void)hipEventRecord(f1, stream);
@@ -845,7 +862,7 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
       HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
       ties += h.stamps[4];
     }
-    std::fprintf(stderr, "[wr bvh tail] max nodes/ray %llu, max tests/ray %llu, rays > 256 nodes %llu, tie fallbacks %llu\n",
+    std::fprintf(stderr, "[wr bvh tail] max nodes/ray %llu, max tests/ray %llu, rays > 256 nodes %llu, ties resolved by visit order %llu\n",
                  mx[0], mx[1], mx[2], ties);
   }
   if (c->stamps) {
@@ -1221,7 +1238,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       const size_t fbn = fh.nodes.size(), ftr = fh.tris.size(), fpo = fh.prim_leaf_off.size(),
                    fpl = std::max<size_t>(1, fh.prim_leaf.size()), fpa = fh.path.size() / 2;
       const size_t fbytes = measure([&](Arena& a) {
-        a.take<wrf::BNode>(fbn); a.take<wrf::TriRec>(ftr); a.take<int>(fpo); a.take<int>(fpl); a.take<uint2>(fpa);
+        a.take<wrf::BNode>(fbn); a.take<wrf::TriRec>(ftr); a.take<int>(fpo); a.take<int>(fpl); a.take<int>(fpl);
+        a.take<uint2>(fpa);
       });
       if (int rc = c->fast_mem.reserve(fbytes)) {
         wr_destroy(c);
@@ -1232,12 +1250,15 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       auto* dtr = F.take<wrf::TriRec>(ftr);
       int* dpo = F.take<int>(fpo);
       int* dpl = F.take<int>(fpl);
+      int* dpp = F.take<int>(fpl);
       uint2* dpa = F.take<uint2>(fpa);
       hipError_t fe = hipSuccess;
       for (hipError_t x : {hipMemcpy(dno, fh.nodes.data(), fbn * sizeof(wrf::BNode), hipMemcpyHostToDevice),
                            hipMemcpy(dtr, fh.tris.data(), ftr * sizeof(wrf::TriRec), hipMemcpyHostToDevice),
                            hipMemcpy(dpo, fh.prim_leaf_off.data(), fpo * sizeof(int), hipMemcpyHostToDevice),
                            hipMemcpy(dpl, fh.prim_leaf.data(), fh.prim_leaf.size() * sizeof(int), hipMemcpyHostToDevice),
+                           hipMemcpy(dpp, fh.prim_leaf_pos.data(), fh.prim_leaf_pos.size() * sizeof(int),
+                                     hipMemcpyHostToDevice),
                            hipMemcpy(dpa, fh.path.data(), fpa * sizeof(uint2), hipMemcpyHostToDevice)})
         if (x != hipSuccess) fe = x;
       if (fe != hipSuccess) {
@@ -1249,6 +1270,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       fs.tris = reinterpret_cast<const float4*>(dtr);
       fs.prim_leaf_off = dpo;
       fs.prim_leaf = dpl;
+      fs.prim_leaf_pos = dpp;
       fs.path = dpa;
       float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
       for (int k = 0; k < 3; ++k) {
@@ -1366,12 +1388,12 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
     if (c->api_t2) (void)hipFree(c->api_t2);
     c->api_t2 = nullptr;
     c->api_t2_cap = 0;
-    HIPCHK(hipMalloc(&c->api_t2, nb * sizeof(float)));
+    HIPCHK(hipMalloc(&c->api_t2, 2 * nb * sizeof(float)));
     c->api_t2_cap = nb;
   }
   QueueList ql;
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
-  const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap};
+  const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard};
   trace_launch(c, c->stream, c->ctr, ts, tm, false, ql.Q, ql.max_rays,
                c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN));
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
