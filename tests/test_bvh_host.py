@@ -1,0 +1,41 @@
+"""CPU checks of the verified-BVH data built on the host (wr_bvh.cpp): every
+triangle in exactly one BVH leaf with its Triangle::hit record, boxes nested and
+holding their triangles, and the KD membership data (each primitive's leaves,
+its position in them, the root paths) equal to the reference tree's
+(tests/native/bvh_check.cpp, compiled here from the product's own sources)."""
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+import _scenes
+from winmad_rt import scenes
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "winmad-s-raytracer-v1.0_amd", "csrc")
+_bin = {}
+
+
+def checker():
+    if "b" not in _bin:
+        out = os.path.join(tempfile.mkdtemp(prefix="wr_bvhchk_"), "bvh_check")
+        subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-I", os.path.join(REPO, "include"),
+                        os.path.join(REPO, "tests", "native", "bvh_check.cpp"), os.path.join(CSRC, "wr_scene.cpp"),
+                        os.path.join(CSRC, "wr_bvh.cpp"), "-o", out, "-lpthread"], check=True)
+        _bin["b"] = out
+    return _bin["b"]
+
+
+def small_torus():
+    p = os.path.join(_scenes._DIR, "torus_small.obj")
+    if not os.path.exists(p):
+        scenes.synth_torus_obj(p, U=200, V=100)
+    return _scenes.path("torus_small.scene", scenes.torus_scene(64, 64, "bdpt", torus_obj=p))
+
+
+@pytest.mark.parametrize("maker", [lambda: _scenes.torus(64, 64), lambda: _scenes.cbox(64, 48), small_torus],
+                         ids=["torus", "cbox_dragon", "synthetic_torus_40k"])
+def test_bvh_structure(maker):
+    r = subprocess.run([checker(), maker()], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr

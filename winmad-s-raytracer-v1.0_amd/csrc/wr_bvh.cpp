@@ -189,6 +189,7 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
     float lo[3], hi[3];   // the node's cell: the root box cut by the splits above
   };
   std::vector<Item> st;
+  out.node_path.assign(s.nodes.size(), -1);
   st.push_back({0, 0, 0u, 0u, {s.root_l.x, s.root_l.y, s.root_l.z}, {s.root_r.x, s.root_r.y, s.root_r.z}});
   while (!st.empty()) {
     const Item it = st.back();
@@ -219,6 +220,7 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
         out.path.push_back(0u);
       }
       const int32_t off = static_cast<int32_t>(out.path.size() / 2);
+      out.node_path[static_cast<size_t>(it.node)] = off;
       out.path.push_back(static_cast<uint32_t>(it.depth));
       out.path.push_back(0u);
       for (int a = 0; a < 3; ++a) {  // the leaf's cell (orders the replays)

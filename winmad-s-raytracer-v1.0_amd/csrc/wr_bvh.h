@@ -59,7 +59,8 @@ static_assert(sizeof(TriRec) == 48, "BVH triangle record is 48 bytes");
 // leaf's cell, which orders the replays -- then n entries (split bits,
 // axis | went_right << 2) from the root down; 8 zero entries pad the array's end.
 // prim_leaf[prim_leaf_off[p] .. prim_leaf_off[p+1]) = path offsets of the KD
-// leaves that hold primitive p, prim_leaf_pos = its index in each leaf's list.
+// leaves that hold primitive p (ascending), prim_leaf_pos = its index in each
+// leaf's list; node_path maps a KD leaf node to its record.
 #ifndef WR_BVH_LEAF
 #define WR_BVH_LEAF 4
 #endif
@@ -88,6 +89,7 @@ struct FastHost {
   std::vector<BNode> nodes;
   std::vector<TriRec> tris;
   std::vector<int32_t> prim_leaf_off, prim_leaf, prim_leaf_pos;
+  std::vector<int32_t> node_path;  // KD leaf node -> its path record offset (-1: inner node)
   std::vector<uint32_t> path;  // pairs
   int depth = 0;               // deepest node chain (stack bound)
   int leaves = 0;

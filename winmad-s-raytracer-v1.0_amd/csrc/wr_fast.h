@@ -42,6 +42,7 @@ struct FastScene {
   const int* prim_leaf;
   const int* prim_leaf_pos;
   const uint2* path;
+  const int* node_path;  // KD leaf node -> path record offset
   V3 lo, hi;  // union of the (grown) triangle boxes
   int depth;  // stack entries (BVH search and KD fallback walk)
   int diag;   // WR_BVH_DIAG: 1 = skip the KD walks (wrong answers, measurement only); 2 = KD walk for every tie
@@ -61,9 +62,14 @@ __host__ __device__ constexpr size_t fast_lds_bytes(int depth) { return size_t(d
 // KDtreeAccel::traverse reaches the leaf whose root path is rec[1..n]: the
 // near / far rule (:331-357) and the `ray.tmax < tmin` stop (:323), evaluated
 // with the reference's floats along that one path.  (tmin, tmax) = root clip.
-// The record is read 8 entries (4 x 16 bytes) per round trip.
+// The record is read 8 entries (4 x 16 bytes) per round trip.  `key` gets the
+// leaf's place in the ray's visit order: bit 63 - k is set when the path takes
+// the far child at depth k.  The walk visits a node's near subtree before its
+// far one, so for two visited leaves the smaller key is visited first (their
+// paths part at a node where one goes near, the other far).
 __device__ __forceinline__ bool kd_reaches(const uint2* rec, V3 o, V3 d, V3 inv, float tmin, float tmax, float rtmax,
-                                           uint32_t& steps) {
+                                           uint32_t& steps, unsigned long long& key) {
+  key = 0ull;
   const int n = static_cast<int>(rec[0].x);
   const uint4* R = reinterpret_cast<const uint4*>(rec + 4);  // after the header
   for (int base = 0;; base += 8) {
@@ -85,6 +91,7 @@ __device__ __forceinline__ bool kd_reaches(const uint2* rec, V3 o, V3 d, V3 inv,
       const float t = (split - oa) * ia;
       const bool below = (oa < split) | ((oa == split) & (da <= 0));
       const bool is_near = right != below;  // near = left iff below
+      if (!is_near) key |= 1ull << (63 - min(k - 1, 63));
       const bool go_near = (t > tmax) | (t <= 0);
       const bool go_far = !go_near & (t < tmin);
       if (go_near) {
@@ -102,6 +109,34 @@ __device__ __forceinline__ bool kd_reaches(const uint2* rec, V3 o, V3 d, V3 inv,
   }
 }
 
+// The KD leaf whose cell holds point p (descent by p's coordinates, three
+// levels per 64-byte record): its path record offset.
+__device__ __forceinline__ int kd_locate(const DevScene& S, const FastScene& F, V3 p) {
+  uint32_t node = 0;
+  for (;;) {
+    const uint4* rp = S.nrec3 + 4 * static_cast<size_t>(node);
+    const uint4 q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3];
+    // entries: 0 self, 1 L, 2 R, 3 LL, 4 LR, 5 RL, 6 RR (two per uint4)
+    const uint2 e[7] = {make_uint2(q0.x, q0.y), make_uint2(q0.z, q0.w), make_uint2(q1.x, q1.y),
+                        make_uint2(q1.z, q1.w), make_uint2(q2.x, q2.y), make_uint2(q2.z, q2.w),
+                        make_uint2(q3.x, q3.y)};
+    int h = 0;
+    uint32_t at = node;
+#pragma unroll
+    for (int lev = 0; lev < 3; ++lev) {
+      const uint2 w = e[h];
+      if ((w.y & 3u) == 3u) return F.node_path[at];
+      const uint32_t axis = w.y & 3u;
+      const float split = __uint_as_float(w.x);
+      const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+      const bool right = !(pa < split);
+      at = right ? (w.y >> 2) : at + 1;
+      h = 2 * h + (right ? 2 : 1);
+      if (lev == 2) node = at;
+    }
+  }
+}
+
 // Is the primitive whose KD leaves are prim_leaf[lb, lb + ln) tested by the
 // reference's traversal of this ray?
 __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F, int lb, int ln, V3 o, V3 d,
@@ -109,9 +144,23 @@ __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F,
   float tmin, tmax;
   if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) return false;  // :312-313, :323
   const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+  const V3 p = o + d * t_hit;
+  unsigned long long key;
+  if (ln > 4) {
+    // a big primitive (walls: hundreds of leaves): the leaf holding the hit
+    // point, found by descent, then by binary search in the (ascending) list
+    const int want = kd_locate(S, F, p);
+    int a = lb, b = lb + ln;
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (F.prim_leaf[mid] < want) a = mid + 1;
+      else b = mid;
+    }
+    if (a < lb + ln && F.prim_leaf[a] == want && kd_reaches(F.path + want, o, d, inv, tmin, tmax, rtmax, steps, key))
+      return true;
+  }
   // the leaves whose cell holds the hit point first (usually the one reached),
   // then the others
-  const V3 p = o + d * t_hit;
   for (int pass = 0; pass < 2; ++pass) {
     for (int k = lb; k < lb + ln; ++k) {
       const uint2* rec = F.path + F.prim_leaf[k];
@@ -119,7 +168,7 @@ __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F,
       const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
       const bool in = p.x >= __uint_as_float(h0.z) && p.y >= __uint_as_float(h0.w) && p.z >= __uint_as_float(h1.x) &&
                       p.x <= __uint_as_float(h1.y) && p.y <= __uint_as_float(h1.z) && p.z <= __uint_as_float(h1.w);
-      if (in == (pass == 0) && kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps)) return true;
+      if (in == (pass == 0) && kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return true;
     }
   }
   return false;
@@ -210,6 +259,7 @@ __device__ __forceinline__ float clamp_inv(float x) { return fminf(fmaxf(1.f / x
 // smallest hit so far (and cap), with the main search's box margins.  Returns
 // the number of hits <= cap found (> kTie: more exist beyond ct[kTie - 1]).
 constexpr int kTie = 8;
+constexpr int kTieLeaves = 16;  // resolve_tie: at most this many KD leaves per candidate
 __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float rtmin, float rtmax, float cap,
                                            int* stk_link, float* stk_t, float (&ct)[kTie], int (&cp)[kTie]) {
   rtmax = fminf(rtmax, cap);
@@ -303,41 +353,20 @@ __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float
   }
 }
 
-// Does the reference's traversal visit leaf A (path record offset oa, the
-// primitive at position pa of its list) before leaf B?  Same leaf: list order.
-// Otherwise both paths agree down to their last common node, where the one that
-// goes to the near child (belowFirst, :331-343) is visited first -- the far
-// child waits on the stack until the near subtree is done.
-__device__ __forceinline__ bool visits_before(const FastScene& F, int oa, int pa, int ob, int pb, V3 o, V3 d) {
-  if (oa == ob) return pa < pb;
-  const uint2* ra = F.path + oa + 4;
-  const uint2* rb = F.path + ob + 4;
-  const int n = min(static_cast<int>(F.path[oa].x), static_cast<int>(F.path[ob].x));
-  for (int k = 0; k < n; ++k) {
-    const uint2 ea = ra[k], eb = rb[k];
-    if (ea.x == eb.x && ea.y == eb.y) continue;
-    const uint32_t axis = ea.y & 3u;
-    const float split = __uint_as_float(ea.x);
-    const float oa_ = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-    const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-    const bool below = (oa_ < split) | ((oa_ == split) & (da <= 0));
-    return ((ea.y & 4u) != 0u) != below;  // A took the near child
-  }
-  return false;  // distinct leaves always diverge; not reached
-}
-
-// The first leaf of primitive p that the reference's traversal visits: its
-// path offset and p's position in its list (off = -1: p is not visited).
+// The first leaf of primitive p that the reference's traversal visits, as its
+// visit key (kd_reaches) and p's position in that leaf's list; key = ~0: p is
+// not visited.  (pos < 256, so (key, pos) orders the visits of one ray.)
 __device__ __noinline__ void first_leaf(const FastScene& F, int p, V3 o, V3 d, V3 inv, float tmin0, float tmax0,
-                                        float rtmax, int& off, int& pos, uint32_t& steps) {
-  off = -1;
+                                        float rtmax, unsigned long long& key, int& pos, uint32_t& steps) {
+  key = ~0ull;
   pos = 0;
   const int lb = F.prim_leaf_off[p], le = F.prim_leaf_off[p + 1];
   for (int k = lb; k < le; ++k) {
-    const int ok = F.prim_leaf[k], pk = F.prim_leaf_pos[k];
-    if (!kd_reaches(F.path + ok, o, d, inv, tmin0, tmax0, rtmax, steps)) continue;
-    if (off < 0 || visits_before(F, ok, pk, off, pos, o, d)) {
-      off = ok;
+    unsigned long long kk;
+    if (!kd_reaches(F.path + F.prim_leaf[k], o, d, inv, tmin0, tmax0, rtmax, steps, kk)) continue;
+    const int pk = F.prim_leaf_pos[k];
+    if (kk < key || (kk == key && pk < pos)) {
+      key = kk;
       pos = pk;
     }
   }
@@ -363,7 +392,8 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
   const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
   float ct[kTie];
   int cp[kTie];
-  int off[kTie], pos[kTie];
+  unsigned long long key[kTie];
+  int pos[kTie];
   float m = WR_INF;
   int n = 0;
   // first the hits up to t1 + 3 EPS (t1 = the scene's smallest); if t1's
@@ -373,12 +403,15 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
     n = bvh_collect(F, o, d, rtmin, rtmax, cap, stk_link, stk_t, ct, cp);
     m = WR_INF;
 #pragma unroll
-    for (int c = 0; c < kTie; ++c) {  // per candidate: its first visited leaf (-1: none)
-      off[c] = -1;
+    for (int c = 0; c < kTie; ++c) {  // per candidate: its first visited leaf (~0: none)
+      key[c] = ~0ull;
       pos[c] = 0;
       if (c < min(n, kTie)) {
-        first_leaf(F, cp[c], o, d, inv, tmin0, tmax0, rtmax, off[c], pos[c], steps);
-        if (off[c] >= 0 && m == WR_INF) m = ct[c];  // sorted by t: the first visited one
+        // a primitive in many leaves (walls): the KD walk is cheaper than
+        // replaying every one of them
+        if (F.prim_leaf_off[cp[c] + 1] - F.prim_leaf_off[cp[c]] > kTieLeaves) return false;
+        first_leaf(F, cp[c], o, d, inv, tmin0, tmax0, rtmax, key[c], pos[c], steps);
+        if (key[c] != ~0ull && m == WR_INF) m = ct[c];  // sorted by t: the first visited one
       }
     }
     if (pass == 0 && m == t1) break;  // the window t1 + 3 EPS is complete when n <= kTie
@@ -392,21 +425,21 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
   bool band = false;
 #pragma unroll
   for (int c = 0; c < kTie; ++c)
-    if (c < nc && off[c] >= 0 && ct[c] <= lim && ct[c] - m > 1.5f * WR_EPS) band = true;  // exact difference
+    if (c < nc && key[c] != ~0ull && ct[c] <= lim && ct[c] - m > 1.5f * WR_EPS) band = true;  // exact difference
   if (band) return false;
   // first-found-wins over the visited candidates up to m + 1.5 EPS, in visit
   // order: each candidate's rank, then the rule rank by rank (compile-time
   // indices only: the lists stay in registers)
   bool use[kTie];
 #pragma unroll
-  for (int c = 0; c < kTie; ++c) use[c] = c < nc && off[c] >= 0 && ct[c] - m <= 1.5f * WR_EPS;
+  for (int c = 0; c < kTie; ++c) use[c] = c < nc && key[c] != ~0ull && ct[c] - m <= 1.5f * WR_EPS;
   int rank[kTie];
 #pragma unroll
   for (int c = 0; c < kTie; ++c) {
     rank[c] = 0;
 #pragma unroll
     for (int e = 0; e < kTie; ++e)
-      if (e != c && use[c] && use[e] && visits_before(F, off[e], pos[e], off[c], pos[c], o, d)) ++rank[c];
+      if (e != c && use[c] && use[e] && (key[e] < key[c] || (key[e] == key[c] && pos[e] < pos[c]))) ++rank[c];
   }
   float best = WR_INF;
   int win = -1;

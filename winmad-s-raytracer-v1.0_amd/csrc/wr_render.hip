@@ -1237,9 +1237,10 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     if (fh.ok) {
       const size_t fbn = fh.nodes.size(), ftr = fh.tris.size(), fpo = fh.prim_leaf_off.size(),
                    fpl = std::max<size_t>(1, fh.prim_leaf.size()), fpa = fh.path.size() / 2;
+      const size_t fnp = fh.node_path.size();
       const size_t fbytes = measure([&](Arena& a) {
         a.take<wrf::BNode>(fbn); a.take<wrf::TriRec>(ftr); a.take<int>(fpo); a.take<int>(fpl); a.take<int>(fpl);
-        a.take<uint2>(fpa);
+        a.take<uint2>(fpa); a.take<int>(fnp);
       });
       if (int rc = c->fast_mem.reserve(fbytes)) {
         wr_destroy(c);
@@ -1252,6 +1253,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       int* dpl = F.take<int>(fpl);
       int* dpp = F.take<int>(fpl);
       uint2* dpa = F.take<uint2>(fpa);
+      int* dnp = F.take<int>(fnp);
       hipError_t fe = hipSuccess;
       for (hipError_t x : {hipMemcpy(dno, fh.nodes.data(), fbn * sizeof(wrf::BNode), hipMemcpyHostToDevice),
                            hipMemcpy(dtr, fh.tris.data(), ftr * sizeof(wrf::TriRec), hipMemcpyHostToDevice),
@@ -1259,7 +1261,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                            hipMemcpy(dpl, fh.prim_leaf.data(), fh.prim_leaf.size() * sizeof(int), hipMemcpyHostToDevice),
                            hipMemcpy(dpp, fh.prim_leaf_pos.data(), fh.prim_leaf_pos.size() * sizeof(int),
                                      hipMemcpyHostToDevice),
-                           hipMemcpy(dpa, fh.path.data(), fpa * sizeof(uint2), hipMemcpyHostToDevice)})
+                           hipMemcpy(dpa, fh.path.data(), fpa * sizeof(uint2), hipMemcpyHostToDevice),
+                           hipMemcpy(dnp, fh.node_path.data(), fnp * sizeof(int), hipMemcpyHostToDevice)})
         if (x != hipSuccess) fe = x;
       if (fe != hipSuccess) {
         wr_destroy(c);
@@ -1272,6 +1275,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       fs.prim_leaf = dpl;
       fs.prim_leaf_pos = dpp;
       fs.path = dpa;
+      fs.node_path = dnp;
       float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
       for (int k = 0; k < 3; ++k) {
         lo[k] = std::min(fh.nodes[0].b[k], fh.nodes[0].b[6 + k]);
