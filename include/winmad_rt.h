@@ -134,6 +134,10 @@ typedef struct {
   int64_t bvh_tests;         /* triangle tests of the BVH search                */
   int64_t kd_replay_steps;   /* KD path entries replayed (membership checks)    */
   int64_t fallback_rays;     /* rays handed to the faithful KD traversal        */
+  /* WR_TRACE_BVH with env WR_BVH_VERIFY=1 (validation, slow): every ray is
+   * traced again by the reference's KD walk and the two answers compared.     */
+  int64_t verify_rays;
+  int64_t verify_mismatches; /* (t, primitive) pairs that differ bit for bit      */
 } wr_stats;
 
 /* ---- scene (Scene::init, scene/scene.cpp:469-489 + loadScene :259-467) ---- */

@@ -161,3 +161,27 @@ def test_bvh_bdpt_render_1m_triangles():
     fb, sb = fast.render_bdpt(192, 108, iterations=2, seed=3, count_work=True)
     assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
     assert _film_close(fa, fb)
+
+
+@pytest.mark.parametrize("name,maker,kind", [("torus", lambda: _scenes.torus(256, 256), "bdpt"),
+                                             ("torus_vcm", lambda: _scenes.torus(256, 256), "vcm"),
+                                             ("cbox", lambda: _scenes.cbox(256, 192), "pt"),
+                                             ("torus1m", lambda: big_torus(128, 72), "bdpt")])
+def test_bvh_verify_every_ray_against_the_kd_walk(name, maker, kind, monkeypatch):
+    """WR_BVH_VERIFY: every ray of a render is traced again by the reference's
+    KD walk inside the library and the (t, primitive) pairs are compared bit for
+    bit: no mismatch, and every ray checked."""
+    monkeypatch.setenv("WR_BVH_VERIFY", "1")
+    s = native.Scene(maker())
+    c = native.Context(s, 0)
+    c.set_trace_mode(native.TRACE_BVH)
+    if kind == "pt":
+        _, st = c.render_path(256, 192, spp=4, max_depth=7, seed=3)
+    elif kind == "vcm":
+        _, st = c.render_vcm(256, 256, iterations=2, seed=3)
+    elif name == "torus1m":
+        _, st = c.render_bdpt(128, 72, iterations=2, seed=3)
+    else:
+        _, st = c.render_bdpt(256, 256, iterations=4, seed=3)
+    assert st.verify_rays == st.closest_rays + st.shadow_rays > 0
+    assert st.verify_mismatches == 0, (st.verify_mismatches, st.verify_rays)

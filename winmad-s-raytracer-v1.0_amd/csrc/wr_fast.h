@@ -784,4 +784,33 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
   }
 }
 
+// k_fast_verify (WR_BVH_VERIFY=1, validation only): the reference's KD walk
+// for every ray of the launch, compared bit for bit with the BVH mode's answer.
+__device__ __forceinline__ void verify_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, uint32_t* lds,
+                                            uint32_t& rays, uint32_t& bad) {
+  const int lane = __lane_id();
+  int* stk_node = reinterpret_cast<int*>(lds) + lane;
+  float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
+  const QueueIndex QI(Q);
+  FastCounters dummy{};
+  for (int idx = blockIdx.x * 64 + lane; idx < QI.n; idx += gridDim.x * 64) {
+    int q, r;
+    QI.locate(idx, q, r);
+    const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
+    const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
+    const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
+    const float* tmn = qfield(Q, q, [](const RayQueue& x) { return x.tmin; });
+    const float* tmx = qfield(Q, q, [](const RayQueue& x) { return x.tmax; });
+    const V3 o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
+    const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+    float tb;
+    int pb;
+    kd_walk<false>(S, o, d, tmn ? tmn[r] : 0.f, tmx ? tmx[r] : WR_INF, stk_node, stk_tmin, tb, pb, dummy);
+    const int p = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r];
+    const float t = qfield(Q, q, [](const RayQueue& x) { return x.out_t; })[r];
+    ++rays;
+    if (p != pb || (pb >= 0 && __float_as_uint(t) != __float_as_uint(tb))) ++bad;
+  }
+}
+
 }  // namespace wrd

@@ -97,6 +97,7 @@ struct DevCounters {
   unsigned long long closest, shadow, inner, leaves, refs, tests;
   unsigned long long vm_queries, vm_found, vm_merged;  // VCM range queries / vertices in radius / merges
   unsigned long long bvh_nodes, bvh_tests, kd_replay, fallback;  // WR_TRACE_BVH work (count_work)
+  unsigned long long verify_rays, verify_bad;                   // WR_BVH_VERIFY
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -228,6 +229,18 @@ k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const floa
   FastCounters fc{};
   hard_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, smem, fc);
   if (COUNT) fast_counts<COUNT>(ctr, fc);
+}
+
+__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
+k_fast_verify(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr) {
+  extern __shared__ uint32_t smem[];
+  uint32_t rays = 0, bad = 0;
+  verify_fast(S, F, Q, smem, rays, bad);
+  const unsigned long long a = wave_sum(rays), b = wave_sum(bad);
+  if (lane_id() == 0) {
+    atomicAdd(&ctr->verify_rays, a);
+    atomicAdd(&ctr->verify_bad, b);
+  }
 }
 
 // C-ABI traversal, before: AoS wr_ray -> SoA queue (occlusion rays re-normalised
@@ -398,6 +411,7 @@ struct wr_context {
   bool fast_ok = false;   // scene supports it
   bool fast_on = false;   // WR_TRACE_BVH mode selected
   int fast_blocks = 4096; // resident one-wave workgroups of k_trace_fast
+  bool verify = false;      // WR_BVH_VERIFY=1: every BVH answer checked against the KD walk
   float* api_t2 = nullptr;  // t2 scratch of the API path
   size_t api_t2_cap = 0;
 };
@@ -728,6 +742,9 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     // the hard rays are a few in 10^4: a small grid drains any count
     hipLaunchKernelGGL(count ? k_fast_hard<true> : k_fast_hard<false>, dim3(std::max(1, std::min(256, blocks))),
                        dim3(kTraceBlock), lds, stream, c->ds, c->fs, Q, ctr, ts.t2, hard, ts.hard_n);
+    if (c->verify)
+      hipLaunchKernelGGL(k_fast_verify, dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), lds,
+                         stream, c->ds, c->fs, Q, ctr);
     tm.mark(WR_K_TRACE);
     if (c->trace_log) {
       (void)hipEventRecord(f1, stream);
@@ -832,6 +849,8 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
     sum.bvh_tests += h.bvh_tests;
     sum.kd_replay += h.kd_replay;
     sum.fallback += h.fallback;
+    sum.verify_rays += h.verify_rays;
+    sum.verify_bad += h.verify_bad;
     for (int k = 0; k < 8; ++k) sum.stamps[k] += h.stamps[k];
   }
   st->closest_rays += static_cast<int64_t>(sum.closest);
@@ -847,6 +866,8 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
   st->bvh_tests += static_cast<int64_t>(sum.bvh_tests);
   st->kd_replay_steps += static_cast<int64_t>(sum.kd_replay);
   st->fallback_rays += static_cast<int64_t>(sum.fallback);
+  st->verify_rays += static_cast<int64_t>(sum.verify_rays);
+  st->verify_mismatches += static_cast<int64_t>(sum.verify_bad);
   if (c->trace_log && c->fast_on) {
     unsigned long long mx[3] = {0, 0, 0};
     for (int i = 0; i < n; ++i) {
@@ -1294,6 +1315,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       c->fast_blocks = c->cus * per_cu;
       if (const char* e = std::getenv("WR_TRACE_BVH")) c->fast_on = std::atoi(e) != 0;
       if (const char* e = std::getenv("WR_BVH_DIAG")) fs.diag = std::atoi(e);
+      if (const char* e = std::getenv("WR_BVH_VERIFY")) c->verify = std::atoi(e) != 0;
       if (c->trace_log)
         std::fprintf(stderr, "[wr bvh] nodes %zu tris %zu depth %d lds %zu B/wave, %d waves/CU -> grid %d; kd grid %d\n",
                      fbn, ftr, fs.depth, fast_lds_bytes(fs.depth), per_cu, c->fast_blocks, c->trace_blocks);

@@ -67,7 +67,8 @@ class WrStats(C.Structure):
                 ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8), ("trace_wall_ms", C.c_double),
                 ("vm_queries", C.c_int64), ("vm_found", C.c_int64), ("vm_merged", C.c_int64),
                 ("prim_tests", C.c_int64), ("bvh_nodes", C.c_int64), ("bvh_tests", C.c_int64),
-                ("kd_replay_steps", C.c_int64), ("fallback_rays", C.c_int64)]
+                ("kd_replay_steps", C.c_int64), ("fallback_rays", C.c_int64), ("verify_rays", C.c_int64),
+                ("verify_mismatches", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
