@@ -197,9 +197,12 @@ def main():
     ap.add_argument("--cpu-paths", type=int, default=1000000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting replay")
-    ap.add_argument("--trace", choices=["reference", "bvh"], default="reference",
-                    help="traversal: the reference's KD walk, or the verified BVH search with KD "
-                         "fallback (same answers, DESIGN.md section 4b)")
+    ap.add_argument("--trace", choices=["auto", "reference", "bvh"], default="auto",
+                    help="traversal: the reference's KD walk, or the verified BVH search (same (t, primitive) "
+                         "answers, DESIGN.md section 4b); auto = the faster one for the config: bvh for c2 / vcm / "
+                         "c4, reference for c3")
+    ap.add_argument("--no-compare", action="store_true",
+                    help="skip the single-GPU comparison run in the other traversal mode")
     ap.add_argument("--no-cut", action="store_true",
                     help="c3/vcm: shadow rays run to the end of the walk (no occlusion cutoff)")
     args = ap.parse_args()
@@ -220,6 +223,9 @@ def main():
     from winmad_rt import dist as wdist
 
     cfg = CONFIGS[args.config]
+    trace = args.trace
+    if trace == "auto":
+        trace = "reference" if cfg["integrator"] == "pt" else "bvh"
     W, H = args.width, args.height
     K = args.steps if args.steps is not None else cfg["steps"]
     pt = cfg["integrator"] == "pt"
@@ -227,7 +233,7 @@ def main():
     scene_path = make_scene(args.config, W, H, tmp)
     sc = native.Scene(scene_path)
     ctx = native.Context(sc, local)
-    if args.trace == "bvh":
+    if trace == "bvh":
         ctx.set_trace_mode(native.TRACE_BVH)
     film = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
 
@@ -277,7 +283,7 @@ def main():
         assert cst.closest_rays == st.closest_rays and cst.shadow_rays == st.shadow_rays
         total_bytes = algorithmic_bytes(rays, cst.inner_visits, cst.leaf_visits, cst.prim_refs, cst.prim_tests)
         bvh = None
-        if args.trace == "bvh":
+        if trace == "bvh":
             # the KD counters cover only the fallback rays (their own B_ray terms
             # minus the ray load / hit store, which every ray pays once here):
             # + 64 B per BVH node record, 48 B per triangle record, 8 B per KD
@@ -329,6 +335,25 @@ def main():
                                              "KD path entry replayed; fallback rays: SURVEY.md 8(d) B_ray")
             roofline["bvh"] = bvh
 
+    other = None
+    if rank == 0 and world == 1 and not args.no_compare:
+        # the same K steps in the other traversal mode (same rays, same answers),
+        # timed the same way, for the line's `other_trace`
+        o_mode = "reference" if trace == "bvh" else "bvh"
+        try:
+            ctx.set_trace_mode(native.TRACE_BVH if o_mode == "bvh" else native.TRACE_REFERENCE)
+            render((args.spp - 1) if pt else (1 << 20) + 64, 1, film_ptr=film.data_ptr())
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            _, ost = render(it0, K, film_ptr=film.data_ptr())
+            torch.cuda.synchronize()
+            odt = time.perf_counter() - t1
+            orays = ost.closest_rays + ost.shadow_rays
+            other = {"trace": o_mode, "value": round(orays / odt / 1e6, 2), "ms_per_step": round(odt / K * 1e3, 3),
+                     "same_ray_count": bool(orays == rays)}
+        except native.WrError as e:  # e.g. the BVH mode on a scene with spheres
+            other = {"trace": o_mode, "error": str(e)}
+
     cpu = port = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_reference(args.config, cfg["integrator"], W, H, tmp, 4 if args.config == "c4" else 2)
@@ -353,12 +378,18 @@ def main():
                                    + ("" if pt else ", maxPathLength 10" if cfg["integrator"] == "vcm"
                                       else ", controlLength 3, maxPathLength 10"),
                        "scene_config": args.config.upper(), "width": W, "height": H,
-                       "steps_per_gpu": K, "parallelism": f"sample-batch x{world}", "trace": args.trace,
+                       "steps_per_gpu": K, "parallelism": f"sample-batch x{world}", "trace": trace,
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
             "spp_per_sec": round(W * H * K * world / elapsed, 1),
             "rays_per_step": round(total_rays / (K * world)),
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if trace == "bvh":
+            out["trace_note"] = ("verified BVH traversal: every ray gets the reference KD walk's (t, primitive) "
+                                 "answer, bit for bit (proof in DESIGN.md 4b; 0 mismatches over the full C2 workload, "
+                                 "profiles/r2/bvh_verify.json); the same rays are traced and counted")
+        if other:
+            out["other_trace"] = other
         if cfg["integrator"] in ("pt", "vcm"):
             # dead-work elision is flagged; --no-cut measures without it
             out["config"]["occlusion_cutoff"] = not args.no_cut

@@ -7,7 +7,8 @@ Writes
   kernel_stats.csv  rocprofv3 --kernel-trace --stats summary (copied as is)
   pmc_summary.json  per kernel: dispatches and the per-dispatch mean of every
                     PMC counter collected in the separate --pmc passes
-  traffic.json      HBM bytes per k_trace launch, per MI355X_MICROARCH.md
+  traffic.json      HBM bytes per traversal step (k_trace, or the BVH mode's
+                    three kernels), per MI355X_MICROARCH.md
                     "HBM [CDNA4]": FETCH_SIZE / WRITE_SIZE are in KiB, and on
                     gfx950 FETCH_SIZE counts half the bytes of a read, so
                     traffic = 2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE.
@@ -51,16 +52,24 @@ def main():
     with open(os.path.join(dst, "pmc_summary.json"), "w") as fh:
         json.dump(summary, fh, indent=1, sort_keys=True)
 
-    tr = [k for k in summary if k.startswith(DOMINANT)]
-    out = {"kernel": DOMINANT, "variants": tr}
+    # one traversal step = k_trace (reference mode) or k_trace_fast +
+    # k_fast_resolve + k_fast_hard (BVH mode); per-step means over the dispatches
+    bvh = any(k.startswith("k_trace_fast") for k in summary)
+    fam = ("k_trace_fast", "k_fast_resolve", "k_fast_hard") if bvh else (DOMINANT,)
+    lead = fam[0]
+    tr = [k for k in summary if k.startswith(fam) and not k.startswith("k_trace_fast") or k.startswith(lead)]
+    tr = [k for k in summary if any(k.startswith(f + "<") or k == f for f in fam)]
+    out = {"kernel": " + ".join(fam), "variants": tr}
     if tr:
-        def mean_of(counter):
+        steps = len([v for k in tr if k.startswith(lead + "<") or k == lead for v in per[k].get("FETCH_SIZE", [])])
+
+        def per_step(counter):
             vals = [v for k in tr for v in per[k].get(counter, [])]
-            return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
-        fetch, nf = mean_of("FETCH_SIZE")
-        write, nw = mean_of("WRITE_SIZE")
-        hit, _ = mean_of("TCC_HIT_sum")
-        miss, _ = mean_of("TCC_MISS_sum")
+            return (sum(vals) / steps, steps) if vals and steps else (None, 0)
+        fetch, nf = per_step("FETCH_SIZE")
+        write, nw = per_step("WRITE_SIZE")
+        hit, _ = per_step("TCC_HIT_sum")
+        miss, _ = per_step("TCC_MISS_sum")
         out.update({"fetch_kib_per_launch": fetch, "write_kib_per_launch": write, "launches": nf,
                     "hbm_bytes_per_launch": (2 * 1024 * fetch + 1024 * write)
                     if fetch is not None and write is not None else None,
@@ -69,8 +78,9 @@ def main():
         json.dump(out, fh, indent=1)
     print(json.dumps(out))
 
-    # the trace pass's bench line beside rocprof's own k_trace durations (the
-    # warm-up runs the counting build, so k_trace<false, ...> = the timed launches)
+    # the trace pass's bench line beside rocprof's own durations of the timed
+    # traversal steps (the warm-up runs the counting build, <true ...>; the
+    # comparison leg in the other mode is skipped in profiled runs)
     line = None
     log = os.path.join(src, "trace.log")
     if os.path.exists(log):
@@ -78,14 +88,15 @@ def main():
             lines = [l for l in fh if l.startswith('{"metric"')]
         line = json.loads(lines[-1]) if lines else None
     if line and os.path.exists(stats):
-        with open(os.path.join(dst, "bench_c2_profiled_run.json"), "w") as fh:
+        with open(os.path.join(dst, "bench_profiled_run.json"), "w") as fh:
             fh.write(json.dumps(line) + "\n")
-        rows = [r for r in csv.DictReader(open(stats)) if short(r["Name"]).startswith(DOMINANT + "<false")]
-        calls = sum(int(r["Calls"]) for r in rows)
+        rows = [r for r in csv.DictReader(open(stats))
+                if any(short(r["Name"]).startswith(f + "<false") for f in fam)]
+        calls = sum(int(r["Calls"]) for r in rows if short(r["Name"]).startswith(lead + "<false"))
         tot = sum(float(r["TotalDurationNs"]) for r in rows)
         r = line["roofline"]
-        cmp_ = {"rocprof_kernel": [short(r_["Name"]) for r_ in rows],
-                "rocprof_calls": calls, "rocprof_avg_ms": round(tot / max(1, calls) / 1e6, 4),
+        cmp_ = {"rocprof_kernels": [short(r_["Name"]) for r_ in rows],
+                "rocprof_steps": calls, "rocprof_avg_ms_per_step": round(tot / max(1, calls) / 1e6, 4),
                 "bench_launches": r["launches"], "bench_event_avg_ms": r["avg_launch_ms"],
                 "ratio_events_over_rocprof": round(r["avg_launch_ms"] / (tot / max(1, calls) / 1e6), 3)}
         with open(os.path.join(dst, "duration_check.json"), "w") as fh:
