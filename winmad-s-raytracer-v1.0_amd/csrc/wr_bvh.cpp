@@ -190,6 +190,7 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
   };
   std::vector<Item> st;
   out.node_path.assign(s.nodes.size(), -1);
+  out.node_cell.assign(8 * s.nodes.size(), 0.f);
   st.push_back({0, 0, 0u, 0u, {s.root_l.x, s.root_l.y, s.root_l.z}, {s.root_r.x, s.root_r.y, s.root_r.z}});
   while (!st.empty()) {
     const Item it = st.back();
@@ -200,6 +201,10 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
       cur[2 * (it.depth - 1) + 1] = it.e1;
     }
     const wr::KdNode& k = s.nodes[static_cast<size_t>(it.node)];
+    for (int a = 0; a < 3; ++a) {  // the node's cell (targeted walks prune by it)
+      out.node_cell[8 * static_cast<size_t>(it.node) + a] = it.lo[a];
+      out.node_cell[8 * static_cast<size_t>(it.node) + 4 + a] = it.hi[a];
+    }
     if (k.axis >= 0) {
       uint32_t bits;
       std::memcpy(&bits, &k.split, 4);

@@ -90,6 +90,7 @@ struct FastHost {
   std::vector<TriRec> tris;
   std::vector<int32_t> prim_leaf_off, prim_leaf, prim_leaf_pos;
   std::vector<int32_t> node_path;  // KD leaf node -> its path record offset (-1: inner node)
+  std::vector<float> node_cell;    // per KD node: cell lo.xyz, 0, hi.xyz, 0
   std::vector<uint32_t> path;  // pairs
   int depth = 0;               // deepest node chain (stack bound)
   int leaves = 0;

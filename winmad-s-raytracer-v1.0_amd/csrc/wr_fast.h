@@ -43,6 +43,7 @@ struct FastScene {
   const int* prim_leaf_pos;
   const uint2* path;
   const int* node_path;  // KD leaf node -> path record offset
+  const float4* node_cell;  // 2 per KD node: cell lo, hi
   V3 lo, hi;  // union of the (grown) triangle boxes
   int depth;  // stack entries (BVH search and KD fallback walk)
   int diag;   // WR_BVH_DIAG: 1 = skip the KD walks (wrong answers, measurement only); 2 = KD walk for every tie
@@ -53,6 +54,7 @@ struct FastCounters {  // algorithmic work (count_work)
   uint32_t kinner, kleaves, krefs;           // KD walks of the fallback rays
   uint32_t max_nodes, max_tests, long_rays;  // per-ray tail: max visits, rays > 256 nodes
   uint32_t fb_tie;                            // near-ties resolved by visit order
+  uint32_t why[4];                            // KD walks: many-leaf candidate, no visited hit, crowd, band
 };
 
 // Per wave: the stack columns, 8 bytes per entry and lane (BVH: link + entry t;
@@ -259,7 +261,7 @@ __device__ __forceinline__ float clamp_inv(float x) { return fminf(fmaxf(1.f / x
 // smallest hit so far (and cap), with the main search's box margins.  Returns
 // the number of hits <= cap found (> kTie: more exist beyond ct[kTie - 1]).
 constexpr int kTie = 8;
-constexpr int kTieLeaves = 16;  // resolve_tie: at most this many KD leaves per candidate
+constexpr int kTieLeaves = 16;  // resolve_tie: replay up to this many KD leaves per candidate, else a pruned walk
 __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float rtmin, float rtmax, float cap,
                                            int* stk_link, float* stk_t, float (&ct)[kTie], int (&cp)[kTie]) {
   rtmax = fminf(rtmax, cap);
@@ -372,6 +374,90 @@ __device__ __noinline__ void first_leaf(const FastScene& F, int p, V3 o, V3 d, V
   }
 }
 
+// The first visited leaf of several primitives at once, by the reference's own
+// walk (KDtreeAccel.cpp:309-388: root clip, near / far rule, the :323 stop)
+// restricted to subtrees whose cell meets one of their boxes: a primitive is
+// put in a child only when its box reaches into it by more than EPS
+// (KDtreeAccel.cpp:138-157), so a subtree whose cell misses every box holds
+// none of their leaves.  Leaves are numbered in visit order; at a leaf each
+// unresolved primitive is looked up in its (ascending) leaf list.  want: mask
+// of the candidates to find; vis / pos get (visit number, position in list).
+__device__ __noinline__ void kd_first_leaves(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmax,
+                                             const int* cp, unsigned want, int* stk_node, float* stk_tmin,
+                                             int* vis, int* pos, uint32_t& steps) {
+  float tmin, tmax;
+  if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) return;
+  const float root_tmax = tmax;
+  const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+  uint32_t node = 0;
+  int sp = 0, visit = 0;
+  for (;;) {
+    const uint4 w = S.nrec[node];
+    const float4 clo = F.node_cell[2 * node], chi = F.node_cell[2 * node + 1];
+    ++steps;
+    bool meets = false;
+    for (int c = 0; c < kTie; ++c) {
+      if (!((want >> c) & 1u)) continue;
+      const float4 b0 = S.prim_sbox0[cp[c]];
+      const float2 b1 = S.prim_sbox1[cp[c]];
+      meets |= b0.x <= chi.x && b0.y <= chi.y && b0.z <= chi.z && b0.w >= clo.x && b1.x >= clo.y && b1.y >= clo.z;
+    }
+    bool pop = !meets;
+    if (meets) {
+      if ((w.y & 3u) != 3u) {  // inner (:325-358)
+        const uint32_t axis = w.y & 3u;
+        const float split = __uint_as_float(w.x);
+        const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+        const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+        const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
+        const float t = (split - oa) * ia;
+        const bool below = (oa < split) | ((oa == split) & (da <= 0));
+        const uint32_t left = node + 1, right = w.y >> 2;
+        const uint32_t nearc = below ? left : right, farc = below ? right : left;
+        if ((t > tmax) | (t <= 0)) {
+          node = nearc;
+        } else if (t < tmin) {
+          node = farc;
+        } else {
+          stk_node[sp * 64] = static_cast<int>(farc);
+          stk_tmin[sp * 64] = t;
+          ++sp;
+          node = nearc;
+          tmax = t;
+        }
+        continue;
+      }
+      // leaf: which wanted primitives does it hold?
+      ++visit;
+      const int off = F.node_path[node];
+      for (int c = 0; c < kTie; ++c) {
+        if (!((want >> c) & 1u)) continue;
+        int a = F.prim_leaf_off[cp[c]], b = F.prim_leaf_off[cp[c] + 1];
+        while (a < b) {
+          const int mid = (a + b) >> 1;
+          if (F.prim_leaf[mid] < off) a = mid + 1;
+          else b = mid;
+        }
+        if (a < F.prim_leaf_off[cp[c] + 1] && F.prim_leaf[a] == off) {
+          vis[c] = visit;
+          pos[c] = F.prim_leaf_pos[a];
+          want &= ~(1u << c);
+        }
+      }
+      if (!want) return;
+      pop = true;
+    }
+    if (pop) {
+      if (sp == 0) return;  // :375-383
+      --sp;
+      node = static_cast<uint32_t>(stk_node[sp * 64]);
+      tmin = stk_tmin[sp * 64];
+      tmax = sp > 0 ? stk_tmin[(sp - 1) * 64] : root_tmax;
+      if (rtmax < tmin) return;  // :323
+    }
+  }
+}
+
 // Resolution by visit order.  The reference's answer is first-found-wins
 // (cmp(t - best) < 0) over the hits it visits, in visit order.  Let m be the
 // smallest hit it visits.  Its winner lies within EPS of m (once m is reached
@@ -402,31 +488,64 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
     const float cap = pass == 0 ? t1 + 3.f * WR_EPS : WR_INF;
     n = bvh_collect(F, o, d, rtmin, rtmax, cap, stk_link, stk_t, ct, cp);
     m = WR_INF;
+    const int ncand = min(n, kTie);
+    // per candidate: its first visited leaf as a visit-order key (~0: none).
+    // Primitives in many leaves (walls, floors): one walk of the KD tree
+    // pruned to the candidates' boxes finds them all (keys = visit numbers);
+    // otherwise each candidate's leaves are replayed (keys = far-child bits)
+    bool big = false;
+    for (int c = 0; c < ncand; ++c) big |= F.prim_leaf_off[cp[c] + 1] - F.prim_leaf_off[cp[c]] > kTieLeaves;
+    if (big) {
+      int vis[kTie], ps[kTie];
+      for (int c = 0; c < kTie; ++c) {
+        vis[c] = -1;
+        ps[c] = 0;
+      }
+      kd_first_leaves(S, F, o, d, rtmax, cp, (1u << ncand) - 1u, stk_link, stk_t, vis, ps, steps);
 #pragma unroll
-    for (int c = 0; c < kTie; ++c) {  // per candidate: its first visited leaf (~0: none)
-      key[c] = ~0ull;
-      pos[c] = 0;
-      if (c < min(n, kTie)) {
-        // a primitive in many leaves (walls): the KD walk is cheaper than
-        // replaying every one of them
-        if (F.prim_leaf_off[cp[c] + 1] - F.prim_leaf_off[cp[c]] > kTieLeaves) return false;
-        first_leaf(F, cp[c], o, d, inv, tmin0, tmax0, rtmax, key[c], pos[c], steps);
-        if (key[c] != ~0ull && m == WR_INF) m = ct[c];  // sorted by t: the first visited one
+      for (int c = 0; c < kTie; ++c) {
+        key[c] = (c < ncand && vis[c] >= 0) ? static_cast<unsigned long long>(vis[c]) : ~0ull;
+        pos[c] = ps[c];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < kTie; ++c) {
+        key[c] = ~0ull;
+        pos[c] = 0;
+        if (c < ncand) first_leaf(F, cp[c], o, d, inv, tmin0, tmax0, rtmax, key[c], pos[c], steps);
       }
     }
+#pragma unroll
+    for (int c = 0; c < kTie; ++c)
+      if (c < ncand && key[c] != ~0ull && m == WR_INF) m = ct[c];  // sorted by t: the first visited one
     if (pass == 0 && m == t1) break;  // the window t1 + 3 EPS is complete when n <= kTie
   }
   dbg = n;
   const int nc = min(n, kTie);
+  if (m == WR_INF && n <= kTie) {  // every hit is known and none is visited: the reference misses
+    t_out = WR_INF;
+    p_out = -1;
+    dbg |= 1 << 8;
+    return true;
+  }
   // m < 4096: fl(m + 3 EPS) is within EPS / 4 of m + 3 EPS
-  if (!(m < 4096.f)) return false;
+  if (!(m < 4096.f)) {
+    dbg |= 3 << 16;
+    return false;
+  }
   const float lim = m + 3.f * WR_EPS;
-  if (n > kTie && !(ct[kTie - 1] > lim)) return false;  // hits up to m + 3 EPS may be missing
+  if (n > kTie && !(ct[kTie - 1] > lim)) {  // hits up to m + 3 EPS may be missing
+    dbg |= 4 << 16;
+    return false;
+  }
   bool band = false;
 #pragma unroll
   for (int c = 0; c < kTie; ++c)
     if (c < nc && key[c] != ~0ull && ct[c] <= lim && ct[c] - m > 1.5f * WR_EPS) band = true;  // exact difference
-  if (band) return false;
+  if (band) {
+    dbg |= 5 << 16;
+    return false;
+  }
   // first-found-wins over the visited candidates up to m + 1.5 EPS, in visit
   // order: each candidate's rank, then the rule rank by rank (compile-time
   // indices only: the lists stay in registers)
@@ -768,6 +887,8 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
       if (COUNT) {
         ctr.replay += steps;
         ctr.fb_tie += done ? 1u : 0u;
+        const int why = dbg >> 16;
+        if (!done && why >= 2 && why <= 5) ++ctr.why[why - 2];
       }
       if (done) {
         outt[r] = tb;

@@ -205,6 +205,7 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
   atomicMax(&ctr->stamps[6], static_cast<unsigned long long>(fc.max_tests));
   atomicAdd(&ctr->stamps[7], static_cast<unsigned long long>(fc.long_rays));
   atomicAdd(&ctr->stamps[4], static_cast<unsigned long long>(fc.fb_tie));
+  for (int k = 0; k < 4; ++k) atomicAdd(&ctr->stamps[k], static_cast<unsigned long long>(fc.why[k]));
 }
 template <bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32
@@ -877,12 +878,15 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
       mx[1] = std::max(mx[1], h.stamps[6]);
       mx[2] += h.stamps[7];
     }
-    unsigned long long ties = 0;
+    unsigned long long ties = 0, why[4] = {0, 0, 0, 0};
     for (int i = 0; i < n; ++i) {
       DevCounters h;
       HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
       ties += h.stamps[4];
+      for (int k = 0; k < 4; ++k) why[k] += h.stamps[k];
     }
+    std::fprintf(stderr, "[wr bvh walks] many-leaf %llu, no visited hit %llu, crowd %llu, band %llu\n", why[0], why[1],
+                 why[2], why[3]);
     std::fprintf(stderr, "[wr bvh tail] max nodes/ray %llu, max tests/ray %llu, rays > 256 nodes %llu, ties resolved by visit order %llu\n",
                  mx[0], mx[1], mx[2], ties);
   }
@@ -1261,7 +1265,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       const size_t fnp = fh.node_path.size();
       const size_t fbytes = measure([&](Arena& a) {
         a.take<wrf::BNode>(fbn); a.take<wrf::TriRec>(ftr); a.take<int>(fpo); a.take<int>(fpl); a.take<int>(fpl);
-        a.take<uint2>(fpa); a.take<int>(fnp);
+        a.take<uint2>(fpa); a.take<int>(fnp); a.take<float4>(2 * fnp);
       });
       if (int rc = c->fast_mem.reserve(fbytes)) {
         wr_destroy(c);
@@ -1275,6 +1279,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       int* dpp = F.take<int>(fpl);
       uint2* dpa = F.take<uint2>(fpa);
       int* dnp = F.take<int>(fnp);
+      float4* dnc = F.take<float4>(2 * fnp);
       hipError_t fe = hipSuccess;
       for (hipError_t x : {hipMemcpy(dno, fh.nodes.data(), fbn * sizeof(wrf::BNode), hipMemcpyHostToDevice),
                            hipMemcpy(dtr, fh.tris.data(), ftr * sizeof(wrf::TriRec), hipMemcpyHostToDevice),
@@ -1283,7 +1288,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                            hipMemcpy(dpp, fh.prim_leaf_pos.data(), fh.prim_leaf_pos.size() * sizeof(int),
                                      hipMemcpyHostToDevice),
                            hipMemcpy(dpa, fh.path.data(), fpa * sizeof(uint2), hipMemcpyHostToDevice),
-                           hipMemcpy(dnp, fh.node_path.data(), fnp * sizeof(int), hipMemcpyHostToDevice)})
+                           hipMemcpy(dnp, fh.node_path.data(), fnp * sizeof(int), hipMemcpyHostToDevice),
+                           hipMemcpy(dnc, fh.node_cell.data(), 8 * fnp * sizeof(float), hipMemcpyHostToDevice)})
         if (x != hipSuccess) fe = x;
       if (fe != hipSuccess) {
         wr_destroy(c);
@@ -1297,6 +1303,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       fs.prim_leaf_pos = dpp;
       fs.path = dpa;
       fs.node_path = dnp;
+      fs.node_cell = dnc;
       float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
       for (int k = 0; k < 3; ++k) {
         lo[k] = std::min(fh.nodes[0].b[k], fh.nodes[0].b[6 + k]);
