@@ -46,7 +46,7 @@ struct FastScene {
   const float4* node_cell;  // 2 per KD node: cell lo, hi
   V3 lo, hi;  // union of the (grown) triangle boxes
   int depth;  // stack entries (BVH search and KD fallback walk)
-  int diag;   // WR_BVH_DIAG: 1 = skip the KD walks (wrong answers, measurement only); 2 = KD walk for every tie
+  int diag;   // WR_BVH_DIAG (measurement only): 1 = skip the KD walks, 8 = skip the replays (wrong answers); 2 = KD walk for every tie
 };
 
 struct FastCounters {  // algorithmic work (count_work)
@@ -60,6 +60,8 @@ struct FastCounters {  // algorithmic work (count_work)
 // Per wave: the stack columns, 8 bytes per entry and lane (BVH: link + entry t;
 // KD walk: node + tmin).
 __host__ __device__ constexpr size_t fast_lds_bytes(int depth) { return size_t(depth) * 64 * 8; }
+
+__device__ __forceinline__ float clamp_inv(float x) { return fminf(fmaxf(1.f / x, -1e30f), 1e30f); }
 
 // KDtreeAccel::traverse reaches the leaf whose root path is rec[1..n]: the
 // near / far rule (:331-357) and the `ray.tmax < tmin` stop (:323), evaluated
@@ -139,6 +141,38 @@ __device__ __forceinline__ int kd_locate(const DevScene& S, const FastScene& F, 
   }
 }
 
+// Does the reference's walk reach a leaf whose cell holds a point of the ray,
+// o + d t with 0 < t <= rtmax, with room to spare -- without replaying its
+// path?  The walk hands each node's float interval [a, b] down to the child
+// that contains the ray's points there.  With the point at distance > delta
+// from every face of the cell (delta_axis = 1e-6 x (|faces| + 2 |o| + |t d|)),
+// each split's t = (split - o) * (1 / d) lies on the correct side of t despite
+// its rounding (< 3 ulp relative: (split - o) and 1 / d rounded, then the
+// product), and so do the root clip's slab t's; so every decision on the
+// leaf's path (:331-357) keeps t inside the interval it passes on, and the
+// leaf is visited.  (The exact point o + d t is within 2 ulp of the computed
+// p.)
+__device__ __forceinline__ bool cell_holds_with_margin(uint4 h0, uint4 h1, V3 o, V3 d, float t, V3 p) {
+  const float lx = __uint_as_float(h0.z), ly = __uint_as_float(h0.w), lz = __uint_as_float(h1.x);
+  const float hx = __uint_as_float(h1.y), hy = __uint_as_float(h1.z), hz = __uint_as_float(h1.w);
+  const float mx = 1e-6f * (fabsf(lx) + fabsf(hx) + 2.f * fabsf(o.x) + fabsf(t * d.x));
+  const float my = 1e-6f * (fabsf(ly) + fabsf(hy) + 2.f * fabsf(o.y) + fabsf(t * d.y));
+  const float mz = 1e-6f * (fabsf(lz) + fabsf(hz) + 2.f * fabsf(o.z) + fabsf(t * d.z));
+  return p.x - lx > mx && hx - p.x > mx && p.y - ly > my && hy - p.y > my && p.z - lz > mz && hz - p.z > mz;
+}
+
+// The witness: the middle of the ray's stretch inside the cell (in (0, rtmax]).
+__device__ __forceinline__ bool cell_crossed_with_margin(uint4 h0, uint4 h1, V3 o, V3 d, V3 binv, float rtmax) {
+  const float x0 = (__uint_as_float(h0.z) - o.x) * binv.x, x1 = (__uint_as_float(h1.y) - o.x) * binv.x;
+  const float y0 = (__uint_as_float(h0.w) - o.y) * binv.y, y1 = (__uint_as_float(h1.z) - o.y) * binv.y;
+  const float z0 = (__uint_as_float(h1.x) - o.z) * binv.z, z1 = (__uint_as_float(h1.w) - o.z) * binv.z;
+  const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.f));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), rtmax));
+  if (!(tn < tf)) return false;
+  const float tw = 0.5f * (tn + tf);
+  return tw > 0.f && cell_holds_with_margin(h0, h1, o, d, tw, o + d * tw);
+}
+
 // Is the primitive whose KD leaves are prim_leaf[lb, lb + ln) tested by the
 // reference's traversal of this ray?
 __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F, int lb, int ln, V3 o, V3 d,
@@ -146,20 +180,27 @@ __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F,
   float tmin, tmax;
   if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) return false;  // :312-313, :323
   const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+  const V3 binv = v3(clamp_inv(d.x), clamp_inv(d.y), clamp_inv(d.z));
   const V3 p = o + d * t_hit;
   unsigned long long key;
   if (ln > 4) {
-    // a big primitive (walls: hundreds of leaves): the leaf holding the hit
-    // point, found by descent, then by binary search in the (ascending) list
-    const int want = kd_locate(S, F, p);
+    // a big primitive (walls: hundreds of leaves): the leaf holding a point
+    // just before the hit (a hit on a wall lies on a split plane), found by
+    // descent, then by binary search in the (ascending) list
+    const int want = kd_locate(S, F, o + d * (t_hit * 0.99999f - 1e-4f));
     int a = lb, b = lb + ln;
     while (a < b) {
       const int mid = (a + b) >> 1;
       if (F.prim_leaf[mid] < want) a = mid + 1;
       else b = mid;
     }
-    if (a < lb + ln && F.prim_leaf[a] == want && kd_reaches(F.path + want, o, d, inv, tmin, tmax, rtmax, steps, key))
-      return true;
+    if (a < lb + ln && F.prim_leaf[a] == want) {
+      const uint2* rec = F.path + want;
+      const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
+      const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
+      if (cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return true;
+      if (kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return true;
+    }
   }
   // the leaves whose cell holds the hit point first (usually the one reached),
   // then the others
@@ -170,6 +211,7 @@ __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F,
       const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
       const bool in = p.x >= __uint_as_float(h0.z) && p.y >= __uint_as_float(h0.w) && p.z >= __uint_as_float(h1.x) &&
                       p.x <= __uint_as_float(h1.y) && p.y <= __uint_as_float(h1.z) && p.z <= __uint_as_float(h1.w);
+      if (pass == 0 && cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return true;
       if (in == (pass == 0) && kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return true;
     }
   }
@@ -253,8 +295,6 @@ __device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtm
     if (rtmax < tmin) return;  // :323
   }
 }
-
-__device__ __forceinline__ float clamp_inv(float x) { return fminf(fmaxf(1.f / x, -1e30f), 1e30f); }
 
 // The kTie smallest triangle hits (Triangle::hit) with t <= cap of the ray over
 // the BVH, as (t, prim) sorted by t: a search whose bound is the kTie-th
@@ -838,7 +878,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
           const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
           uint32_t steps = 0;
           const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
-          need = !kd_member(S, F, lb, ln, o, d, tmx ? tmx[r] : WR_INF, t1, steps);
+          need = (F.diag & 8) ? false : !kd_member(S, F, lb, ln, o, d, tmx ? tmx[r] : WR_INF, t1, steps);
           if (COUNT) ctr.replay += steps;
         }
       }
