@@ -45,7 +45,8 @@ struct FastScene {
   const int* node_path;  // KD leaf node -> path record offset
   const float4* node_cell;  // 2 per KD node: cell lo, hi
   V3 lo, hi;  // union of the (grown) triangle boxes
-  int depth;  // stack entries (BVH search and KD fallback walk)
+  int depth;   // stack entries of the KD walks and tie resolution (k_fast_hard, k_fast_verify)
+  int sdepth;  // stack entries of the BVH search (k_trace_fast): the BVH's depth + 1
   int diag;   // WR_BVH_DIAG (measurement only): 1 = skip the KD walks, 8 = skip the replays (wrong answers); 2 = KD walk for every tie
 };
 
@@ -55,11 +56,24 @@ struct FastCounters {  // algorithmic work (count_work)
   uint32_t max_nodes, max_tests, long_rays;  // per-ray tail: max visits, rays > 256 nodes
   uint32_t fb_tie;                            // near-ties resolved by visit order
   uint32_t why[4];                            // KD walks: many-leaf candidate, no visited hit, crowd, band
+  // latency tail (count_work, 100 MHz ticks): k_fast_resolve membership,
+  // k_fast_hard tie resolution and KD walk -- max and sum per ray -- and the
+  // rays whose membership test scanned a many-leaf primitive's whole list
+  uint32_t mem_max, mem_sum, tie_max, tie_sum, walk_max, walk_sum, scans;
 };
 
 // Per wave: the stack columns, 8 bytes per entry and lane (BVH: link + entry t;
 // KD walk: node + tmin).
 __host__ __device__ constexpr size_t fast_lds_bytes(int depth) { return size_t(depth) * 64 * 8; }
+// The search's stack: link (4 bytes) + entry t rounded down to bfloat16 (2
+// bytes).  A rounded-down entry t only lets more subtrees through the pop test
+// (t_entry <= bound), never fewer, so the search still reports every hit it
+// must; 6 instead of 8 bytes per entry raise the waves per CU the LDS allows.
+__host__ __device__ constexpr size_t search_lds_bytes(int depth) { return size_t(depth) * 64 * 6; }
+__device__ __forceinline__ uint16_t t_down16(float t) {
+  return static_cast<uint16_t>(__float_as_uint(fmaxf(t, 0.f)) >> 16);  // truncation: down for t >= 0
+}
+__device__ __forceinline__ float t_up32(uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); }
 
 __device__ __forceinline__ float clamp_inv(float x) { return fminf(fmaxf(1.f / x, -1e30f), 1e30f); }
 
@@ -657,14 +671,16 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
                                            float* t2buf, uint32_t* lds, FastCounters& ctr) {
   const int lane = __lane_id();
   int* stk_link = reinterpret_cast<int*>(lds) + lane;
-  float* stk_t = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
+  uint16_t* stk_t = reinterpret_cast<uint16_t*>(reinterpret_cast<int*>(lds) + F.sdepth * 64) + lane;
   const QueueIndex QI(Q);
   const int n = QI.n;
   int r = -1, qi = 0, lidx = 0;
   bool pool = true;
   int pb = 0, pe = 0;
   V3 o = v3(0.f, 0.f, 0.f), d = o, binv = o;
-  float rtmin = 0.f, rtmax = WR_INF, t1 = WR_INF, t2 = WR_INF, tcap = 0.f, dlen = 1.f;
+  V3 cl = o, ch = o;  // slab offsets -(o + g) binv, -(o - g) binv for the current margin g
+  float rtmin = 0.f, rtmax = WR_INF, t1 = WR_INF, t2 = WR_INF, tcap = 0.f, dlen = 1.f, olen = 0.f;
+  float lo_t = 0.f, hi_t = 0.f;
   int p1 = -1, sp = 0;
   uint32_t rn = 0, rt = 0;  // COUNT: this ray's node visits / tests
   int cur = 0;  // >= 0 inner node to visit; < 0 leaf link to test; kDone when finished
@@ -690,14 +706,24 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   };
   // the search window: hits up to t1 + 2 EPS, and rtmax
   auto bound = [&]() { return fminf(rtmax, t1 + 2.f * WR_EPS); };
+  // the ray's box margin g (space) and the node test's constants for it.  A
+  // box face x is tested as fma(x, binv, -(o -+ g) binv): the product
+  // (o -+ g) binv is rounded once, an error of < 1 ulp of |o| |binv| in t, i.e.
+  // < 1.2e-7 |o| in space, covered by the 1e-6 |o| term of g
+  auto margins = [&]() {
+    const float tc = fminf(bound(), tcap);
+    const float g = wrf::kRayGrow * (tc * dlen + 1.f) + 1e-6f * olen;
+    const float gt = g / dlen;
+    lo_t = rtmin - gt;
+    hi_t = bound() + gt;
+    cl = v3(-(o.x + g) * binv.x, -(o.y + g) * binv.y, -(o.z + g) * binv.z);
+    ch = v3(-(o.x - g) * binv.x, -(o.y - g) * binv.y, -(o.z - g) * binv.z);
+  };
   auto pop = [&]() {
-    const float thi = bound();
-    const float tc = fminf(thi, tcap);
-    const float gt = (wrf::kRayGrow * (tc * dlen + 1.f)) / dlen;
     cur = kDone;
     while (sp > 0) {
       --sp;
-      if (stk_t[sp * 64] <= thi + gt) {
+      if (t_up32(stk_t[sp * 64]) <= hi_t) {
         cur = stk_link[sp * 64];
         break;
       }
@@ -736,6 +762,8 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           const float ay = (F.lo.y - o.y) * binv.y, by = (F.hi.y - o.y) * binv.y;
           const float az = (F.lo.z - o.z) * binv.z, bz = (F.hi.z - o.z) * binv.z;
           tcap = fmaxf(0.f, fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)));
+          olen = fabsf(o.x) + fabsf(o.y) + fabsf(o.z);
+          margins();
         }
         if (__ballot(idle && idx >= n)) pool = false;
       }
@@ -755,15 +783,10 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         const float4* np = F.nodes + 4 * static_cast<size_t>(cur);
         const float4 n0 = np[0], n1 = np[1], n2 = np[2];
         const int4 lk = *reinterpret_cast<const int4*>(np + 3);
-        const float thi = bound();
-        const float tc = fminf(thi, tcap);
-        const float g = wrf::kRayGrow * (tc * dlen + 1.f);  // spatial margin for this ray
-        const float gt = g / dlen;
-        const float lo_t = rtmin - gt, hi_t = thi + gt;
         auto slab = [&](float lx, float ly, float lz, float hx, float hy, float hz, float& tn) {
-          const float x0 = (lx - g - o.x) * binv.x, x1 = (hx + g - o.x) * binv.x;
-          const float y0 = (ly - g - o.y) * binv.y, y1 = (hy + g - o.y) * binv.y;
-          const float z0 = (lz - g - o.z) * binv.z, z1 = (hz + g - o.z) * binv.z;
+          const float x0 = fmaf(lx, binv.x, cl.x), x1 = fmaf(hx, binv.x, ch.x);
+          const float y0 = fmaf(ly, binv.y, cl.y), y1 = fmaf(hy, binv.y, ch.y);
+          const float z0 = fmaf(lz, binv.z, cl.z), z1 = fmaf(hz, binv.z, ch.z);
           tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), lo_t));
           const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), hi_t));
           return tn <= tf;
@@ -774,7 +797,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         if (ha && hb) {
           const bool af = ta <= tb;
           stk_link[sp * 64] = af ? lk.y : lk.x;
-          stk_t[sp * 64] = af ? tb : ta;
+          stk_t[sp * 64] = t_down16(af ? tb : ta);
           ++sp;
           cur = af ? lk.x : lk.y;
         } else if (ha) {
@@ -818,6 +841,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           }
         }
       }
+      margins();
       pop();
     }
     // ---- finished rays: the candidate goes to k_fast_resolve
@@ -878,8 +902,15 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
           const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
           uint32_t steps = 0;
           const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
+          const uint64_t c0 = COUNT ? wall_clock64() : 0;
           need = (F.diag & 8) ? false : !kd_member(S, F, lb, ln, o, d, tmx ? tmx[r] : WR_INF, t1, steps);
-          if (COUNT) ctr.replay += steps;
+          if (COUNT) {
+            ctr.replay += steps;
+            const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c0);
+            ctr.mem_max = max(ctr.mem_max, dt);
+            ctr.mem_sum += dt;
+            ctr.scans += (ln > 4 && steps > 64) ? 1u : 0u;
+          }
         }
       }
     }
@@ -919,7 +950,13 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
     if (!(F.diag & 2)) {
       uint32_t steps = 0;
       int dbg = 0;
+      const uint64_t c0 = COUNT ? wall_clock64() : 0;
       const bool done = resolve_tie(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, dbg);
+      if (COUNT) {
+        const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c0);
+        ctr.tie_max = max(ctr.tie_max, dt);
+        ctr.tie_sum += dt;
+      }
       if (F.diag & 4) {  // debug: the resolution record instead of the answer
         outp[r] = -2 - dbg;
         continue;
@@ -939,7 +976,13 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
     // unresolved (a crowd of hits near m, or visited hits in the band): the walk decides
     if (COUNT) ++ctr.fallback;
     if (F.diag & 1) continue;
+    const uint64_t c1 = COUNT ? wall_clock64() : 0;
     kd_walk<COUNT>(S, o, d, rtmin, rtmax, stk_node, stk_tmin, tb, pb, ctr);
+    if (COUNT) {
+      const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c1);
+      ctr.walk_max = max(ctr.walk_max, dt);
+      ctr.walk_sum += dt;
+    }
     outt[r] = tb;
     outp[r] = pb;
   }

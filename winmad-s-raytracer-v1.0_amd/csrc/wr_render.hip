@@ -98,6 +98,7 @@ struct DevCounters {
   unsigned long long vm_queries, vm_found, vm_merged;  // VCM range queries / vertices in radius / merges
   unsigned long long bvh_nodes, bvh_tests, kd_replay, fallback;  // WR_TRACE_BVH work (count_work)
   unsigned long long verify_rays, verify_bad;                   // WR_BVH_VERIFY
+  unsigned long long lat[7];  // WR_TRACE_BVH latency tail (FastCounters mem_max .. scans; max or sum)
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -206,6 +207,11 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
   atomicAdd(&ctr->stamps[7], static_cast<unsigned long long>(fc.long_rays));
   atomicAdd(&ctr->stamps[4], static_cast<unsigned long long>(fc.fb_tie));
   for (int k = 0; k < 4; ++k) atomicAdd(&ctr->stamps[k], static_cast<unsigned long long>(fc.why[k]));
+  const uint32_t lat[7] = {fc.mem_max, fc.mem_sum, fc.tie_max, fc.tie_sum, fc.walk_max, fc.walk_sum, fc.scans};
+  for (int k = 0; k < 7; ++k) {
+    if (k % 2 == 0 && k < 6) atomicMax(&ctr->lat[k], static_cast<unsigned long long>(lat[k]));
+    else atomicAdd(&ctr->lat[k], static_cast<unsigned long long>(lat[k]));
+  }
 }
 template <bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32
@@ -727,19 +733,23 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
   if (c->fast_on && !c->stamps && ts.t2 && static_cast<size_t>(max_rays) <= ts.t2_cap) {
     const int blocks = (max_rays + kTraceBlock - 1) / kTraceBlock;
     const int fgrid = std::max(1, std::min(c->fast_blocks, blocks));
-    const size_t lds = fast_lds_bytes(c->fs.depth);
-    hipEvent_t f0 = nullptr, f1 = nullptr;
+    const size_t lds = fast_lds_bytes(c->fs.depth), slds = search_lds_bytes(c->fs.sdepth);
+    hipEvent_t f0 = nullptr, f1 = nullptr, fa = nullptr, fb = nullptr;
     if (c->trace_log) {
       (void)hipEventCreate(&f0);
       (void)hipEventCreate(&f1);
+      (void)hipEventCreate(&fa);
+      (void)hipEventCreate(&fb);
       (void)hipEventRecord(f0, stream);
     }
-    hipLaunchKernelGGL(count ? k_trace_fast<true> : k_trace_fast<false>, dim3(fgrid), dim3(kTraceBlock), lds, stream,
+    hipLaunchKernelGGL(count ? k_trace_fast<true> : k_trace_fast<false>, dim3(fgrid), dim3(kTraceBlock), slds, stream,
                        c->ds, c->fs, Q, ctr, fetch, ts.t2);
+    if (c->trace_log) (void)hipEventRecord(fa, stream);
     int* hard = reinterpret_cast<int*>(ts.t2 + ts.t2_cap);
     hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
                        dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), 0, stream, c->ds, c->fs,
                        Q, ctr, ts.t2, hard, ts.hard_n);
+    if (c->trace_log) (void)hipEventRecord(fb, stream);
     // the hard rays are a few in 10^4: a small grid drains any count
     hipLaunchKernelGGL(count ? k_fast_hard<true> : k_fast_hard<false>, dim3(std::max(1, std::min(256, blocks))),
                        dim3(kTraceBlock), lds, stream, c->ds, c->fs, Q, ctr, ts.t2, hard, ts.hard_n);
@@ -756,11 +766,18 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
         if (Q.q[i].count) (void)hipMemcpy(&k, Q.q[i].count, sizeof(int), hipMemcpyDeviceToHost);
         tot += k;
       }
-      float ms = 0.f;
+      float ms = 0.f, ma = 0.f, mb = 0.f;
+      int nh = 0;
+      (void)hipMemcpy(&nh, ts.hard_n, sizeof(int), hipMemcpyDeviceToHost);
       (void)hipEventElapsedTime(&ms, f0, f1);
-      std::fprintf(stderr, "[wr bvh] %d rays  %.1f us  grid %d\n", tot, ms * 1e3f, fgrid);
+      (void)hipEventElapsedTime(&ma, f0, fa);
+      (void)hipEventElapsedTime(&mb, fa, fb);
+      std::fprintf(stderr, "[wr bvh] %d rays  %.1f us (search %.1f, resolve %.1f, hard %.1f: %d rays)  grid %d\n", tot,
+                   ms * 1e3f, ma * 1e3f, mb * 1e3f, (ms - ma - mb) * 1e3f, nh, fgrid);
       (void)hipEventDestroy(f0);
       (void)hipEventDestroy(f1);
+      (void)hipEventDestroy(fa);
+      (void)hipEventDestroy(fb);
     }
     return WR_OK;
   }
@@ -878,13 +895,18 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
       mx[1] = std::max(mx[1], h.stamps[6]);
       mx[2] += h.stamps[7];
     }
-    unsigned long long ties = 0, why[4] = {0, 0, 0, 0};
+    unsigned long long ties = 0, why[4] = {0, 0, 0, 0}, lat[7] = {0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < n; ++i) {
       DevCounters h;
       HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
       ties += h.stamps[4];
       for (int k = 0; k < 4; ++k) why[k] += h.stamps[k];
+      for (int k = 0; k < 7; ++k) lat[k] = (k % 2 == 0 && k < 6) ? std::max(lat[k], h.lat[k]) : lat[k] + h.lat[k];
     }
+    std::fprintf(stderr,
+                 "[wr bvh latency, us] membership max %.1f sum %.1f; ties max %.1f sum %.1f; walks max %.1f sum %.1f; "
+                 "long many-leaf scans %llu\n",
+                 lat[0] * 0.01, lat[1] * 0.01, lat[2] * 0.01, lat[3] * 0.01, lat[4] * 0.01, lat[5] * 0.01, lat[6]);
     std::fprintf(stderr, "[wr bvh walks] many-leaf %llu, no visited hit %llu, crowd %llu, band %llu\n", why[0], why[1],
                  why[2], why[3]);
     std::fprintf(stderr, "[wr bvh tail] max nodes/ray %llu, max tests/ray %llu, rays > 256 nodes %llu, ties resolved by visit order %llu\n",
@@ -1311,12 +1333,14 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       }
       fs.lo = v3(lo[0], lo[1], lo[2]);
       fs.hi = v3(hi[0], hi[1], hi[2]);
-      // one stack serves the BVH search and the lane's KD fallback walk
+      // the search's stack holds BVH entries only; the hard rays' kernel walks
+      // both trees
+      fs.sdepth = fh.depth + 1;
       fs.depth = std::max(fh.depth + 1, d.max_stack + 1);
       c->fast_ok = true;
       int per_cu = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_fast<false>, kTraceBlock,
-                                                       fast_lds_bytes(fs.depth)) != hipSuccess ||
+                                                       search_lds_bytes(fs.sdepth)) != hipSuccess ||
           per_cu <= 0)
         per_cu = 8;
       c->fast_blocks = c->cus * per_cu;
@@ -1325,7 +1349,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       if (const char* e = std::getenv("WR_BVH_VERIFY")) c->verify = std::atoi(e) != 0;
       if (c->trace_log)
         std::fprintf(stderr, "[wr bvh] nodes %zu tris %zu depth %d lds %zu B/wave, %d waves/CU -> grid %d; kd grid %d\n",
-                     fbn, ftr, fs.depth, fast_lds_bytes(fs.depth), per_cu, c->fast_blocks, c->trace_blocks);
+                     fbn, ftr, fs.sdepth, search_lds_bytes(fs.sdepth), per_cu, c->fast_blocks, c->trace_blocks);
     }
   }
   *out = c;
