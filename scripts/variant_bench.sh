@@ -8,5 +8,5 @@ for v in "$@"; do
   lib=""; [ "$v" != default ] && lib=winmad-s-raytracer-v1.0_amd/variants/$v.so
   WR_LIB=$lib timeout -k 10 300 python3 bench.py --config $cfg --steps ${STEPS:-32} --warmup 2 --no-cpu $BENCH_ARGS \
     > gpurun_out/var_${cfg}_$v.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/var_${cfg}_$v.log; exit 1; }
-  echo "$cfg $v: $(python3 -c "import json; d=json.loads(open('gpurun_out/var_${cfg}_$v.log').read().strip().splitlines()[-1]); r=d['roofline']; print(d['value'], 'Mrays/s', r['tests_per_ray'], 'tests/ray', r.get('refs_per_ray'), 'refs/ray', r.get('bvh'))")"
+  echo "$cfg $v: $(python3 -c "import json; d=json.loads(open('gpurun_out/var_${cfg}_$v.log').read().strip().splitlines()[-1]); r=d['roofline'] or {}; print(d['value'], 'Mrays/s', r.get('tests_per_ray'), 'tests/ray', r.get('bvh'))")"
 done

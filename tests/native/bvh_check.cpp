@@ -1,6 +1,7 @@
 // Structural check of the verified-BVH data (wr_bvh.cpp) on a scene, CPU only:
 // built and run by tests/test_bvh_host.py.  Prints "OK <stats>" or the first
 // violated property and exits non-zero.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -87,6 +88,62 @@ int main(int argc, char** argv) {
   }
   if (leaves != static_cast<size_t>(f.leaves)) return fail("leaf count");
   if (maxdepth > f.depth + 1) return fail("depth bound");
+  // 2b. the 4-wide tree: the same leaves with the same boxes (bit for bit),
+  //     each once, inner boxes holding their children's, depth within depth4
+  //     (built with -DWR_BVH_WIDE=4 only)
+  if (!f.nodes4.empty()) {
+    std::vector<std::pair<int, std::vector<float>>> want, got;
+    std::vector<It> s2;
+    for (int c = 0; c < 2; ++c) {
+      const wrf::BNode& n = f.nodes[0];
+      s2.push_back(It{n.c[c], 1, {n.b[6 * c], n.b[6 * c + 1], n.b[6 * c + 2]}, {n.b[6 * c + 3], n.b[6 * c + 4], n.b[6 * c + 5]}});
+    }
+    while (!s2.empty()) {
+      const It it = s2.back();
+      s2.pop_back();
+      if (!(it.lo[0] <= it.hi[0])) continue;  // empty slot
+      if (it.link >= 0) {
+        const wrf::BNode& n = f.nodes[static_cast<size_t>(it.link)];
+        for (int c = 0; c < 2; ++c)
+          s2.push_back(It{n.c[c], 0, {n.b[6 * c], n.b[6 * c + 1], n.b[6 * c + 2]}, {n.b[6 * c + 3], n.b[6 * c + 4], n.b[6 * c + 5]}});
+      } else {
+        want.push_back({it.link, {it.lo[0], it.lo[1], it.lo[2], it.hi[0], it.hi[1], it.hi[2]}});
+      }
+    }
+    struct It4 {
+      int node, depth;
+      float lo[3], hi[3];
+    };
+    std::vector<It4> s4{{0, 1, {-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}}};
+    int maxd4 = 0;
+    size_t visits = 0;
+    while (!s4.empty()) {
+      const It4 it = s4.back();
+      s4.pop_back();
+      if (++visits > f.nodes4.size()) return fail("4-wide tree has a cycle");
+      maxd4 = std::max(maxd4, it.depth);
+      const wrf::BNode4& n = f.nodes4[static_cast<size_t>(it.node)];
+      for (int k = 0; k < 4; ++k) {
+        const float lo[3] = {n.lo[0][k], n.lo[1][k], n.lo[2][k]}, hi[3] = {n.hi[0][k], n.hi[1][k], n.hi[2][k]};
+        if (!(lo[0] <= hi[0])) continue;  // empty slot
+        for (int a = 0; a < 3; ++a)
+          if (lo[a] < it.lo[a] || hi[a] > it.hi[a]) return fail("4-wide child box outside its parent's");
+        if (n.c[k] >= 0) {
+          if (static_cast<size_t>(n.c[k]) >= f.nodes4.size()) return fail("4-wide link out of range");
+          s4.push_back(It4{n.c[k], it.depth + 1, {lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}});
+        } else {
+          got.push_back({n.c[k], {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]}});
+        }
+      }
+    }
+    if (maxd4 > f.depth4) return fail("4-wide depth bound");
+    std::sort(want.begin(), want.end());
+    std::sort(got.begin(), got.end());
+    if (want.size() != got.size()) return fail("4-wide tree leaf count");
+    for (size_t i = 0; i < want.size(); ++i)
+      if (want[i].first != got[i].first || std::memcmp(want[i].second.data(), got[i].second.data(), 24) != 0)
+        return fail("4-wide tree leaves differ from the binary tree's");
+  }
   // 3. KD membership: each primitive's leaves (ascending), its position in
   //    each, and the leaf paths lead from the root to that leaf
   std::vector<std::vector<std::pair<int, int>>> per(np);
@@ -100,16 +157,22 @@ int main(int argc, char** argv) {
     if (off < 0 || (off & 1)) return fail("leaf without an aligned path record");
     const uint32_t* rec = f.path.data() + 2 * static_cast<size_t>(off);
     const uint32_t n = rec[0];
-    size_t node = 0;  // follow the entries from the root
+    size_t node = 0;  // follow the entries from the root, cutting the root box
+    float lo[3] = {s.root_l.x, s.root_l.y, s.root_l.z}, hi[3] = {s.root_r.x, s.root_r.y, s.root_r.z};
     for (uint32_t e = 0; e < n; ++e) {
       const uint32_t bits = rec[2 * (4 + e)], w = rec[2 * (4 + e) + 1];
       const wr::KdNode& a = s.nodes[node];
       uint32_t sb;
       std::memcpy(&sb, &a.split, 4);
       if (a.axis < 0 || sb != bits || static_cast<uint32_t>(a.axis) != (w & 3u)) return fail("path entry mismatch");
+      if (w & 4u) lo[a.axis] = std::max(lo[a.axis], a.split);
+      else hi[a.axis] = std::min(hi[a.axis], a.split);
       node = (w & 4u) ? static_cast<size_t>(a.right) : node + 1;
     }
     if (node != i) return fail("path does not lead to its leaf");
+    // the record's cell (the membership witnesses' box) is the leaf's region
+    const float want_cell[6] = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
+    if (std::memcmp(want_cell, rec + 2, sizeof want_cell) != 0) return fail("leaf cell differs from its region");
     for (int j = 0; j < k.count; ++j) per[static_cast<size_t>(s.refs[static_cast<size_t>(k.first + j)])].emplace_back(off, j);
   }
   for (size_t p = 0; p < np; ++p) {
@@ -121,6 +184,16 @@ int main(int argc, char** argv) {
         return fail("leaf list of prim " + std::to_string(p));
       if (k > lb && f.prim_leaf[static_cast<size_t>(k)] <= f.prim_leaf[static_cast<size_t>(k - 1)])
         return fail("leaf list not ascending");
+    }
+    // the primitive's record: leaf count, first four leaves' offsets and cells
+    const wrf::PrimRec& r = f.prim_rec[p];
+    if (r.ln != le - lb) return fail("record leaf count of prim " + std::to_string(p));
+    for (int k = 0; k < 4; ++k) {
+      const int off = k < r.ln ? f.prim_leaf[static_cast<size_t>(lb + k)] : -1;
+      if (r.off[k] != off) return fail("record offsets of prim " + std::to_string(p));
+      float want_cell[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      if (off >= 0) std::memcpy(want_cell, f.path.data() + 2 * static_cast<size_t>(off) + 2, sizeof want_cell);
+      if (std::memcmp(want_cell, r.cell[k], sizeof want_cell) != 0) return fail("record cells of prim " + std::to_string(p));
     }
   }
   std::printf("OK prims %zu nodes %zu leaves %zu depth %d refs %zu\n", np, f.nodes.size(), leaves, f.depth,

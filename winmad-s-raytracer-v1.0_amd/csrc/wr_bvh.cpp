@@ -257,7 +257,80 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
     }
   // the replay reads 8 entries at a time: pad past the last record
   out.path.resize(out.path.size() + 2 * 8, 0u);
+  // per primitive: its first four leaves' cells and records in one line
+  out.prim_rec.assign(np, PrimRec{});
+  for (size_t p = 0; p < np; ++p) {
+    PrimRec& r = out.prim_rec[p];
+    r.ln = static_cast<int32_t>(per[p].size());
+    for (int k = 0; k < 4; ++k) {
+      const bool have = k < r.ln;
+      const int32_t off = have ? per[p][static_cast<size_t>(k)].first : -1;
+      r.off[k] = off;
+      for (int a = 0; a < 6; ++a) {
+        float v = a < 3 ? INFINITY : -INFINITY;
+        if (have) std::memcpy(&v, &out.path[2 * static_cast<size_t>(off) + 2 + static_cast<size_t>(a)], 4);
+        r.cell[k][a] = v;
+      }
+    }
+  }
 }
+
+// The 4-wide tree: each node takes its binary node's children and opens the
+// inner child of largest area until it holds four (or only leaves remain).
+struct Collapse {
+  FastHost& out;
+  struct Kid {
+    float lo[3], hi[3];
+    int link;
+    double area() const {
+      if (!(lo[0] <= hi[0])) return 0.0;
+      const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+      return 2.0 * (x * y + x * z + y * z);
+    }
+  };
+  Kid kid(int n2, int side) const {
+    const BNode& b = out.nodes[static_cast<size_t>(n2)];
+    Kid k;
+    for (int a = 0; a < 3; ++a) {
+      k.lo[a] = b.b[6 * side + a];
+      k.hi[a] = b.b[6 * side + 3 + a];
+    }
+    k.link = b.c[side];
+    return k;
+  }
+  int node(int n2, int depth) {
+    out.depth4 = std::max(out.depth4, depth);
+    Kid ks[4] = {kid(n2, 0), kid(n2, 1), {}, {}};
+    int n = 2;
+    while (n < 4) {
+      int best = -1;
+      double ba = -1.0;
+      for (int i = 0; i < n; ++i)
+        if (ks[i].link >= 0 && ks[i].area() > ba) {
+          ba = ks[i].area();
+          best = i;
+        }
+      if (best < 0) break;
+      const int open = ks[best].link;
+      ks[best] = kid(open, 0);
+      ks[n++] = kid(open, 1);
+    }
+    const int at = static_cast<int>(out.nodes4.size());
+    out.nodes4.emplace_back();
+    int links[4];
+    for (int i = 0; i < 4; ++i) links[i] = i < n && ks[i].link >= 0 ? node(ks[i].link, depth + 1) : (i < n ? ks[i].link : ~0);
+    BNode4& d = out.nodes4[static_cast<size_t>(at)];
+    for (int i = 0; i < 4; ++i) {
+      for (int a = 0; a < 3; ++a) {
+        d.lo[a][i] = i < n ? ks[i].lo[a] : INFINITY;
+        d.hi[a][i] = i < n ? ks[i].hi[a] : -INFINITY;
+      }
+      d.c[i] = links[i];
+      d.pad[i] = 0;
+    }
+    return at;
+  }
+};
 
 }  // namespace
 
@@ -325,6 +398,10 @@ void build_fast(const wr::Scene& s, FastHost& out) {
     int m = B.split(0, nn, all);
     if (m < 0) m = nn / 2;
     B.inner(0, nn, m, 1);
+  }
+  if (out.ok && WR_BVH_WIDE == 4) {
+    out.nodes4.reserve(out.nodes.size() / 2 + 4);
+    Collapse{out}.node(0, 1);
   }
 }
 

@@ -45,6 +45,18 @@ struct BNode {
 };
 static_assert(sizeof(BNode) == 64, "BVH node record is 64 bytes");
 
+// 128 bytes (one cache line): a 4-wide node of the search, collapsed from the
+// binary BVH (same leaves).  Boxes by axis across the children, then links:
+//   lo[a][k], hi[a][k]  child k's box; c[k] child link as in BNode (empty
+//   slot: inverted box, never hit)
+struct BNode4 {
+  float lo[3][4];
+  float hi[3][4];
+  int32_t c[4];
+  int32_t pad[4];
+};
+static_assert(sizeof(BNode4) == 128, "4-wide BVH node is 128 bytes");
+
 // 48 bytes per triangle, in BVH leaf order, laid out as the KD refs
 // (wr_traverse.h): (p0.xyz, A), (B, C, D, E), (F, prim, lb, ln) with A..F =
 // p0 - p1, p0 - p2 exactly as Triangle::hit forms them and [lb, lb + ln) the
@@ -61,6 +73,20 @@ static_assert(sizeof(TriRec) == 48, "BVH triangle record is 48 bytes");
 // prim_leaf[prim_leaf_off[p] .. prim_leaf_off[p+1]) = path offsets of the KD
 // leaves that hold primitive p (ascending), prim_leaf_pos = its index in each
 // leaf's list; node_path maps a KD leaf node to its record.
+// 128 bytes per primitive (one cache line): the cells and path record offsets
+// of its first four KD leaves, for the membership test of a winning primitive
+// without index lookups.  Unused cells are empty (lo = +inf, hi = -inf).
+struct PrimRec {
+  float cell[4][6];  // lo.xyz, hi.xyz
+  int32_t off[4];    // path record offsets (-1: none)
+  int32_t ln;        // the primitive's KD leaf count (> 4: only the first four here)
+  int32_t pad[3];
+};
+static_assert(sizeof(PrimRec) == 128, "primitive membership record is 128 bytes");
+
+#ifndef WR_BVH_WIDE
+#define WR_BVH_WIDE 2  // the search's tree: 2 = BNode (measured faster), 4 = BNode4
+#endif
 #ifndef WR_BVH_LEAF
 #define WR_BVH_LEAF 4
 #endif
@@ -87,11 +113,14 @@ struct Scene;
 namespace wrf {
 struct FastHost {
   std::vector<BNode> nodes;
+  std::vector<BNode4> nodes4;  // the search's tree (root 0)
+  int depth4 = 0;              // deepest 4-wide node chain
   std::vector<TriRec> tris;
   std::vector<int32_t> prim_leaf_off, prim_leaf, prim_leaf_pos;
   std::vector<int32_t> node_path;  // KD leaf node -> its path record offset (-1: inner node)
   std::vector<float> node_cell;    // per KD node: cell lo.xyz, 0, hi.xyz, 0
   std::vector<uint32_t> path;  // pairs
+  std::vector<PrimRec> prim_rec;  // per primitive
   int depth = 0;               // deepest node chain (stack bound)
   int leaves = 0;
   bool ok = false;

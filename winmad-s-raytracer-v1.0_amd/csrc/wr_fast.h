@@ -36,7 +36,8 @@
 namespace wrd {
 
 struct FastScene {
-  const float4* nodes;  // 4 per wrf::BNode
+  const float4* nodes;  // 4 per wrf::BNode (tie resolution's collection)
+  const float4* nodes4;  // 8 per wrf::BNode4 (the search, WR_BVH_WIDE 4)
   const float4* tris;   // 3 per wrf::TriRec
   const int* prim_leaf_off;
   const int* prim_leaf;
@@ -44,6 +45,7 @@ struct FastScene {
   const uint2* path;
   const int* node_path;  // KD leaf node -> path record offset
   const float4* node_cell;  // 2 per KD node: cell lo, hi
+  const float4* prim_rec;   // 8 per primitive (wrf::PrimRec): its first four leaves' cells and records
   V3 lo, hi;  // union of the (grown) triangle boxes
   int depth;   // stack entries of the KD walks and tie resolution (k_fast_hard, k_fast_verify)
   int sdepth;  // stack entries of the BVH search (k_trace_fast): the BVH's depth + 1
@@ -69,7 +71,20 @@ __host__ __device__ constexpr size_t fast_lds_bytes(int depth) { return size_t(d
 // bytes).  A rounded-down entry t only lets more subtrees through the pop test
 // (t_entry <= bound), never fewer, so the search still reports every hit it
 // must; 6 instead of 8 bytes per entry raise the waves per CU the LDS allows.
-__host__ __device__ constexpr size_t search_lds_bytes(int depth) { return size_t(depth) * 64 * 6; }
+// The first kLdsStack entries live in LDS, deeper ones (rare) in a per-lane
+// global spill area, so that the 4-wide tree's worst case (3 entries per
+// level) does not set the LDS size and with it the waves per CU.
+#ifndef WR_BVH_LDS_STACK
+#define WR_BVH_LDS_STACK 64  // the binary tree never spills; the 4-wide one ran with 12
+#endif
+constexpr int kLdsStack = WR_BVH_LDS_STACK;
+__host__ __device__ constexpr size_t search_lds_bytes(int depth) {
+  return size_t(depth < kLdsStack ? depth : kLdsStack) * 64 * 6;
+}
+// spill entries per lane for a search stack of `depth` entries
+__host__ __device__ constexpr size_t search_spill_entries(int depth) {
+  return depth > kLdsStack ? size_t(depth - kLdsStack) : 0;
+}
 __device__ __forceinline__ uint16_t t_down16(float t) {
   return static_cast<uint16_t>(__float_as_uint(fmaxf(t, 0.f)) >> 16);  // truncation: down for t >= 0
 }
@@ -187,6 +202,14 @@ __device__ __forceinline__ bool cell_crossed_with_margin(uint4 h0, uint4 h1, V3 
   return tw > 0.f && cell_holds_with_margin(h0, h1, o, d, tw, o + d * tw);
 }
 
+// The witness for a cell given as six floats.
+__device__ __forceinline__ bool box_crossed_with_margin(float lx, float ly, float lz, float hx, float hy, float hz, V3 o,
+                                                        V3 d, V3 binv, float rtmax) {
+  const uint4 h0 = make_uint4(0u, 0u, __float_as_uint(lx), __float_as_uint(ly));
+  const uint4 h1 = make_uint4(__float_as_uint(lz), __float_as_uint(hx), __float_as_uint(hy), __float_as_uint(hz));
+  return cell_crossed_with_margin(h0, h1, o, d, binv, rtmax);
+}
+
 // Is the primitive whose KD leaves are prim_leaf[lb, lb + ln) tested by the
 // reference's traversal of this ray?
 __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F, int lb, int ln, V3 o, V3 d,
@@ -216,8 +239,26 @@ __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F,
       if (kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return true;
     }
   }
-  // the leaves whose cell holds the hit point first (usually the one reached),
-  // then the others
+  if (ln >= 1 && ln <= 4) {
+    // witnesses first, all of the primitive's leaves at once: the list
+    // entries, then the cells, each set of loads in flight together
+    int off[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) off[k] = F.prim_leaf[lb + min(k, ln - 1)];
+    uint4 h0[4], h1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint2* rec = F.path + off[k];
+      h0[k] = *reinterpret_cast<const uint4*>(rec);
+      h1[k] = *reinterpret_cast<const uint4*>(rec + 2);
+    }
+    bool seen = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) seen |= k < ln && cell_crossed_with_margin(h0[k], h1[k], o, d, binv, rtmax);
+    if (seen) return true;
+  }
+  // replays: the leaves whose cell holds the hit point first (usually the one
+  // reached), then the others
   for (int pass = 0; pass < 2; ++pass) {
     for (int k = lb; k < lb + ln; ++k) {
       const uint2* rec = F.path + F.prim_leaf[k];
@@ -225,7 +266,7 @@ __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F,
       const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
       const bool in = p.x >= __uint_as_float(h0.z) && p.y >= __uint_as_float(h0.w) && p.z >= __uint_as_float(h1.x) &&
                       p.x <= __uint_as_float(h1.y) && p.y <= __uint_as_float(h1.z) && p.z <= __uint_as_float(h1.w);
-      if (pass == 0 && cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return true;
+      if (pass == 0 && ln > 4 && cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return true;
       if (in == (pass == 0) && kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return true;
     }
   }
@@ -668,10 +709,11 @@ __device__ __forceinline__ auto qfield(const TraceQueues& Q, int q, Fn field) {
 
 template <bool COUNT>
 __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, int* fetch,
-                                           float* t2buf, uint32_t* lds, FastCounters& ctr) {
+                                           float* t2buf, int2* spill, uint32_t* lds, FastCounters& ctr) {
   const int lane = __lane_id();
   int* stk_link = reinterpret_cast<int*>(lds) + lane;
-  uint16_t* stk_t = reinterpret_cast<uint16_t*>(reinterpret_cast<int*>(lds) + F.sdepth * 64) + lane;
+  uint16_t* stk_t = reinterpret_cast<uint16_t*>(reinterpret_cast<int*>(lds) + min(F.sdepth, kLdsStack) * 64) + lane;
+  const size_t gl = static_cast<size_t>(gridDim.x) * 64, gidx = static_cast<size_t>(blockIdx.x) * 64 + lane;
   const QueueIndex QI(Q);
   const int n = QI.n;
   int r = -1, qi = 0, lidx = 0;
@@ -719,12 +761,31 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
     cl = v3(-(o.x + g) * binv.x, -(o.y + g) * binv.y, -(o.z + g) * binv.z);
     ch = v3(-(o.x - g) * binv.x, -(o.y - g) * binv.y, -(o.z - g) * binv.z);
   };
+  auto push = [&](int link, float t) {
+    if (sp < kLdsStack) {
+      stk_link[sp * 64] = link;
+      stk_t[sp * 64] = t_down16(t);
+    } else {
+      spill[static_cast<size_t>(sp - kLdsStack) * gl + gidx] = make_int2(link, __float_as_int(t));
+    }
+    ++sp;
+  };
   auto pop = [&]() {
     cur = kDone;
     while (sp > 0) {
       --sp;
-      if (t_up32(stk_t[sp * 64]) <= hi_t) {
-        cur = stk_link[sp * 64];
+      int link;
+      float te;
+      if (sp < kLdsStack) {
+        link = stk_link[sp * 64];
+        te = t_up32(stk_t[sp * 64]);
+      } else {
+        const int2 e = spill[static_cast<size_t>(sp - kLdsStack) * gl + gidx];
+        link = e.x;
+        te = __int_as_float(e.y);
+      }
+      if (te <= hi_t) {
+        cur = link;
         break;
       }
     }
@@ -780,6 +841,50 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           ++ctr.nodes;
           ++rn;
         }
+#if WR_BVH_WIDE == 4
+        // a 4-wide node: the four boxes, then the hit children nearest first
+        // (the nearest is visited next, the others pushed farthest first)
+        const float4* np = F.nodes4 + 8 * static_cast<size_t>(cur);
+        const float4 bx0 = np[0], by0 = np[1], bz0 = np[2], bx1 = np[3], by1 = np[4], bz1 = np[5];
+        const int4 lk = *reinterpret_cast<const int4*>(np + 6);
+        auto slab4 = [&](float lx, float ly, float lz, float hx, float hy, float hz) {
+          const float x0 = fmaf(lx, binv.x, cl.x), x1 = fmaf(hx, binv.x, ch.x);
+          const float y0 = fmaf(ly, binv.y, cl.y), y1 = fmaf(hy, binv.y, ch.y);
+          const float z0 = fmaf(lz, binv.z, cl.z), z1 = fmaf(hz, binv.z, ch.z);
+          const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), lo_t));
+          const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), hi_t));
+          return tn <= tf ? tn : __int_as_float(0x7f800000);  // miss: +inf (a hit's tn <= hi_t is finite)
+        };
+        float k0 = slab4(bx0.x, by0.x, bz0.x, bx1.x, by1.x, bz1.x);
+        float k1 = slab4(bx0.y, by0.y, bz0.y, bx1.y, by1.y, bz1.y);
+        float k2 = slab4(bx0.z, by0.z, bz0.z, bx1.z, by1.z, bz1.z);
+        float k3 = slab4(bx0.w, by0.w, bz0.w, bx1.w, by1.w, bz1.w);
+        int l0 = lk.x, l1 = lk.y, l2 = lk.z, l3 = lk.w;
+        const int nh = (k0 < __int_as_float(0x7f800000)) + (k1 < __int_as_float(0x7f800000)) +
+                       (k2 < __int_as_float(0x7f800000)) + (k3 < __int_as_float(0x7f800000));
+        auto cswap = [](float& ta, int& la, float& tb, int& lb) {
+          const bool s = tb < ta;
+          const float t = s ? tb : ta;
+          tb = s ? ta : tb;
+          ta = t;
+          const int l = s ? lb : la;
+          lb = s ? la : lb;
+          la = l;
+        };
+        cswap(k0, l0, k1, l1);
+        cswap(k2, l2, k3, l3);
+        cswap(k0, l0, k2, l2);
+        cswap(k1, l1, k3, l3);
+        cswap(k1, l1, k2, l2);
+        if (nh == 0) {
+          pop();
+        } else {
+          if (nh > 3) push(l3, k3);
+          if (nh > 2) push(l2, k2);
+          if (nh > 1) push(l1, k1);
+          cur = l0;
+        }
+#else
         const float4* np = F.nodes + 4 * static_cast<size_t>(cur);
         const float4 n0 = np[0], n1 = np[1], n2 = np[2];
         const int4 lk = *reinterpret_cast<const int4*>(np + 3);
@@ -796,9 +901,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         const bool hb = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tb);
         if (ha && hb) {
           const bool af = ta <= tb;
-          stk_link[sp * 64] = af ? lk.y : lk.x;
-          stk_t[sp * 64] = t_down16(af ? tb : ta);
-          ++sp;
+          push(af ? lk.y : lk.x, af ? tb : ta);
           cur = af ? lk.x : lk.y;
         } else if (ha) {
           cur = lk.x;
@@ -807,6 +910,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         } else {
           pop();
         }
+#endif
       }
     }
     // ---- leaf: test its triangles (Triangle::hit), keep (t1, p1) and t2
@@ -887,29 +991,42 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
     if (idx < QI.n) {
       int q, r;
       QI.locate(idx, q, r);
+      // every load that does not depend on p1 in flight at once
       const int p1 = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r];
+      const float t1 = qfield(Q, q, [](const RayQueue& x) { return x.out_t; })[r], t2 = t2buf[idx];
+      const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
+      const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
+      const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
+      const float* tmx = qfield(Q, q, [](const RayQueue& x) { return x.tmax; });
+      const V3 o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
+      const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+      const float rtmax = tmx ? tmx[r] : WR_INF;
+      // p1's membership record: one line with its first four leaves' cells
+      const float4* pr = F.prim_rec + 8 * static_cast<size_t>(max(p1, 0));
+      const float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3], c4 = pr[4], c5 = pr[5];
       if (p1 >= 0) {  // (no hit anywhere: a miss for the reference too)
-        const float t1 = qfield(Q, q, [](const RayQueue& x) { return x.out_t; })[r], t2 = t2buf[idx];
         const bool tie = !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0);
         if (tie) {
           need = true;
-        } else {
-          const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
-          const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
-          const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
-          const float* tmx = qfield(Q, q, [](const RayQueue& x) { return x.tmax; });
-          const V3 o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
-          const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
-          uint32_t steps = 0;
-          const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
-          const uint64_t c0 = COUNT ? wall_clock64() : 0;
-          need = (F.diag & 8) ? false : !kd_member(S, F, lb, ln, o, d, tmx ? tmx[r] : WR_INF, t1, steps);
-          if (COUNT) {
-            ctr.replay += steps;
-            const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c0);
-            ctr.mem_max = max(ctr.mem_max, dt);
-            ctr.mem_sum += dt;
-            ctr.scans += (ln > 4 && steps > 64) ? 1u : 0u;
+        } else if (!(F.diag & 8)) {
+          const V3 binv = v3(clamp_inv(d.x), clamp_inv(d.y), clamp_inv(d.z));
+          const bool seen = box_crossed_with_margin(c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, o, d, binv, rtmax) ||
+                            box_crossed_with_margin(c1.z, c1.w, c2.x, c2.y, c2.z, c2.w, o, d, binv, rtmax) ||
+                            box_crossed_with_margin(c3.x, c3.y, c3.z, c3.w, c4.x, c4.y, o, d, binv, rtmax) ||
+                            box_crossed_with_margin(c4.z, c4.w, c5.x, c5.y, c5.z, c5.w, o, d, binv, rtmax);
+          if (!seen) {
+            // the other leaves (more than four) and the replays
+            uint32_t steps = 0;
+            const uint64_t t0 = COUNT ? wall_clock64() : 0;
+            const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
+            need = !kd_member(S, F, lb, ln, o, d, rtmax, t1, steps);
+            if (COUNT) {
+              ctr.replay += steps;
+              const uint32_t dt = static_cast<uint32_t>(wall_clock64() - t0);
+              ctr.mem_max = max(ctr.mem_max, dt);
+              ctr.mem_sum += dt;
+              ctr.scans += (ln > 4 && steps > 64) ? 1u : 0u;
+            }
           }
         }
       }

@@ -215,10 +215,10 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
 }
 template <bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32
-k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf) {
+k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* spill) {
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
-  trace_fast<COUNT>(S, F, Q, fetch, t2buf, smem, fc);
+  trace_fast<COUNT>(S, F, Q, fetch, t2buf, spill, smem, fc);
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 template <bool COUNT>
@@ -375,6 +375,7 @@ struct Pipe {
   PtBuf pb[kGroup]{};
   VcmBuf vb[kGroup]{};
   float* t2buf = nullptr;  // WR_TRACE_BVH: per-ray t2 of the BVH search (launch index)
+  int2* spill = nullptr;   // WR_TRACE_BVH: the search stack's spill area (fast_blocks x 64 lanes)
   size_t t2_cap = 0;
   std::vector<hipEvent_t> events;  // Timer marks (time_kernels)
   std::vector<int> ev_cat;
@@ -421,6 +422,7 @@ struct wr_context {
   bool verify = false;      // WR_BVH_VERIFY=1: every BVH answer checked against the KD walk
   float* api_t2 = nullptr;  // t2 scratch of the API path
   size_t api_t2_cap = 0;
+  int2* api_spill = nullptr;  // the API path's search stack spill area
 };
 
 namespace {
@@ -707,13 +709,17 @@ struct TraceSlot {
   float* t2;      // [t2_cap] t2 per launch index, then [t2_cap] the hard-ray list
   size_t t2_cap;
   int* hard_n;
+  int2* spill;    // the search stack's spill area
 };
 TraceSlot tslot(Pipe& p, int slot) {
-  return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap, &p.sc[0].hard[slot]};
+  return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap, &p.sc[0].hard[slot], p.spill};
 }
 // t2 scratch + hard-ray list of a pipeline for launches of up to `rays` rays
 int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
-  if (!c->fast_on || p.t2_cap >= rays) return WR_OK;
+  if (!c->fast_on) return WR_OK;
+  if (!p.spill && search_spill_entries(c->fs.sdepth) > 0)
+    HIPCHK(hipMalloc(&p.spill, search_spill_entries(c->fs.sdepth) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
+  if (p.t2_cap >= rays) return WR_OK;
   if (p.t2buf) (void)hipFree(p.t2buf);
   p.t2buf = nullptr;
   p.t2_cap = 0;
@@ -743,7 +749,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
       (void)hipEventRecord(f0, stream);
     }
     hipLaunchKernelGGL(count ? k_trace_fast<true> : k_trace_fast<false>, dim3(fgrid), dim3(kTraceBlock), slds, stream,
-                       c->ds, c->fs, Q, ctr, fetch, ts.t2);
+                       c->ds, c->fs, Q, ctr, fetch, ts.t2, ts.spill);
     if (c->trace_log) (void)hipEventRecord(fa, stream);
     int* hard = reinterpret_cast<int*>(ts.t2 + ts.t2_cap);
     hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
@@ -1287,7 +1293,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       const size_t fnp = fh.node_path.size();
       const size_t fbytes = measure([&](Arena& a) {
         a.take<wrf::BNode>(fbn); a.take<wrf::TriRec>(ftr); a.take<int>(fpo); a.take<int>(fpl); a.take<int>(fpl);
-        a.take<uint2>(fpa); a.take<int>(fnp); a.take<float4>(2 * fnp);
+        a.take<uint2>(fpa); a.take<int>(fnp); a.take<float4>(2 * fnp); a.take<wrf::PrimRec>(fh.prim_rec.size());
+        a.take<wrf::BNode4>(fh.nodes4.size());
       });
       if (int rc = c->fast_mem.reserve(fbytes)) {
         wr_destroy(c);
@@ -1302,6 +1309,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       uint2* dpa = F.take<uint2>(fpa);
       int* dnp = F.take<int>(fnp);
       float4* dnc = F.take<float4>(2 * fnp);
+      auto* dpr = F.take<wrf::PrimRec>(fh.prim_rec.size());
+      auto* dn4 = F.take<wrf::BNode4>(fh.nodes4.size());
       hipError_t fe = hipSuccess;
       for (hipError_t x : {hipMemcpy(dno, fh.nodes.data(), fbn * sizeof(wrf::BNode), hipMemcpyHostToDevice),
                            hipMemcpy(dtr, fh.tris.data(), ftr * sizeof(wrf::TriRec), hipMemcpyHostToDevice),
@@ -1311,7 +1320,11 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                                      hipMemcpyHostToDevice),
                            hipMemcpy(dpa, fh.path.data(), fpa * sizeof(uint2), hipMemcpyHostToDevice),
                            hipMemcpy(dnp, fh.node_path.data(), fnp * sizeof(int), hipMemcpyHostToDevice),
-                           hipMemcpy(dnc, fh.node_cell.data(), 8 * fnp * sizeof(float), hipMemcpyHostToDevice)})
+                           hipMemcpy(dnc, fh.node_cell.data(), 8 * fnp * sizeof(float), hipMemcpyHostToDevice),
+                           hipMemcpy(dpr, fh.prim_rec.data(), fh.prim_rec.size() * sizeof(wrf::PrimRec),
+                                     hipMemcpyHostToDevice),
+                           hipMemcpy(dn4, fh.nodes4.data(), fh.nodes4.size() * sizeof(wrf::BNode4),
+                                     hipMemcpyHostToDevice)})
         if (x != hipSuccess) fe = x;
       if (fe != hipSuccess) {
         wr_destroy(c);
@@ -1326,6 +1339,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       fs.path = dpa;
       fs.node_path = dnp;
       fs.node_cell = dnc;
+      fs.prim_rec = reinterpret_cast<const float4*>(dpr);
+      fs.nodes4 = reinterpret_cast<const float4*>(dn4);
       float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
       for (int k = 0; k < 3; ++k) {
         lo[k] = std::min(fh.nodes[0].b[k], fh.nodes[0].b[6 + k]);
@@ -1335,7 +1350,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       fs.hi = v3(hi[0], hi[1], hi[2]);
       // the search's stack holds BVH entries only; the hard rays' kernel walks
       // both trees
-      fs.sdepth = fh.depth + 1;
+      fs.sdepth = WR_BVH_WIDE == 4 ? 3 * fh.depth4 + 1 : fh.depth + 1;
       fs.depth = std::max(fh.depth + 1, d.max_stack + 1);
       c->fast_ok = true;
       int per_cu = 0;
@@ -1343,6 +1358,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                                                        search_lds_bytes(fs.sdepth)) != hipSuccess ||
           per_cu <= 0)
         per_cu = 8;
+      // diagnostic: WR_FAST_WAVES_PER_CU caps the search's resident waves
+      if (const char* e = std::getenv("WR_FAST_WAVES_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
       c->fast_blocks = c->cus * per_cu;
       if (const char* e = std::getenv("WR_TRACE_BVH")) c->fast_on = std::atoi(e) != 0;
       if (const char* e = std::getenv("WR_BVH_DIAG")) fs.diag = std::atoi(e);
@@ -1387,8 +1404,11 @@ void wr_destroy(wr_context* c) {
   if (c->film_tmp) (void)hipFree(c->film_tmp);
   if (c->api_tmp) (void)hipFree(c->api_tmp);
   if (c->api_t2) (void)hipFree(c->api_t2);
-  for (Pipe& p : c->pipes)
+  if (c->api_spill) (void)hipFree(c->api_spill);
+  for (Pipe& p : c->pipes) {
     if (p.t2buf) (void)hipFree(p.t2buf);
+    if (p.spill) (void)hipFree(p.spill);
+  }
   c->fast_mem.release();
   c->scene_mem.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1450,7 +1470,9 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   }
   QueueList ql;
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
-  const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard};
+  if (c->fast_on && !c->api_spill && search_spill_entries(c->fs.sdepth) > 0)
+    HIPCHK(hipMalloc(&c->api_spill, search_spill_entries(c->fs.sdepth) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
+  const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard, c->api_spill};
   trace_launch(c, c->stream, c->ctr, ts, tm, false, ql.Q, ql.max_rays,
                c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN));
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
