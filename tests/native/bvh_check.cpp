@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
   for (size_t p = 0; p < np; ++p)
     if (seen[p] != 1) return fail("triangle " + std::to_string(p) + " appears " + std::to_string(seen[p]) + " times");
   // 2. child boxes contain their subtree's triangles (vertices)
-  size_t leaves = 0;
+  size_t leaves = 0, leaf_hist[9] = {};
   int maxdepth = 0;
   struct It {
     int link, depth;
@@ -74,6 +74,7 @@ int main(int argc, char** argv) {
     } else {
       ++leaves;
       const int l = ~it.link, first = l >> 3, cnt = (l & 7) + 1;
+      ++leaf_hist[cnt];
       if (cnt > wrf::kMaxLeaf) return fail("leaf too large");
       for (int j = 0; j < cnt; ++j) {
         int p;
@@ -196,7 +197,9 @@ int main(int argc, char** argv) {
       if (std::memcmp(want_cell, r.cell[k], sizeof want_cell) != 0) return fail("record cells of prim " + std::to_string(p));
     }
   }
-  std::printf("OK prims %zu nodes %zu leaves %zu depth %d refs %zu\n", np, f.nodes.size(), leaves, f.depth,
+  std::printf("OK prims %zu nodes %zu leaves %zu depth %d refs %zu leaf sizes", np, f.nodes.size(), leaves, f.depth,
               f.prim_leaf.size());
+  for (int k = 1; k <= wrf::kMaxLeaf; ++k) std::printf(" %d:%zu", k, leaf_hist[k]);
+  std::printf("\n");
   return 0;
 }

@@ -88,7 +88,12 @@ static_assert(sizeof(PrimRec) == 128, "primitive membership record is 128 bytes"
 #define WR_BVH_WIDE 2  // the search's tree: 2 = BNode (measured faster), 4 = BNode4
 #endif
 #ifndef WR_BVH_LEAF
-#define WR_BVH_LEAF 4
+// 2: the search keeps 2 instead of 4 triangle records in flight per leaf
+// (79 instead of 95 VGPRs, 6 waves per SIMD); the SAH build rarely makes
+// larger leaves anyway (torus: none).  Measured at 64 iterations, BVH mode,
+// leaf 4 -> 2: C2 2,370 -> 2,411, VCM 1,670 -> 1,694, C4 759 -> 809, C3
+// 2,432 -> 2,480 Mrays/s
+#define WR_BVH_LEAF 2
 #endif
 #ifndef WR_BVH_BOX_GROW
 #define WR_BVH_BOX_GROW 0.002f

@@ -49,7 +49,8 @@ struct FastScene {
   V3 lo, hi;  // union of the (grown) triangle boxes
   int depth;   // stack entries of the KD walks and tie resolution (k_fast_hard, k_fast_verify)
   int sdepth;  // stack entries of the BVH search (k_trace_fast): the BVH's depth + 1
-  int diag;   // WR_BVH_DIAG (measurement only): 1 = skip the KD walks, 8 = skip the replays (wrong answers); 2 = KD walk for every tie
+  int diag;   // WR_BVH_DIAG (measurement only): 1 = skip the KD walks, 8 = skip the replays, 16 = skip k_fast_resolve,
+              // 32 = skip k_fast_hard (all wrong answers); 2 = KD walk for every tie
 };
 
 struct FastCounters {  // algorithmic work (count_work)
@@ -85,6 +86,18 @@ __host__ __device__ constexpr size_t search_lds_bytes(int depth) {
 __host__ __device__ constexpr size_t search_spill_entries(int depth) {
   return depth > kLdsStack ? size_t(depth - kLdsStack) : 0;
 }
+// Can the search's stack outgrow the LDS columns?  Not for the binary tree
+// (kMaxBvhDepth + 1 entries fit), so its push / pop carry no spill branch: a
+// generic pointer select between LDS and the spill area made the compiler emit
+// flat loads (vmcnt + lgkmcnt waits) on every pop.
+constexpr bool kSearchSpills = (WR_BVH_WIDE == 4 ? 3 * wrf::kMaxBvhDepth + 1 : wrf::kMaxBvhDepth + 1) > kLdsStack;
+// Speculative leaves (Aila & Laine 2009): a lane that has found its leaf keeps
+// descending inner nodes while other lanes still look for theirs, and the
+// leaf is tested (postponed) with theirs.  Extra nodes visited under a stale
+// (larger) bound only add hits beyond the window, never drop one inside it.
+#ifndef WR_BVH_SPEC
+#define WR_BVH_SPEC 1
+#endif
 __device__ __forceinline__ uint16_t t_down16(float t) {
   return static_cast<uint16_t>(__float_as_uint(fmaxf(t, 0.f)) >> 16);  // truncation: down for t >= 0
 }
@@ -469,6 +482,67 @@ __device__ __noinline__ void first_leaf(const FastScene& F, int p, V3 o, V3 d, V
   }
 }
 
+// first_leaf for the candidates cp[0, ncand) of ONE ray, with the wave's lanes
+// sharing the work (every lane holds the same ray and list): the candidates'
+// leaf lists are laid end to end, lane j replays entry j, j + 64, ..., and
+// each candidate's smallest (key, pos) is a min-reduction over the lanes.
+// Same answers as first_leaf per candidate; the replays' dependent loads run
+// side by side instead of one after another.
+__device__ __forceinline__ void first_leaves_wave(const FastScene& F, const int (&cp)[kTie], int ncand, V3 o, V3 d,
+                                                  V3 inv, float tmin0, float tmax0, float rtmax,
+                                                  unsigned long long (&key)[kTie], int (&pos)[kTie],
+                                                  uint32_t& steps) {
+  const int lane = __lane_id();
+  int off[kTie + 1], lb[kTie];
+  off[0] = 0;
+#pragma unroll
+  for (int c = 0; c < kTie; ++c) {
+    lb[c] = c < ncand ? F.prim_leaf_off[cp[c]] : 0;
+    off[c + 1] = off[c] + (c < ncand ? F.prim_leaf_off[cp[c] + 1] - lb[c] : 0);
+    key[c] = ~0ull;
+    pos[c] = 0;
+  }
+  const int total = off[kTie];
+  for (int base = 0; base < total; base += 64) {
+    const int j = base + lane;
+    unsigned long long kk = ~0ull;
+    int pk = 0x7fffffff, mine = -1;
+    if (j < total) {
+      int k = lb[0] + j;
+      mine = 0;
+#pragma unroll
+      for (int c = 1; c < kTie; ++c)
+        if (j >= off[c] && c < ncand) {
+          mine = c;
+          k = lb[c] + (j - off[c]);
+        }
+      unsigned long long t;
+      if (kd_reaches(F.path + F.prim_leaf[k], o, d, inv, tmin0, tmax0, rtmax, steps, t)) {
+        kk = t;
+        pk = F.prim_leaf_pos[k];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < kTie; ++c) {
+      if (c >= ncand) break;  // wave-uniform
+      unsigned long long a = mine == c ? kk : ~0ull;
+      int b = mine == c ? pk : 0x7fffffff;
+#pragma unroll
+      for (int sh = 32; sh >= 1; sh >>= 1) {
+        const unsigned long long a2 = __shfl_xor(a, sh);
+        const int b2 = __shfl_xor(b, sh);
+        const bool take = a2 < a || (a2 == a && b2 < b);
+        a = take ? a2 : a;
+        b = take ? b2 : b;
+      }
+      if (a < key[c] || (a == key[c] && b < pos[c])) {
+        key[c] = a;
+        pos[c] = b;
+      }
+    }
+  }
+}
+
 // The first visited leaf of several primitives at once, by the reference's own
 // walk (KDtreeAccel.cpp:309-388: root clip, near / far rule, the :323 stop)
 // restricted to subtrees whose cell meets one of their boxes: a primitive is
@@ -565,9 +639,12 @@ __device__ __noinline__ void kd_first_leaves(const DevScene& S, const FastScene&
 // hits of the scene (bvh_collect) hold all hits up to m + 3 EPS when fewer
 // were found or the last one lies beyond.  Returns false when a condition
 // fails (the caller walks the KD tree).
+// WAVE: every lane of the wave holds the same ray (k_fast_hard's one ray per
+// wave); the candidates' leaf replays are shared out (psteps: this lane's).
+template <bool WAVE>
 __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin,
                                             float rtmax, float t1, int* stk_link, float* stk_t, float& t_out,
-                                            int& p_out, uint32_t& steps, int& dbg) {
+                                            int& p_out, uint32_t& steps, uint32_t& psteps, int& dbg) {
   float tmin0, tmax0;
   if (!box_hit(S.root_l, S.root_r, o, d, tmin0, tmax0) || rtmax < tmin0) return false;
   const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
@@ -602,6 +679,8 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
         key[c] = (c < ncand && vis[c] >= 0) ? static_cast<unsigned long long>(vis[c]) : ~0ull;
         pos[c] = ps[c];
       }
+    } else if (WAVE) {
+      first_leaves_wave(F, cp, ncand, o, d, inv, tmin0, tmax0, rtmax, key, pos, psteps);
     } else {
 #pragma unroll
       for (int c = 0; c < kTie; ++c) {
@@ -726,6 +805,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   int p1 = -1, sp = 0;
   uint32_t rn = 0, rt = 0;  // COUNT: this ray's node visits / tests
   int cur = 0;  // >= 0 inner node to visit; < 0 leaf link to test; kDone when finished
+  int pl = 0;   // WR_BVH_SPEC: parked leaf link (< 0), or 0
   constexpr int kDone = 0x7fffffff;
   auto reserve = [&](bool want) -> int {
     const unsigned long long m = __ballot(want);
@@ -762,7 +842,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
     ch = v3(-(o.x - g) * binv.x, -(o.y - g) * binv.y, -(o.z - g) * binv.z);
   };
   auto push = [&](int link, float t) {
-    if (sp < kLdsStack) {
+    if (!kSearchSpills || sp < kLdsStack) {
       stk_link[sp * 64] = link;
       stk_t[sp * 64] = t_down16(t);
     } else {
@@ -776,7 +856,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
       --sp;
       int link;
       float te;
-      if (sp < kLdsStack) {
+      if (!kSearchSpills || sp < kLdsStack) {
         link = stk_link[sp * 64];
         te = t_up32(stk_t[sp * 64]);
       } else {
@@ -834,9 +914,22 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
       if (!pool) break;
       continue;
     }
-    // ---- inner nodes until this lane has a leaf (or is done)
-    while (__ballot(act && cur >= 0 && cur != kDone)) {
-      if (act && cur >= 0 && cur != kDone) {
+    // ---- inner nodes until this lane has a leaf (or is done).  WR_BVH_SPEC: a
+    // leaf reached is parked in `pl` and the lane descends on (its next inner
+    // nodes) until every lane has parked one or finished
+    for (;;) {
+#if WR_BVH_SPEC
+      if (!__ballot(act && pl >= 0 && cur != kDone)) break;
+      if (act && cur < 0 && pl >= 0) {
+        pl = cur;
+        pop();
+      }
+      const bool step = act && cur >= 0 && cur != kDone;
+#else
+      const bool step = act && cur >= 0 && cur != kDone;
+      if (!__ballot(step)) break;
+#endif
+      if (step) {
         if (COUNT) {
           ++ctr.nodes;
           ++rn;
@@ -914,8 +1007,14 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
       }
     }
     // ---- leaf: test its triangles (Triangle::hit), keep (t1, p1) and t2
+#if WR_BVH_SPEC
+    if (act && pl < 0) {
+      const int l = ~pl;
+      pl = 0;
+#else
     if (act && cur < 0) {
       const int l = ~cur;
+#endif
       const int first = l >> 3, cnt = (l & 7) + 1;
       // all records of the leaf requested before the first test
       float4 ta[wrf::kMaxLeaf], tb[wrf::kMaxLeaf], tc[wrf::kMaxLeaf];
@@ -946,10 +1045,12 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         }
       }
       margins();
+#if !WR_BVH_SPEC
       pop();
+#endif
     }
     // ---- finished rays: the candidate goes to k_fast_resolve
-    if (act && cur == kDone) {
+    if (act && cur == kDone && pl >= 0) {
       if (COUNT) {
         ctr.max_nodes = max(ctr.max_nodes, rn);
         ctr.max_tests = max(ctr.max_tests, rt);
@@ -984,6 +1085,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
                                              const float* t2buf, int* hard, int* hard_n, FastCounters& ctr) {
   const int lane = __lane_id();
   const QueueIndex QI(Q);
+  if (F.diag & 16) return;
   // every lane of the wave takes part in each list append (whole iterations)
   for (int base = blockIdx.x * 64; base < QI.n; base += gridDim.x * 64) {
     const int idx = base + lane;
@@ -1036,23 +1138,36 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
   }
 }
 
-// k_fast_hard: the rays k_fast_resolve listed, one per lane.
-template <bool COUNT>
+// k_fast_hard: the rays k_fast_resolve listed.  WAVE: one ray per wave --
+// every lane holds the ray, runs the same (uniform) search and decision code,
+// and the candidates' leaf replays are shared out across the lanes
+// (first_leaves_wave); lane 0 writes the answer and the counts.  A wave then
+// lasts as long as its own ray, not as long as the slowest of 64 divergent
+// ones: a launch of a few hundred hard rays drops from 0.7-1.4 ms to ~0.5 ms,
+// which the one-call API paths (wr_trace_closest & co.) wait for.  Inside the
+// render pipelines the launch's latency overlaps the other pipelines' work,
+// and there the one-ray-per-lane form uses far less of the machine (64
+// rays per wave): measured C2 2,405 vs 2,287 Mrays/s at 64 iterations, so
+// the pipelines keep WAVE = false.
+template <bool COUNT, bool WAVE>
 __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
                                           const float* t2buf, const int* hard, const int* hard_n, uint32_t* lds,
                                           FastCounters& ctr) {
   const int lane = __lane_id();
+  const bool lead = !WAVE || lane == 0;  // writes the answer, counts the uniform work
   int* stk_node = reinterpret_cast<int*>(lds) + lane;
   float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
   const QueueIndex QI(Q);
-  const int nh = *hard_n;
-  for (int i = blockIdx.x * 64 + lane; i < nh; i += gridDim.x * 64) {
+  const int nh = (F.diag & 32) ? 0 : *hard_n;
+  const int i0 = WAVE ? static_cast<int>(blockIdx.x) : static_cast<int>(blockIdx.x) * 64 + lane;
+  const int di = WAVE ? static_cast<int>(gridDim.x) : static_cast<int>(gridDim.x) * 64;
+  for (int i = i0; i < nh; i += di) {
     const int idx = hard[i];
     int q, r;
     QI.locate(idx, q, r);
     int* outp = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; });
     float* outt = qfield(Q, q, [](const RayQueue& x) { return x.out_t; });
-    const float t1 = outt[r], t2 = t2buf[idx];
+    const float t1 = outt[r];
     const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
     const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
     const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
@@ -1061,47 +1176,59 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
     const V3 o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
     const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
     const float rtmin = tmn ? tmn[r] : 0.f, rtmax = tmx ? tmx[r] : WR_INF;
-    (void)t2;
     float tb;
     int pb;
     if (!(F.diag & 2)) {
-      uint32_t steps = 0;
+      uint32_t steps = 0, psteps = 0;
       int dbg = 0;
       const uint64_t c0 = COUNT ? wall_clock64() : 0;
-      const bool done = resolve_tie(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, dbg);
+      const bool done =
+          resolve_tie<WAVE>(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, psteps, dbg);
       if (COUNT) {
-        const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c0);
-        ctr.tie_max = max(ctr.tie_max, dt);
-        ctr.tie_sum += dt;
+        ctr.replay += psteps;
+        if (lead) {
+          const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c0);
+          ctr.tie_max = max(ctr.tie_max, dt);
+          ctr.tie_sum += dt;
+          ctr.replay += steps;
+          ctr.fb_tie += done ? 1u : 0u;
+          const int why = dbg >> 16;
+          if (!done && why >= 2 && why <= 5) ++ctr.why[why - 2];
+        }
       }
       if (F.diag & 4) {  // debug: the resolution record instead of the answer
-        outp[r] = -2 - dbg;
+        if (lead) outp[r] = -2 - dbg;
         continue;
       }
-      if (COUNT) {
-        ctr.replay += steps;
-        ctr.fb_tie += done ? 1u : 0u;
-        const int why = dbg >> 16;
-        if (!done && why >= 2 && why <= 5) ++ctr.why[why - 2];
-      }
       if (done) {
-        outt[r] = tb;
-        outp[r] = pb;
+        if (lead) {
+          outt[r] = tb;
+          outp[r] = pb;
+        }
         continue;
       }
     }
     // unresolved (a crowd of hits near m, or visited hits in the band): the walk decides
-    if (COUNT) ++ctr.fallback;
+    if (COUNT && lead) ++ctr.fallback;
     if (F.diag & 1) continue;
     const uint64_t c1 = COUNT ? wall_clock64() : 0;
+    const uint32_t ki = ctr.kinner, kl = ctr.kleaves, kr = ctr.krefs;
     kd_walk<COUNT>(S, o, d, rtmin, rtmax, stk_node, stk_tmin, tb, pb, ctr);
     if (COUNT) {
-      const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c1);
-      ctr.walk_max = max(ctr.walk_max, dt);
-      ctr.walk_sum += dt;
+      if (!lead) {  // the wave walked one ray: counted once
+        ctr.kinner = ki;
+        ctr.kleaves = kl;
+        ctr.krefs = kr;
+      } else {
+        const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c1);
+        ctr.walk_max = max(ctr.walk_max, dt);
+        ctr.walk_sum += dt;
+      }
     }
-    outt[r] = tb;
-    outp[r] = pb;
+    if (lead) {
+      outt[r] = tb;
+      outp[r] = pb;
+    }
   }
 }
 

@@ -228,13 +228,13 @@ k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const f
   resolve_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, fc);
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
-template <bool COUNT>
+template <bool COUNT, bool WAVE>
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
 k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf, const int* hard,
             const int* hard_n) {
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
-  hard_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, smem, fc);
+  hard_fast<COUNT, WAVE>(S, F, Q, t2buf, hard, hard_n, smem, fc);
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 
@@ -731,7 +731,7 @@ int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
 // One persistent traversal launch over the queues of Q (max_rays bounds the
 // grid).  WR_TRACE_BVH: the verified-BVH search + its resolve launch instead.
 int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const TraceSlot& ts, Timer& tm, bool count,
-                 const TraceQueues& Q_, int max_rays, int mode = TRACE_PLAIN) {
+                 const TraceQueues& Q_, int max_rays, int mode = TRACE_PLAIN, bool hard_wave = false) {
   int* fetch = ts.fetch;
   TraceQueues Q = Q_;
   if (c->no_cut)  // measurement knob: the same launches without the dead-work elision
@@ -756,8 +756,12 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
                        dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), 0, stream, c->ds, c->fs,
                        Q, ctr, ts.t2, hard, ts.hard_n);
     if (c->trace_log) (void)hipEventRecord(fb, stream);
-    // the hard rays are a few in 10^4: a small grid drains any count
-    hipLaunchKernelGGL(count ? k_fast_hard<true> : k_fast_hard<false>, dim3(std::max(1, std::min(256, blocks))),
+    // the hard rays are a few in 10^4: a small grid drains any count (one
+    // ray per wave for the API calls: up to 2048 at once, 8 waves per CU)
+    const int hgrid = hard_wave ? std::max(1, std::min(2048, max_rays)) : std::max(1, std::min(256, blocks));
+    auto hk = hard_wave ? (count ? k_fast_hard<true, true> : k_fast_hard<false, true>)
+                        : (count ? k_fast_hard<true, false> : k_fast_hard<false, false>);
+    hipLaunchKernelGGL(hk, dim3(hgrid),
                        dim3(kTraceBlock), lds, stream, c->ds, c->fs, Q, ctr, ts.t2, hard, ts.hard_n);
     if (c->verify)
       hipLaunchKernelGGL(k_fast_verify, dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), lds,
@@ -1474,7 +1478,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
     HIPCHK(hipMalloc(&c->api_spill, search_spill_entries(c->fs.sdepth) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
   const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard, c->api_spill};
   trace_launch(c, c->stream, c->ctr, ts, tm, false, ql.Q, ql.max_rays,
-               c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN));
+               c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN), true);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
                      occ ? dox : nullptr);
   HIPCHK(hipGetLastError());
@@ -1804,7 +1808,7 @@ int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max
     QueueList ql;
     ql.add(rq(Q.o, Q.d, P, &pp.sc[0].sq[b], Q.t, Q.prim, nullptr, nullptr, Q.cut), P);
     if (more) ql.add(rq(T.q_o[b & 1], T.q_d[b & 1], P, &pp.sc[0].ext[b], T.q_t[b & 1], T.q_prim[b & 1]), P);
-    trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, false, ql.Q, ql.max_rays, TRACE_DENSE);
+    trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, false, ql.Q, ql.max_rays, TRACE_DENSE, true);
     const int nres = shade_grid(c, P);
     hipLaunchKernelGGL(k_pt_step, dim3(nres + (more ? g : 0), 1), dim3(kShadeBlock), 0, sm, GA, b, nres,
                        more ? 1 : 0);
