@@ -224,34 +224,51 @@ __device__ __forceinline__ bool box_crossed_with_margin(float lx, float ly, floa
 }
 
 // Is the primitive whose KD leaves are prim_leaf[lb, lb + ln) tested by the
-// reference's traversal of this ray?
-__device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F, int lb, int ln, V3 o, V3 d,
-                                          float rtmax, float t_hit, uint32_t& steps) {
+// reference's traversal of this ray?  kMember / kNotMember, or kScan: a
+// many-leaf primitive whose located leaf proves nothing, left to the scan
+// waves of k_fast_hard.  WR_RESOLVE_SCAN=1: such primitives are scanned here,
+// by the lane (one leaf after another).
+#ifndef WR_RESOLVE_SCAN
+#define WR_RESOLVE_SCAN 0
+#endif
+constexpr int kNotMember = 0, kMember = 1, kScan = 2;
+__device__ __forceinline__ int kd_member(const DevScene& S, const FastScene& F, int lb, int ln, V3 o, V3 d,
+                                         float rtmax, float t_hit, uint32_t& steps) {
   float tmin, tmax;
-  if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) return false;  // :312-313, :323
+  if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) return kNotMember;  // :312-313, :323
   const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
   const V3 binv = v3(clamp_inv(d.x), clamp_inv(d.y), clamp_inv(d.z));
   const V3 p = o + d * t_hit;
   unsigned long long key;
   if (ln > 4) {
     // a big primitive (walls: hundreds of leaves): the leaf holding a point
-    // just before the hit (a hit on a wall lies on a split plane), found by
+    // just before the hit, else just after it (a hit on a wall lies on a split
+    // plane, and the wall is in the leaves on one side of it only), found by
     // descent, then by binary search in the (ascending) list
-    const int want = kd_locate(S, F, o + d * (t_hit * 0.99999f - 1e-4f));
-    int a = lb, b = lb + ln;
-    while (a < b) {
-      const int mid = (a + b) >> 1;
-      if (F.prim_leaf[mid] < want) a = mid + 1;
-      else b = mid;
-    }
-    if (a < lb + ln && F.prim_leaf[a] == want) {
-      const uint2* rec = F.path + want;
-      const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
-      const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
-      if (cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return true;
-      if (kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return true;
+    for (int side = 0; side < 2; ++side) {
+      const float tp = side == 0 ? t_hit * 0.99999f - 1e-4f : t_hit * 1.00001f + 1e-4f;
+      const int want = kd_locate(S, F, o + d * tp);
+      int a = lb, b = lb + ln;
+      while (a < b) {
+        const int mid = (a + b) >> 1;
+        if (F.prim_leaf[mid] < want) a = mid + 1;
+        else b = mid;
+      }
+      if (a < lb + ln && F.prim_leaf[a] == want) {
+        const uint2* rec = F.path + want;
+        const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
+        const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
+        if (cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return kMember;
+        if (kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return kMember;
+      }
     }
   }
+#if !WR_RESOLVE_SCAN
+  // a many-leaf primitive whose located leaf proved nothing: its whole leaf
+  // list is scanned by one wave per ray in k_fast_hard (scan_fast) instead of
+  // by this lane, which would hold the resolve wave for up to ~1 ms
+  if (ln > 4) return kScan;
+#endif
   if (ln >= 1 && ln <= 4) {
     // witnesses first, all of the primitive's leaves at once: the list
     // entries, then the cells, each set of loads in flight together
@@ -268,7 +285,7 @@ __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F,
     bool seen = false;
 #pragma unroll
     for (int k = 0; k < 4; ++k) seen |= k < ln && cell_crossed_with_margin(h0[k], h1[k], o, d, binv, rtmax);
-    if (seen) return true;
+    if (seen) return kMember;
   }
   // replays: the leaves whose cell holds the hit point first (usually the one
   // reached), then the others
@@ -279,11 +296,11 @@ __device__ __forceinline__ bool kd_member(const DevScene& S, const FastScene& F,
       const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
       const bool in = p.x >= __uint_as_float(h0.z) && p.y >= __uint_as_float(h0.w) && p.z >= __uint_as_float(h1.x) &&
                       p.x <= __uint_as_float(h1.y) && p.y <= __uint_as_float(h1.z) && p.z <= __uint_as_float(h1.w);
-      if (pass == 0 && ln > 4 && cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return true;
-      if (in == (pass == 0) && kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return true;
+      if (pass == 0 && ln > 4 && cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return kMember;
+      if (in == (pass == 0) && kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return kMember;
     }
   }
-  return false;
+  return kNotMember;
 }
 
 // KDtreeAccel::traverse (KDtreeAccel.cpp:309-388) for one ray on one lane:
@@ -1082,14 +1099,15 @@ __device__ __forceinline__ int fast_append(int* counter, bool want) {
 // kernel's occupancy.
 template <bool COUNT>
 __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
-                                             const float* t2buf, int* hard, int* hard_n, FastCounters& ctr) {
+                                             const float* t2buf, int* hard, int* hard_n, int hcap,
+                                             FastCounters& ctr) {
   const int lane = __lane_id();
   const QueueIndex QI(Q);
   if (F.diag & 16) return;
   // every lane of the wave takes part in each list append (whole iterations)
   for (int base = blockIdx.x * 64; base < QI.n; base += gridDim.x * 64) {
     const int idx = base + lane;
-    bool need = false;
+    bool need = false, scan = false;
     if (idx < QI.n) {
       int q, r;
       QI.locate(idx, q, r);
@@ -1121,7 +1139,9 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
             uint32_t steps = 0;
             const uint64_t t0 = COUNT ? wall_clock64() : 0;
             const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
-            need = !kd_member(S, F, lb, ln, o, d, rtmax, t1, steps);
+            const int m = kd_member(S, F, lb, ln, o, d, rtmax, t1, steps);
+            need = m == kNotMember;
+            scan = m == kScan;
             if (COUNT) {
               ctr.replay += steps;
               const uint32_t dt = static_cast<uint32_t>(wall_clock64() - t0);
@@ -1135,6 +1155,9 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
     }
     const int slot = fast_append(hard_n, need);
     if (need) hard[slot] = idx;
+    // the scan list fills the same array from the top (a ray is in one list)
+    const int sslot = fast_append(hard_n + 1, scan);
+    if (scan) hard[hcap - 1 - sslot] = idx;
   }
 }
 
@@ -1149,86 +1172,156 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
 // and there the one-ray-per-lane form uses far less of the machine (64
 // rays per wave): measured C2 2,405 vs 2,287 Mrays/s at 64 iterations, so
 // the pipelines keep WAVE = false.
+// One listed ray's general resolution: the reference's rule over the visited
+// hits near the smallest (resolve_tie), or failing that its KD walk.
+template <bool COUNT, bool WAVE>
+__device__ __forceinline__ void settle_ray(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin, float rtmax,
+                                           float t1, int* stk_node, float* stk_tmin, float* outt, int* outp, int r,
+                                           bool lead, FastCounters& ctr) {
+  float tb;
+  int pb;
+  if (!(F.diag & 2)) {
+    uint32_t steps = 0, psteps = 0;
+    int dbg = 0;
+    const uint64_t c0 = COUNT ? wall_clock64() : 0;
+    const bool done = resolve_tie<WAVE>(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, psteps, dbg);
+    if (COUNT) {
+      ctr.replay += psteps;
+      if (lead) {
+        const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c0);
+        ctr.tie_max = max(ctr.tie_max, dt);
+        ctr.tie_sum += dt;
+        ctr.replay += steps;
+        ctr.fb_tie += done ? 1u : 0u;
+        const int why = dbg >> 16;
+        if (!done && why >= 2 && why <= 5) ++ctr.why[why - 2];
+      }
+    }
+    if (F.diag & 4) {  // debug: the resolution record instead of the answer
+      if (lead) outp[r] = -2 - dbg;
+      return;
+    }
+    if (done) {
+      if (lead) {
+        outt[r] = tb;
+        outp[r] = pb;
+      }
+      return;
+    }
+  }
+  // unresolved (a crowd of hits near m, or visited hits in the band): the walk decides
+  if (COUNT && lead) ++ctr.fallback;
+  if (F.diag & 1) return;
+  const uint64_t c1 = COUNT ? wall_clock64() : 0;
+  const uint32_t ki = ctr.kinner, kl = ctr.kleaves, kr = ctr.krefs;
+  kd_walk<COUNT>(S, o, d, rtmin, rtmax, stk_node, stk_tmin, tb, pb, ctr);
+  if (COUNT) {
+    if (!lead) {  // the wave walked one ray: counted once
+      ctr.kinner = ki;
+      ctr.kleaves = kl;
+      ctr.krefs = kr;
+    } else {
+      const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c1);
+      ctr.walk_max = max(ctr.walk_max, dt);
+      ctr.walk_sum += dt;
+    }
+  }
+  if (lead) {
+    outt[r] = tb;
+    outp[r] = pb;
+  }
+}
+
+struct ListedRay {
+  V3 o, d;
+  float rtmin, rtmax, t1;
+  int p1, r;
+  float* outt;
+  int* outp;
+};
+__device__ __forceinline__ ListedRay listed_ray(const TraceQueues& Q, const QueueIndex& QI, int idx) {
+  ListedRay L;
+  int q;
+  QI.locate(idx, q, L.r);
+  const int r = L.r;
+  L.outp = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; });
+  L.outt = qfield(Q, q, [](const RayQueue& x) { return x.out_t; });
+  L.t1 = L.outt[r];
+  L.p1 = L.outp[r];
+  const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
+  const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
+  const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
+  const float* tmn = qfield(Q, q, [](const RayQueue& x) { return x.tmin; });
+  const float* tmx = qfield(Q, q, [](const RayQueue& x) { return x.tmax; });
+  L.o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
+  L.d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+  L.rtmin = tmn ? tmn[r] : 0.f;
+  L.rtmax = tmx ? tmx[r] : WR_INF;
+  return L;
+}
+
 template <bool COUNT, bool WAVE>
 __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
-                                          const float* t2buf, const int* hard, const int* hard_n, uint32_t* lds,
+                                          const int* hard, const int* hard_n, int bid, int nb, uint32_t* lds,
                                           FastCounters& ctr) {
   const int lane = __lane_id();
   const bool lead = !WAVE || lane == 0;  // writes the answer, counts the uniform work
   int* stk_node = reinterpret_cast<int*>(lds) + lane;
   float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
   const QueueIndex QI(Q);
-  const int nh = (F.diag & 32) ? 0 : *hard_n;
-  const int i0 = WAVE ? static_cast<int>(blockIdx.x) : static_cast<int>(blockIdx.x) * 64 + lane;
-  const int di = WAVE ? static_cast<int>(gridDim.x) : static_cast<int>(gridDim.x) * 64;
+  const int nh = (F.diag & 32) ? 0 : hard_n[0];
+  const int i0 = WAVE ? bid : bid * 64 + lane;
+  const int di = WAVE ? nb : nb * 64;
   for (int i = i0; i < nh; i += di) {
-    const int idx = hard[i];
-    int q, r;
-    QI.locate(idx, q, r);
-    int* outp = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; });
-    float* outt = qfield(Q, q, [](const RayQueue& x) { return x.out_t; });
-    const float t1 = outt[r];
-    const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
-    const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
-    const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
-    const float* tmn = qfield(Q, q, [](const RayQueue& x) { return x.tmin; });
-    const float* tmx = qfield(Q, q, [](const RayQueue& x) { return x.tmax; });
-    const V3 o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
-    const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
-    const float rtmin = tmn ? tmn[r] : 0.f, rtmax = tmx ? tmx[r] : WR_INF;
-    float tb;
-    int pb;
-    if (!(F.diag & 2)) {
-      uint32_t steps = 0, psteps = 0;
-      int dbg = 0;
-      const uint64_t c0 = COUNT ? wall_clock64() : 0;
-      const bool done =
-          resolve_tie<WAVE>(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, psteps, dbg);
-      if (COUNT) {
-        ctr.replay += psteps;
-        if (lead) {
-          const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c0);
-          ctr.tie_max = max(ctr.tie_max, dt);
-          ctr.tie_sum += dt;
-          ctr.replay += steps;
-          ctr.fb_tie += done ? 1u : 0u;
-          const int why = dbg >> 16;
-          if (!done && why >= 2 && why <= 5) ++ctr.why[why - 2];
+    const ListedRay L = listed_ray(Q, QI, hard[i]);
+    settle_ray<COUNT, WAVE>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r, lead, ctr);
+  }
+}
+
+// The scan list (k_fast_resolve's kScan rays, at the top of the list array):
+// one ray per wave.  The lanes share out p1's leaves -- the witness for each
+// leaf's cell, else the replay of its path -- and stop once one is reached;
+// p1 then stands.  If none is, t1's triangle is not visited and the ray is
+// settled in general by the same wave (settle_ray, one ray per wave).
+template <bool COUNT>
+__device__ __forceinline__ void scan_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
+                                          const int* hard, const int* hard_n, int hcap, int bid, int nb, uint32_t* lds,
+                                          FastCounters& ctr) {
+  const int lane = __lane_id();
+  int* stk_node = reinterpret_cast<int*>(lds) + lane;
+  float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
+  const QueueIndex QI(Q);
+  const int ns = (F.diag & 32) ? 0 : hard_n[1];
+  for (int i = bid; i < ns; i += nb) {
+    const ListedRay L = listed_ray(Q, QI, hard[hcap - 1 - i]);
+    bool member = false;
+    float tmin, tmax;
+    uint32_t steps = 0;
+    if (box_hit(S.root_l, S.root_r, L.o, L.d, tmin, tmax) && !(L.rtmax < tmin)) {  // :312-313, :323
+      const V3 inv = v3(1.f / L.d.x, 1.f / L.d.y, 1.f / L.d.z);
+      const V3 binv = v3(clamp_inv(L.d.x), clamp_inv(L.d.y), clamp_inv(L.d.z));
+      const int lb = F.prim_leaf_off[L.p1], ln = F.prim_leaf_off[L.p1 + 1] - lb;
+      for (int base = 0; base < ln && !member; base += 64) {  // wave-uniform
+        const int k = base + lane;
+        bool ok = false;
+        if (k < ln) {
+          const uint2* rec = F.path + F.prim_leaf[lb + k];
+          const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
+          const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
+          unsigned long long key;
+          ok = cell_crossed_with_margin(h0, h1, L.o, L.d, binv, L.rtmax) ||
+               kd_reaches(rec, L.o, L.d, inv, tmin, tmax, L.rtmax, steps, key);
         }
-      }
-      if (F.diag & 4) {  // debug: the resolution record instead of the answer
-        if (lead) outp[r] = -2 - dbg;
-        continue;
-      }
-      if (done) {
-        if (lead) {
-          outt[r] = tb;
-          outp[r] = pb;
-        }
-        continue;
+        member = __ballot(ok) != 0ull;
       }
     }
-    // unresolved (a crowd of hits near m, or visited hits in the band): the walk decides
-    if (COUNT && lead) ++ctr.fallback;
-    if (F.diag & 1) continue;
-    const uint64_t c1 = COUNT ? wall_clock64() : 0;
-    const uint32_t ki = ctr.kinner, kl = ctr.kleaves, kr = ctr.krefs;
-    kd_walk<COUNT>(S, o, d, rtmin, rtmax, stk_node, stk_tmin, tb, pb, ctr);
     if (COUNT) {
-      if (!lead) {  // the wave walked one ray: counted once
-        ctr.kinner = ki;
-        ctr.kleaves = kl;
-        ctr.krefs = kr;
-      } else {
-        const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c1);
-        ctr.walk_max = max(ctr.walk_max, dt);
-        ctr.walk_sum += dt;
-      }
+      ctr.replay += steps;
+      ctr.scans += lane == 0 ? 1u : 0u;
     }
-    if (lead) {
-      outt[r] = tb;
-      outp[r] = pb;
-    }
+    if (member) continue;
+    settle_ray<COUNT, true>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r,
+                            lane == 0, ctr);
   }
 }
 

@@ -88,11 +88,11 @@ struct StepCounters {
   int vcm_pending;    // VCM: light paths whose first vertex is an emitter (k_vcm_fixup)
   int vcm_nverts;     // VCM: light vertices in the merge grid
   int mq[kSlots];     // VCM: merge queries queued at step `slot`
-  int hard[kSlots];   // WR_TRACE_BVH: rays of step `slot` left to k_fast_hard
+  int hard[kSlots][2];  // WR_TRACE_BVH: rays of step `slot` left to k_fast_hard (tie list, scan list)
 };
 struct DevCounters {
   int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
-  int hard;   // API path: rays left to k_fast_hard
+  int hard[2];  // API path: rays left to k_fast_hard (tie list, scan list)
   unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
   unsigned long long closest, shadow, inner, leaves, refs, tests;
   unsigned long long vm_queries, vm_found, vm_merged;  // VCM range queries / vertices in radius / merges
@@ -223,18 +223,24 @@ k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetc
 }
 template <bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
-k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf, int* hard, int* hard_n) {
+k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf, int* hard, int* hard_n,
+               int hcap) {
   FastCounters fc{};
-  resolve_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, fc);
+  resolve_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, hcap, fc);
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 template <bool COUNT, bool WAVE>
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
-k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf, const int* hard,
-            const int* hard_n) {
+k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const int* hard, const int* hard_n, int hcap,
+            int hard_blocks) {
+  // blocks [0, hard_blocks): the tie list; the rest: the scan list, one ray per wave
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
-  hard_fast<COUNT, WAVE>(S, F, Q, t2buf, hard, hard_n, smem, fc);
+  const int b = static_cast<int>(blockIdx.x);
+  if (b < hard_blocks)
+    hard_fast<COUNT, WAVE>(S, F, Q, hard, hard_n, b, hard_blocks, smem, fc);
+  else
+    scan_fast<COUNT>(S, F, Q, hard, hard_n, hcap, b - hard_blocks, static_cast<int>(gridDim.x) - hard_blocks, smem, fc);
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 
@@ -706,13 +712,13 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, int
 // WR_TRACE_BVH mode the per-ray t2 scratch of the BVH search (>= the launch's rays).
 struct TraceSlot {
   int* fetch;
-  float* t2;      // [t2_cap] t2 per launch index, then [t2_cap] the hard-ray list
+  float* t2;      // [t2_cap] t2 per launch index, then [t2_cap] the tie list (from the bottom) and the scan list (from the top)
   size_t t2_cap;
   int* hard_n;
   int2* spill;    // the search stack's spill area
 };
 TraceSlot tslot(Pipe& p, int slot) {
-  return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap, &p.sc[0].hard[slot], p.spill};
+  return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap, &p.sc[0].hard[slot][0], p.spill};
 }
 // t2 scratch + hard-ray list of a pipeline for launches of up to `rays` rays
 int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
@@ -754,15 +760,17 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     int* hard = reinterpret_cast<int*>(ts.t2 + ts.t2_cap);
     hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
                        dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), 0, stream, c->ds, c->fs,
-                       Q, ctr, ts.t2, hard, ts.hard_n);
+                       Q, ctr, ts.t2, hard, ts.hard_n, static_cast<int>(ts.t2_cap));
     if (c->trace_log) (void)hipEventRecord(fb, stream);
     // the hard rays are a few in 10^4: a small grid drains any count (one
     // ray per wave for the API calls: up to 2048 at once, 8 waves per CU)
     const int hgrid = hard_wave ? std::max(1, std::min(2048, max_rays)) : std::max(1, std::min(256, blocks));
+    const int sgrid = std::max(1, std::min(256, max_rays));  // scan waves
     auto hk = hard_wave ? (count ? k_fast_hard<true, true> : k_fast_hard<false, true>)
                         : (count ? k_fast_hard<true, false> : k_fast_hard<false, false>);
-    hipLaunchKernelGGL(hk, dim3(hgrid),
-                       dim3(kTraceBlock), lds, stream, c->ds, c->fs, Q, ctr, ts.t2, hard, ts.hard_n);
+    hipLaunchKernelGGL(hk, dim3(hgrid + sgrid),
+                       dim3(kTraceBlock), lds, stream, c->ds, c->fs, Q, ctr, hard, ts.hard_n,
+                       static_cast<int>(ts.t2_cap), hgrid);
     if (c->verify)
       hipLaunchKernelGGL(k_fast_verify, dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), lds,
                          stream, c->ds, c->fs, Q, ctr);
@@ -777,13 +785,14 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
         tot += k;
       }
       float ms = 0.f, ma = 0.f, mb = 0.f;
-      int nh = 0;
-      (void)hipMemcpy(&nh, ts.hard_n, sizeof(int), hipMemcpyDeviceToHost);
+      int nhs[2] = {0, 0};
+      (void)hipMemcpy(nhs, ts.hard_n, 2 * sizeof(int), hipMemcpyDeviceToHost);
+      const int nh = nhs[0], ns = nhs[1];
       (void)hipEventElapsedTime(&ms, f0, f1);
       (void)hipEventElapsedTime(&ma, f0, fa);
       (void)hipEventElapsedTime(&mb, fa, fb);
-      std::fprintf(stderr, "[wr bvh] %d rays  %.1f us (search %.1f, resolve %.1f, hard %.1f: %d rays)  grid %d\n", tot,
-                   ms * 1e3f, ma * 1e3f, mb * 1e3f, (ms - ma - mb) * 1e3f, nh, fgrid);
+      std::fprintf(stderr, "[wr bvh] %d rays  %.1f us (search %.1f, resolve %.1f, hard %.1f: %d + %d scan rays)  grid %d\n",
+                   tot, ms * 1e3f, ma * 1e3f, mb * 1e3f, (ms - ma - mb) * 1e3f, nh, ns, fgrid);
       (void)hipEventDestroy(f0);
       (void)hipEventDestroy(f1);
       (void)hipEventDestroy(fa);
@@ -1476,7 +1485,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
   if (c->fast_on && !c->api_spill && search_spill_entries(c->fs.sdepth) > 0)
     HIPCHK(hipMalloc(&c->api_spill, search_spill_entries(c->fs.sdepth) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
-  const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard, c->api_spill};
+  const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard[0], c->api_spill};
   trace_launch(c, c->stream, c->ctr, ts, tm, false, ql.Q, ql.max_rays,
                c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN), true);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
