@@ -200,6 +200,16 @@ int main(int argc, char** argv) {
   std::printf("OK prims %zu nodes %zu leaves %zu depth %d refs %zu leaf sizes", np, f.nodes.size(), leaves, f.depth,
               f.prim_leaf.size());
   for (int k = 1; k <= wrf::kMaxLeaf; ++k) std::printf(" %d:%zu", k, leaf_hist[k]);
+  // KD leaves per primitive (the membership / tie resolution's list lengths)
+  size_t big16 = 0, big256 = 0;
+  int maxln = 0;
+  for (size_t p = 0; p < np; ++p) {
+    const int ln = f.prim_leaf_off[p + 1] - f.prim_leaf_off[p];
+    maxln = std::max(maxln, ln);
+    big16 += ln > 16;
+    big256 += ln > 256;
+  }
+  std::printf(" kd leaves per prim: max %d, >16: %zu, >256: %zu", maxln, big16, big256);
   std::printf("\n");
   return 0;
 }

@@ -387,6 +387,7 @@ __device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtm
 // the number of hits <= cap found (> kTie: more exist beyond ct[kTie - 1]).
 constexpr int kTie = 8;
 constexpr int kTieLeaves = 16;  // resolve_tie: replay up to this many KD leaves per candidate, else a pruned walk
+constexpr int kTieWaveLeaves = 8192;  // ... or, one ray per wave, up to this many leaves of all candidates
 __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float rtmin, float rtmax, float cap,
                                            int* stk_link, float* stk_t, float (&ct)[kTie], int (&cp)[kTie]) {
   rtmax = fminf(rtmax, cap);
@@ -683,7 +684,15 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
     // pruned to the candidates' boxes finds them all (keys = visit numbers);
     // otherwise each candidate's leaves are replayed (keys = far-child bits)
     bool big = false;
-    for (int c = 0; c < ncand; ++c) big |= F.prim_leaf_off[cp[c] + 1] - F.prim_leaf_off[cp[c]] > kTieLeaves;
+    int total = 0;
+    for (int c = 0; c < ncand; ++c) {
+      const int ln = F.prim_leaf_off[cp[c] + 1] - F.prim_leaf_off[cp[c]];
+      big |= ln > kTieLeaves;
+      total += ln;
+    }
+    // one ray per wave: the lanes replay every leaf of the candidates side by
+    // side (up to kTieWaveLeaves of them, 128 rounds) instead of the walk
+    if (WAVE && total <= kTieWaveLeaves) big = false;
     if (big) {
       int vis[kTie], ps[kTie];
       for (int c = 0; c < kTie; ++c) {
@@ -1107,7 +1116,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
   // every lane of the wave takes part in each list append (whole iterations)
   for (int base = blockIdx.x * 64; base < QI.n; base += gridDim.x * 64) {
     const int idx = base + lane;
-    bool need = false, scan = false;
+    bool need = false, scan = false, big_tie = false;
     if (idx < QI.n) {
       int q, r;
       QI.locate(idx, q, r);
@@ -1127,7 +1136,13 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
       if (p1 >= 0) {  // (no hit anywhere: a miss for the reference too)
         const bool tie = !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0);
         if (tie) {
-          need = true;
+          // a tie on a many-leaf primitive (walls, floors: up to thousands of
+          // leaves) is resolved by one wave (scan list, marked), the others
+          // one per lane
+          const bool big = F.prim_leaf_off[p1 + 1] - F.prim_leaf_off[p1] > kTieLeaves;
+          need = !big;
+          scan = big;
+          big_tie = big;
         } else if (!(F.diag & 8)) {
           const V3 binv = v3(clamp_inv(d.x), clamp_inv(d.y), clamp_inv(d.z));
           const bool seen = box_crossed_with_margin(c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, o, d, binv, rtmax) ||
@@ -1157,7 +1172,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
     if (need) hard[slot] = idx;
     // the scan list fills the same array from the top (a ray is in one list)
     const int sslot = fast_append(hard_n + 1, scan);
-    if (scan) hard[hcap - 1 - sslot] = idx;
+    if (scan) hard[hcap - 1 - sslot] = big_tie ? ~idx : idx;
   }
 }
 
@@ -1278,8 +1293,8 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
   }
 }
 
-// The scan list (k_fast_resolve's kScan rays, at the top of the list array):
-// one ray per wave.  The lanes share out p1's leaves -- the witness for each
+// The scan list (k_fast_resolve's kScan rays and near-ties on many-leaf
+// primitives, at the top of the list array): one ray per wave.  The lanes share out p1's leaves -- the witness for each
 // leaf's cell, else the replay of its path -- and stop once one is reached;
 // p1 then stands.  If none is, t1's triangle is not visited and the ray is
 // settled in general by the same wave (settle_ray, one ray per wave).
@@ -1293,11 +1308,13 @@ __device__ __forceinline__ void scan_fast(const DevScene& S, const FastScene& F,
   const QueueIndex QI(Q);
   const int ns = (F.diag & 32) ? 0 : hard_n[1];
   for (int i = bid; i < ns; i += nb) {
-    const ListedRay L = listed_ray(Q, QI, hard[hcap - 1 - i]);
+    const int e = hard[hcap - 1 - i];
+    const bool tie = e < 0;  // a near-tie on a many-leaf primitive: straight to the general resolution
+    const ListedRay L = listed_ray(Q, QI, tie ? ~e : e);
     bool member = false;
     float tmin, tmax;
     uint32_t steps = 0;
-    if (box_hit(S.root_l, S.root_r, L.o, L.d, tmin, tmax) && !(L.rtmax < tmin)) {  // :312-313, :323
+    if (!tie && box_hit(S.root_l, S.root_r, L.o, L.d, tmin, tmax) && !(L.rtmax < tmin)) {  // :312-313, :323
       const V3 inv = v3(1.f / L.d.x, 1.f / L.d.y, 1.f / L.d.z);
       const V3 binv = v3(clamp_inv(L.d.x), clamp_inv(L.d.y), clamp_inv(L.d.z));
       const int lb = F.prim_leaf_off[L.p1], ln = F.prim_leaf_off[L.p1 + 1] - lb;
