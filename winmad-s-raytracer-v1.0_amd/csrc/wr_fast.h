@@ -50,7 +50,8 @@ struct FastScene {
   int depth;   // stack entries of the KD walks and tie resolution (k_fast_hard, k_fast_verify)
   int sdepth;  // stack entries of the BVH search (k_trace_fast): the BVH's depth + 1
   int diag;   // WR_BVH_DIAG (measurement only): 1 = skip the KD walks, 8 = skip the replays, 16 = skip k_fast_resolve,
-              // 32 = skip k_fast_hard (all wrong answers); 2 = KD walk for every tie
+              // 32 = skip k_fast_hard, 64 its scan list, 128 its tie list (all wrong answers);
+              // 2 = KD walk for every tie
 };
 
 struct FastCounters {  // algorithmic work (count_work)
@@ -387,7 +388,10 @@ __device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtm
 // the number of hits <= cap found (> kTie: more exist beyond ct[kTie - 1]).
 constexpr int kTie = 8;
 constexpr int kTieLeaves = 16;  // resolve_tie: replay up to this many KD leaves per candidate, else a pruned walk
-constexpr int kTieWaveLeaves = 8192;  // ... or, one ray per wave, up to this many leaves of all candidates
+#ifndef WR_TIE_WAVE_ALL
+#define WR_TIE_WAVE_ALL 0  // 1: every near-tie to the one-ray-per-wave resolution
+#endif
+constexpr int kTieWaveLeaves = 65536;  // ... or, one ray per wave, up to this many leaves of all candidates (cell-filtered)
 __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float rtmin, float rtmax, float cap,
                                            int* stk_link, float* stk_t, float (&ct)[kTie], int (&cp)[kTie]) {
   rtmax = fminf(rtmax, cap);
@@ -500,16 +504,44 @@ __device__ __noinline__ void first_leaf(const FastScene& F, int p, V3 o, V3 d, V
   }
 }
 
+// Can the reference's walk reach the KD leaf whose cell is (h0.zw, h1) (the
+// header of its path record)?  False only when the ray's LINE misses the cell
+// grown by delta_a = 1e-5 x (|lo_a| + |hi_a| + 2 |o_a|) on every axis.  A leaf is
+// reached only if its walk interval [tmin, tmax] stays non-empty (each near /
+// far step of :331-357 keeps tmin <= tmax), and the interval's ends are float
+// crossings of the cell's own faces (the root box and the splits on its path),
+// each within 3 ulp of the exact crossing; missing the grown cell leaves a gap
+// between the exact crossings far wider than that.  Rays with a near-zero
+// direction component are never pruned.
+__device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3 d) {
+  if (!(fabsf(d.x) > 1e-20f && fabsf(d.y) > 1e-20f && fabsf(d.z) > 1e-20f)) return true;
+  const float lx = __uint_as_float(h0.z), ly = __uint_as_float(h0.w), lz = __uint_as_float(h1.x);
+  const float hx = __uint_as_float(h1.y), hy = __uint_as_float(h1.z), hz = __uint_as_float(h1.w);
+  const float mx = 1e-5f * (fabsf(lx) + fabsf(hx) + 2.f * fabsf(o.x)) + 1e-30f;
+  const float my = 1e-5f * (fabsf(ly) + fabsf(hy) + 2.f * fabsf(o.y)) + 1e-30f;
+  const float mz = 1e-5f * (fabsf(lz) + fabsf(hz) + 2.f * fabsf(o.z)) + 1e-30f;
+  const float ix = 1.f / d.x, iy = 1.f / d.y, iz = 1.f / d.z;
+  const float x0 = (lx - mx - o.x) * ix, x1 = (hx + mx - o.x) * ix;
+  const float y0 = (ly - my - o.y) * iy, y1 = (hy + my - o.y) * iy;
+  const float z0 = (lz - mz - o.z) * iz, z1 = (hz + mz - o.z) * iz;
+  const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+  return !(tn > tf);  // NaN: kept
+}
+
 // first_leaf for the candidates cp[0, ncand) of ONE ray, with the wave's lanes
 // sharing the work (every lane holds the same ray and list): the candidates'
-// leaf lists are laid end to end, lane j replays entry j, j + 64, ..., and
-// each candidate's smallest (key, pos) is a min-reduction over the lanes.
-// Same answers as first_leaf per candidate; the replays' dependent loads run
-// side by side instead of one after another.
+// leaf lists are laid end to end and lane j takes entries j, j + 64, ..., four
+// at a time with their loads in flight together.  A leaf whose cell the ray
+// cannot reach (cell_may_be_reached) is dropped before its path replay --
+// floors and walls sit in thousands of leaves, the ray meets a few.  Each lane
+// keeps its smallest (key, pos) per candidate; one min-reduction over the
+// lanes at the end.  Same answers as first_leaf per candidate.
 __device__ __forceinline__ void first_leaves_wave(const FastScene& F, const int (&cp)[kTie], int ncand, V3 o, V3 d,
                                                   V3 inv, float tmin0, float tmax0, float rtmax,
                                                   unsigned long long (&key)[kTie], int (&pos)[kTie],
                                                   uint32_t& steps) {
+  constexpr int U = 4;
   const int lane = __lane_id();
   int off[kTie + 1], lb[kTie];
   off[0] = 0;
@@ -518,47 +550,70 @@ __device__ __forceinline__ void first_leaves_wave(const FastScene& F, const int 
     lb[c] = c < ncand ? F.prim_leaf_off[cp[c]] : 0;
     off[c + 1] = off[c] + (c < ncand ? F.prim_leaf_off[cp[c] + 1] - lb[c] : 0);
     key[c] = ~0ull;
-    pos[c] = 0;
+    pos[c] = 0x7fffffff;
   }
   const int total = off[kTie];
-  for (int base = 0; base < total; base += 64) {
-    const int j = base + lane;
-    unsigned long long kk = ~0ull;
-    int pk = 0x7fffffff, mine = -1;
-    if (j < total) {
-      int k = lb[0] + j;
-      mine = 0;
+  for (int base = 0; base < total; base += 64 * U) {
+    int k[U], mine[U], po[U];
+    uint4 h0[U], h1[U];
 #pragma unroll
-      for (int c = 1; c < kTie; ++c)
-        if (j >= off[c] && c < ncand) {
-          mine = c;
-          k = lb[c] + (j - off[c]);
-        }
-      unsigned long long t;
-      if (kd_reaches(F.path + F.prim_leaf[k], o, d, inv, tmin0, tmax0, rtmax, steps, t)) {
-        kk = t;
-        pk = F.prim_leaf_pos[k];
+    for (int u = 0; u < U; ++u) {
+      const int j = base + u * 64 + lane;
+      mine[u] = -1;
+      k[u] = 0;
+      if (j < total) {
+        k[u] = lb[0] + j;
+        mine[u] = 0;
+#pragma unroll
+        for (int c = 1; c < kTie; ++c)
+          if (j >= off[c] && c < ncand) {
+            mine[u] = c;
+            k[u] = lb[c] + (j - off[c]);
+          }
       }
     }
 #pragma unroll
-    for (int c = 0; c < kTie; ++c) {
-      if (c >= ncand) break;  // wave-uniform
-      unsigned long long a = mine == c ? kk : ~0ull;
-      int b = mine == c ? pk : 0x7fffffff;
+    for (int u = 0; u < U; ++u) po[u] = mine[u] >= 0 ? F.prim_leaf[k[u]] : 0;
 #pragma unroll
-      for (int sh = 32; sh >= 1; sh >>= 1) {
-        const unsigned long long a2 = __shfl_xor(a, sh);
-        const int b2 = __shfl_xor(b, sh);
-        const bool take = a2 < a || (a2 == a && b2 < b);
-        a = take ? a2 : a;
-        b = take ? b2 : b;
-      }
-      if (a < key[c] || (a == key[c] && b < pos[c])) {
-        key[c] = a;
-        pos[c] = b;
+    for (int u = 0; u < U; ++u) {
+      const uint2* rec = F.path + po[u];
+      h0[u] = *reinterpret_cast<const uint4*>(rec);
+      h1[u] = *reinterpret_cast<const uint4*>(rec + 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      unsigned long long t;
+      if (mine[u] >= 0 && cell_may_be_reached(h0[u], h1[u], o, d) &&
+          kd_reaches(F.path + po[u], o, d, inv, tmin0, tmax0, rtmax, steps, t)) {
+        const int pk = F.prim_leaf_pos[k[u]];
+#pragma unroll
+        for (int c = 0; c < kTie; ++c)
+          if (mine[u] == c && (t < key[c] || (t == key[c] && pk < pos[c]))) {
+            key[c] = t;
+            pos[c] = pk;
+          }
       }
     }
   }
+#pragma unroll
+  for (int c = 0; c < kTie; ++c) {
+    if (c >= ncand) break;  // wave-uniform
+    unsigned long long a = key[c];
+    int b = pos[c];
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+      const unsigned long long a2 = __shfl_xor(a, sh);
+      const int b2 = __shfl_xor(b, sh);
+      const bool take = a2 < a || (a2 == a && b2 < b);
+      a = take ? a2 : a;
+      b = take ? b2 : b;
+    }
+    key[c] = a;
+    pos[c] = a == ~0ull ? 0 : b;  // not visited: (~0, 0) as first_leaf leaves it
+  }
+#pragma unroll
+  for (int c = 0; c < kTie; ++c)
+    if (c >= ncand) pos[c] = 0;
 }
 
 // The first visited leaf of several primitives at once, by the reference's own
@@ -1139,7 +1194,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
           // a tie on a many-leaf primitive (walls, floors: up to thousands of
           // leaves) is resolved by one wave (scan list, marked), the others
           // one per lane
-          const bool big = F.prim_leaf_off[p1 + 1] - F.prim_leaf_off[p1] > kTieLeaves;
+          const bool big = WR_TIE_WAVE_ALL || F.prim_leaf_off[p1 + 1] - F.prim_leaf_off[p1] > kTieLeaves;
           need = !big;
           scan = big;
           big_tie = big;
@@ -1284,7 +1339,7 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
   int* stk_node = reinterpret_cast<int*>(lds) + lane;
   float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
   const QueueIndex QI(Q);
-  const int nh = (F.diag & 32) ? 0 : hard_n[0];
+  const int nh = (F.diag & (32 | 128)) ? 0 : hard_n[0];
   const int i0 = WAVE ? bid : bid * 64 + lane;
   const int di = WAVE ? nb : nb * 64;
   for (int i = i0; i < nh; i += di) {
@@ -1306,7 +1361,7 @@ __device__ __forceinline__ void scan_fast(const DevScene& S, const FastScene& F,
   int* stk_node = reinterpret_cast<int*>(lds) + lane;
   float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
   const QueueIndex QI(Q);
-  const int ns = (F.diag & 32) ? 0 : hard_n[1];
+  const int ns = (F.diag & (32 | 64)) ? 0 : hard_n[1];
   for (int i = bid; i < ns; i += nb) {
     const int e = hard[hcap - 1 - i];
     const bool tie = e < 0;  // a near-tie on a many-leaf primitive: straight to the general resolution

@@ -214,7 +214,10 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
   }
 }
 template <bool COUNT>
-__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) WR_NO_PK_FP32
+#ifndef WR_FAST_WAVES
+#define WR_FAST_WAVES 4  // minimum waves per SIMD the search's registers must allow
+#endif
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WR_FAST_WAVES, 8))) WR_NO_PK_FP32
 k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* spill) {
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
@@ -765,7 +768,10 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     // the hard rays are a few in 10^4: a small grid drains any count (one
     // ray per wave for the API calls: up to 2048 at once, 8 waves per CU)
     const int hgrid = hard_wave ? std::max(1, std::min(2048, max_rays)) : std::max(1, std::min(256, blocks));
-    const int sgrid = std::max(1, std::min(256, max_rays));  // scan waves
+#ifndef WR_SCAN_WAVES
+#define WR_SCAN_WAVES 256
+#endif
+    const int sgrid = std::max(1, std::min(WR_SCAN_WAVES, max_rays));  // scan waves
     auto hk = hard_wave ? (count ? k_fast_hard<true, true> : k_fast_hard<false, true>)
                         : (count ? k_fast_hard<true, false> : k_fast_hard<false, false>);
     hipLaunchKernelGGL(hk, dim3(hgrid + sgrid),
