@@ -199,8 +199,8 @@ def main():
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting replay")
     ap.add_argument("--trace", choices=["auto", "reference", "bvh"], default="auto",
                     help="traversal: the reference's KD walk, or the verified BVH search (same (t, primitive) "
-                         "answers, DESIGN.md section 4b); auto = the faster one for the config: bvh for c2 / vcm / "
-                         "c4, reference for c3")
+                         "answers, DESIGN.md section 4b); auto = the faster one: bvh for every config (scenes with "
+                         "spheres, which the BVH mode does not cover, use the KD walk)")
     ap.add_argument("--no-compare", action="store_true",
                     help="skip the single-GPU comparison run in the other traversal mode")
     ap.add_argument("--no-cut", action="store_true",
@@ -225,7 +225,7 @@ def main():
     cfg = CONFIGS[args.config]
     trace = args.trace
     if trace == "auto":
-        trace = "reference" if cfg["integrator"] == "pt" else "bvh"
+        trace = "bvh"
     W, H = args.width, args.height
     K = args.steps if args.steps is not None else cfg["steps"]
     pt = cfg["integrator"] == "pt"
@@ -386,14 +386,17 @@ def main():
         }
         if trace == "bvh":
             out["trace_note"] = ("verified BVH traversal: every ray gets the reference KD walk's (t, primitive) "
-                                 "answer, bit for bit (proof in DESIGN.md 4b; 0 mismatches over the full C2 workload, "
+                                 "answer, bit for bit (proof in DESIGN.md 4b; 0 mismatches over the full bench workloads, "
                                  "profiles/r2/bvh_verify.json); the same rays are traced and counted")
         if other:
             out["other_trace"] = other
         if cfg["integrator"] in ("pt", "vcm"):
-            # dead-work elision is flagged; --no-cut measures without it
-            out["config"]["occlusion_cutoff"] = not args.no_cut
-            if not args.no_cut:
+            # dead-work elision is flagged; --no-cut measures without it.
+            # Only the KD walk has the cutoff: the BVH mode traces every shadow ray
+            # to its closest hit
+            cut = not args.no_cut and trace == "reference"
+            out["config"]["occlusion_cutoff"] = cut
+            if cut:
                 out["dead_work_elision"] = ("occlusion cutoff: a shadow ray ends once a hit below occl_cut "
                                             "settles 'occluded' (exact, DESIGN.md section 4); every ray is "
                                             "still traced and counted; bench.py --no-cut runs without it")
