@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "wr_scene.h"
@@ -36,7 +37,22 @@ struct Box {
   }
 };
 
-constexpr int kBins = 16;
+constexpr int kMaxBins = 256;
+
+// build knobs (measurement only; the defaults are the measured best):
+//   WR_BVH_BINS   SAH bins over the centroids of ranges above the sweep size
+//   WR_BVH_SWEEP  ranges of at most this many triangles take the exact SAH sweep
+//   WR_BVH_CT     cost of one node visit relative to one triangle test
+struct BuildKnobs {
+  int bins = 16;
+  int sweep = 0;
+  double ct = 0.5;
+  BuildKnobs() {
+    if (const char* e = std::getenv("WR_BVH_BINS")) bins = std::max(2, std::min(kMaxBins, std::atoi(e)));
+    if (const char* e = std::getenv("WR_BVH_SWEEP")) sweep = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("WR_BVH_CT")) ct = std::max(0.0, std::atof(e));
+  }
+};
 
 struct Builder {
   const std::vector<Box>& box;
@@ -45,6 +61,9 @@ struct Builder {
   FastHost& out;
   const wr::Scene& s;
   const std::vector<int>& tri_prim;
+  BuildKnobs K;
+  std::vector<int> tmp;
+  std::vector<double> rarea;
 
   int leaf_link(int b, int e) {
     const int first = static_cast<int>(out.tris.size());
@@ -80,10 +99,50 @@ struct Builder {
     return r;
   }
 
-  // split [b, e) by binned SAH over the centroids; returns the split position
-  // (b < m < e) or -1 when a leaf is cheaper (only allowed for e - b <= kMaxLeaf)
+  // exact SAH sweep: every split position of the centroid order on each axis
+  int split_sweep(int b, int e, const Box& nb) {
+    const int n = e - b;
+    double best = INFINITY;
+    int bax = -1, bk = 0;
+    tmp.assign(idx.begin() + b, idx.begin() + e);
+    rarea.resize(static_cast<size_t>(n) + 1);
+    for (int ax = 0; ax < 3; ++ax) {
+      std::sort(tmp.begin(), tmp.end(), [&](int x, int y) {
+        const float cx = cen[3 * x + ax], cy = cen[3 * y + ax];
+        return cx < cy || (cx == cy && x < y);
+      });
+      Box acc;
+      for (int k = n - 1; k > 0; --k) {
+        acc.grow(box[tmp[static_cast<size_t>(k)]]);
+        rarea[static_cast<size_t>(k)] = acc.area();
+      }
+      Box la;
+      for (int k = 1; k < n; ++k) {
+        la.grow(box[tmp[static_cast<size_t>(k - 1)]]);
+        const double cost = la.area() * k + rarea[static_cast<size_t>(k)] * (n - k);
+        if (cost < best) {
+          best = cost;
+          bax = ax;
+          bk = k;
+        }
+      }
+    }
+    if (n <= kMaxLeaf && (bax < 0 || best + K.ct * nb.area() >= nb.area() * n)) return -1;
+    if (bax < 0) return b + n / 2;
+    std::sort(idx.begin() + b, idx.begin() + e, [&](int x, int y) {
+      const float cx = cen[3 * x + bax], cy = cen[3 * y + bax];
+      return cx < cy || (cx == cy && x < y);
+    });
+    return b + bk;
+  }
+
+  // split [b, e) by SAH over the centroids (binned, or swept for small ranges);
+  // returns the split position (b < m < e) or -1 when a leaf is cheaper (only
+  // allowed for e - b <= kMaxLeaf)
   int split(int b, int e, const Box& nb) {
     const int n = e - b;
+    if (n <= K.sweep) return split_sweep(b, e, nb);
+    const int kBins = K.bins;
     Box cb;
     for (int i = b; i < e; ++i) cb.grow(&cen[3 * idx[i]]);
     double best = INFINITY;
@@ -91,8 +150,8 @@ struct Builder {
     for (int ax = 0; ax < 3; ++ax) {
       const float ext = cb.hi[ax] - cb.lo[ax];
       if (!(ext > 0.f)) continue;
-      Box bb[kBins];
-      int bc[kBins] = {0};
+      Box bb[kMaxBins];
+      int bc[kMaxBins] = {0};
       const float sc = kBins / ext;
       for (int i = b; i < e; ++i) {
         int k = static_cast<int>((cen[3 * idx[i] + ax] - cb.lo[ax]) * sc);
@@ -100,8 +159,8 @@ struct Builder {
         bb[k].grow(box[idx[i]]);
         ++bc[k];
       }
-      Box rb[kBins];
-      int rc[kBins];
+      Box rb[kMaxBins];
+      int rc[kMaxBins];
       Box acc;
       int an = 0;
       for (int k = kBins - 1; k > 0; --k) {
@@ -127,7 +186,7 @@ struct Builder {
     if (n <= kMaxLeaf) {
       // leaf cost n tests vs 1 node + the children's tests
       const double leaf = nb.area() * n;
-      if (bax < 0 || best + 0.5 * nb.area() >= leaf) return -1;
+      if (bax < 0 || best + K.ct * nb.area() >= leaf) return -1;
     }
     if (bax < 0) return b + n / 2;  // all centroids equal: split by index
     const float ext = cb.hi[bax] - cb.lo[bax];

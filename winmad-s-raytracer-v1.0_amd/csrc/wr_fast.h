@@ -392,6 +392,13 @@ constexpr int kTieLeaves = 16;  // resolve_tie: replay up to this many KD leaves
 #define WR_TIE_WAVE_ALL 0  // 1: every near-tie to the one-ray-per-wave resolution
 #endif
 constexpr int kTieWaveLeaves = 65536;  // ... or, one ray per wave, up to this many leaves of all candidates (cell-filtered)
+#ifndef WR_TIE_DEFER
+// 1: in the one-ray-per-lane resolution, a near-tie with a many-leaf candidate
+// is handed back (kTieDeferred) and resolved by the lane's whole wave
+// afterwards (first_leaves_wave) instead of a pruned KD walk by the lane alone
+#define WR_TIE_DEFER 1
+#endif
+constexpr int kTieDeferred = -1;
 __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float rtmin, float rtmax, float cap,
                                            int* stk_link, float* stk_t, float (&ct)[kTie], int (&cp)[kTie]) {
   rtmax = fminf(rtmax, cap);
@@ -485,25 +492,6 @@ __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float
   }
 }
 
-// The first leaf of primitive p that the reference's traversal visits, as its
-// visit key (kd_reaches) and p's position in that leaf's list; key = ~0: p is
-// not visited.  (pos < 256, so (key, pos) orders the visits of one ray.)
-__device__ __noinline__ void first_leaf(const FastScene& F, int p, V3 o, V3 d, V3 inv, float tmin0, float tmax0,
-                                        float rtmax, unsigned long long& key, int& pos, uint32_t& steps) {
-  key = ~0ull;
-  pos = 0;
-  const int lb = F.prim_leaf_off[p], le = F.prim_leaf_off[p + 1];
-  for (int k = lb; k < le; ++k) {
-    unsigned long long kk;
-    if (!kd_reaches(F.path + F.prim_leaf[k], o, d, inv, tmin0, tmax0, rtmax, steps, kk)) continue;
-    const int pk = F.prim_leaf_pos[k];
-    if (kk < key || (kk == key && pk < pos)) {
-      key = kk;
-      pos = pk;
-    }
-  }
-}
-
 // Can the reference's walk reach the KD leaf whose cell is (h0.zw, h1) (the
 // header of its path record)?  False only when the ray's LINE misses the cell
 // grown by delta_a = 1e-5 x (|lo_a| + |hi_a| + 2 |o_a|) on every axis.  A leaf is
@@ -527,6 +515,29 @@ __device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3
   const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
   const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
   return !(tn > tf);  // NaN: kept
+}
+
+// The first leaf of primitive p that the reference's traversal visits, as its
+// visit key (kd_reaches) and p's position in that leaf's list; key = ~0: p is
+// not visited.  (pos < 256, so (key, pos) orders the visits of one ray.)
+__device__ __noinline__ void first_leaf(const FastScene& F, int p, V3 o, V3 d, V3 inv, float tmin0, float tmax0,
+                                        float rtmax, unsigned long long& key, int& pos, uint32_t& steps) {
+  key = ~0ull;
+  pos = 0;
+  const int lb = F.prim_leaf_off[p], le = F.prim_leaf_off[p + 1];
+  for (int k = lb; k < le; ++k) {
+    unsigned long long kk;
+    const uint2* rec = F.path + F.prim_leaf[k];
+    // a leaf whose cell the ray's line misses is never reached: no replay
+    if (!cell_may_be_reached(*reinterpret_cast<const uint4*>(rec), *reinterpret_cast<const uint4*>(rec + 2), o, d))
+      continue;
+    if (!kd_reaches(rec, o, d, inv, tmin0, tmax0, rtmax, steps, kk)) continue;
+    const int pk = F.prim_leaf_pos[k];
+    if (kk < key || (kk == key && pk < pos)) {
+      key = kk;
+      pos = pk;
+    }
+  }
 }
 
 // first_leaf for the candidates cp[0, ncand) of ONE ray, with the wave's lanes
@@ -748,6 +759,10 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
     // one ray per wave: the lanes replay every leaf of the candidates side by
     // side (up to kTieWaveLeaves of them, 128 rounds) instead of the walk
     if (WAVE && total <= kTieWaveLeaves) big = false;
+    if (!WAVE && WR_TIE_DEFER && big) {  // the lane's wave resolves it together (hard_fast)
+      dbg = kTieDeferred;
+      return false;
+    }
     if (big) {
       int vis[kTie], ps[kTie];
       for (int c = 0; c < kTie; ++c) {
@@ -1244,8 +1259,10 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
 // the pipelines keep WAVE = false.
 // One listed ray's general resolution: the reference's rule over the visited
 // hits near the smallest (resolve_tie), or failing that its KD walk.
+// Returns false only when the one-lane form hands the ray back (kTieDeferred:
+// nothing written; hard_fast resolves it with the whole wave).
 template <bool COUNT, bool WAVE>
-__device__ __forceinline__ void settle_ray(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin, float rtmax,
+__device__ __forceinline__ bool settle_ray(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin, float rtmax,
                                            float t1, int* stk_node, float* stk_tmin, float* outt, int* outp, int r,
                                            bool lead, FastCounters& ctr) {
   float tb;
@@ -1255,6 +1272,10 @@ __device__ __forceinline__ void settle_ray(const DevScene& S, const FastScene& F
     int dbg = 0;
     const uint64_t c0 = COUNT ? wall_clock64() : 0;
     const bool done = resolve_tie<WAVE>(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, psteps, dbg);
+    if (!WAVE && dbg == kTieDeferred) {
+      if (COUNT) ctr.replay += steps;
+      return false;
+    }
     if (COUNT) {
       ctr.replay += psteps;
       if (lead) {
@@ -1269,19 +1290,19 @@ __device__ __forceinline__ void settle_ray(const DevScene& S, const FastScene& F
     }
     if (F.diag & 4) {  // debug: the resolution record instead of the answer
       if (lead) outp[r] = -2 - dbg;
-      return;
+      return true;
     }
     if (done) {
       if (lead) {
         outt[r] = tb;
         outp[r] = pb;
       }
-      return;
+      return true;
     }
   }
   // unresolved (a crowd of hits near m, or visited hits in the band): the walk decides
   if (COUNT && lead) ++ctr.fallback;
-  if (F.diag & 1) return;
+  if (F.diag & 1) return true;
   const uint64_t c1 = COUNT ? wall_clock64() : 0;
   const uint32_t ki = ctr.kinner, kl = ctr.kleaves, kr = ctr.krefs;
   kd_walk<COUNT>(S, o, d, rtmin, rtmax, stk_node, stk_tmin, tb, pb, ctr);
@@ -1300,6 +1321,7 @@ __device__ __forceinline__ void settle_ray(const DevScene& S, const FastScene& F
     outt[r] = tb;
     outp[r] = pb;
   }
+  return true;
 }
 
 struct ListedRay {
@@ -1340,11 +1362,38 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
   float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
   const QueueIndex QI(Q);
   const int nh = (F.diag & (32 | 128)) ? 0 : hard_n[0];
-  const int i0 = WAVE ? bid : bid * 64 + lane;
-  const int di = WAVE ? nb : nb * 64;
-  for (int i = i0; i < nh; i += di) {
-    const ListedRay L = listed_ray(Q, QI, hard[i]);
-    settle_ray<COUNT, WAVE>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r, lead, ctr);
+  if (WAVE) {
+    for (int i = bid; i < nh; i += nb) {
+      const ListedRay L = listed_ray(Q, QI, hard[i]);
+      settle_ray<COUNT, true>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r, lead,
+                              ctr);
+    }
+    return;
+  }
+  // one ray per lane; the rays a lane hands back (near-ties with a many-leaf
+  // candidate) are then resolved one after another by the whole wave
+  for (int base = bid * 64; base < nh; base += nb * 64) {  // wave-uniform
+    const int i = base + lane;
+    ListedRay L{};
+    bool back = false;
+    if (i < nh) {
+      L = listed_ray(Q, QI, hard[i]);
+      back = !settle_ray<COUNT, false>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r,
+                                       true, ctr);
+    }
+    for (unsigned long long m = __ballot(back); m != 0ull; m &= m - 1ull) {
+      const int src = __ffsll(static_cast<unsigned long long>(m)) - 1;
+      auto bf = [&](float x) { return __shfl(x, src); };
+      auto bi = [&](int x) { return __shfl(x, src); };
+      auto bp = [&](auto* x) {
+        const uint64_t v = reinterpret_cast<uint64_t>(x);
+        const uint32_t lo = __shfl(static_cast<uint32_t>(v), src), hi = __shfl(static_cast<uint32_t>(v >> 32), src);
+        return reinterpret_cast<decltype(x)>((static_cast<uint64_t>(hi) << 32) | lo);
+      };
+      settle_ray<COUNT, true>(S, F, v3(bf(L.o.x), bf(L.o.y), bf(L.o.z)), v3(bf(L.d.x), bf(L.d.y), bf(L.d.z)),
+                              bf(L.rtmin), bf(L.rtmax), bf(L.t1), stk_node, stk_tmin, bp(L.outt), bp(L.outp), bi(L.r),
+                              lane == 0, ctr);
+    }
   }
 }
 
