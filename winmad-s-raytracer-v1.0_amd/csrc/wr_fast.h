@@ -396,7 +396,7 @@ constexpr int kTieWaveLeaves = 65536;  // ... or, one ray per wave, up to this m
 // 1: in the one-ray-per-lane resolution, a near-tie with a many-leaf candidate
 // is handed back (kTieDeferred) and resolved by the lane's whole wave
 // afterwards (first_leaves_wave) instead of a pruned KD walk by the lane alone
-#define WR_TIE_DEFER 1
+#define WR_TIE_DEFER 0
 #endif
 constexpr int kTieDeferred = -1;
 __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float rtmin, float rtmax, float cap,

@@ -232,8 +232,20 @@ k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const f
   resolve_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, hcap, fc);
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
+// WR_HARD_WAVES: register budget of k_fast_hard as waves per SIMD (0: the
+// compiler's choice).  Its waves live for the whole tie / scan work (up to ms)
+// beside the other pipelines' search and vertex waves, so the VGPRs they hold
+// are occupancy taken from those.
+#ifndef WR_HARD_WAVES
+#define WR_HARD_WAVES 0
+#endif
+#if WR_HARD_WAVES > 0
+#define WR_HARD_OCC __attribute__((amdgpu_waves_per_eu(WR_HARD_WAVES, 8)))
+#else
+#define WR_HARD_OCC
+#endif
 template <bool COUNT, bool WAVE>
-__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
+__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32 WR_HARD_OCC
 k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const int* hard, const int* hard_n, int hcap,
             int hard_blocks) {
   // blocks [0, hard_blocks): the tie list; the rest: the scan list, one ray per wave
