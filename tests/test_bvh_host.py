@@ -46,6 +46,15 @@ def test_bvh_structure(maker):
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("knobs", [{"WR_BVH_SWEEP": "100000"}, {"WR_BVH_BINS": "64", "WR_BVH_CT": "1"},
+                                   {"WR_BVH_SWEEP": "64", "WR_BVH_CT": "0.25"}], ids=["sweep", "bins64_ct1", "sweep64_ct025"])
+def test_bvh_build_knobs_keep_the_structure(knobs):
+    """The SAH build knobs (measurement only) change the tree, never its contract."""
+    env = dict(os.environ, **knobs)
+    r = subprocess.run([checker(), _scenes.torus(64, 64)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+
+
 def test_bvh_wide_tree_structure():
     r = subprocess.run([checker(4), _scenes.torus(64, 64)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
