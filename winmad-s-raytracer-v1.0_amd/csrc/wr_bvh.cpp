@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <future>
 
 #include "wr_scene.h"
 
@@ -54,6 +56,21 @@ struct BuildKnobs {
   }
 };
 
+// The right child of a split whose halves both hold >= kParallelMin
+// triangles is built on its own thread (at most kMaxThreads at once) into a
+// separate output, spliced after the left subtree: the layout is the serial
+// build's (node, left subtree, right subtree), bit for bit.  By size, not
+// depth: the SAH's top splits peel small parts (floor, glass) off the scene.
+constexpr int kParallelMin = 8192;
+constexpr int kMaxThreads = 32;
+
+// relocate a child link of a subtree built into its own output
+int relocate(int link, int nbase, int tbase) {
+  if (link >= 0) return link + nbase;
+  const int l = ~link;
+  return ~((((l >> 3) + tbase) << 3) | (l & 7));
+}
+
 struct Builder {
   const std::vector<Box>& box;
   const std::vector<float>& cen;  // 3 per triangle
@@ -61,9 +78,13 @@ struct Builder {
   FastHost& out;
   const wr::Scene& s;
   const std::vector<int>& tri_prim;
+  const std::vector<int32_t>& leaf_off;  // prim_leaf_off of the whole build
+  std::atomic<int>& threads;             // helper threads running
   BuildKnobs K;
   std::vector<int> tmp;
   std::vector<double> rarea;
+  std::vector<Box> bins;  // 2 x K.bins: the bins, then the right-side prefixes
+  std::vector<int> bcount;
 
   int leaf_link(int b, int e) {
     const int first = static_cast<int>(out.tris.size());
@@ -83,8 +104,8 @@ struct Builder {
       const int32_t prim = tri_prim[idx[i]];
       std::memcpy(&r.c[1], &prim, 4);
       // the primitive's KD leaf list (prim_leaf range): no extra lookup when it wins
-      const int32_t lb = out.prim_leaf_off[static_cast<size_t>(prim)];
-      const int32_t ln = out.prim_leaf_off[static_cast<size_t>(prim) + 1] - lb;
+      const int32_t lb = leaf_off[static_cast<size_t>(prim)];
+      const int32_t ln = leaf_off[static_cast<size_t>(prim) + 1] - lb;
       std::memcpy(&r.c[2], &lb, 4);
       std::memcpy(&r.c[3], &ln, 4);
       out.tris.push_back(r);
@@ -136,6 +157,48 @@ struct Builder {
     return b + bk;
   }
 
+  // the binned SAH over one axis: the cheapest split bin (first of equals)
+  void axis_best(int b, int e, const Box& cb, int ax, Box* bb, int* bc, double& best, int& bbin) const {
+    const int kBins = K.bins;
+    const float ext = cb.hi[ax] - cb.lo[ax];
+    best = INFINITY;
+    bbin = -1;
+    if (!(ext > 0.f)) return;
+    Box* rb = bb + kBins;
+    int* rc = bc + kBins;
+    for (int k = 0; k < 2 * kBins; ++k) {  // only the bins in use are cleared
+      bb[k] = Box();
+      bc[k] = 0;
+    }
+    const float sc = kBins / ext;
+    for (int i = b; i < e; ++i) {
+      int k = static_cast<int>((cen[3 * idx[i] + ax] - cb.lo[ax]) * sc);
+      k = std::min(kBins - 1, std::max(0, k));
+      bb[k].grow(box[idx[i]]);
+      ++bc[k];
+    }
+    Box acc;
+    int an = 0;
+    for (int k = kBins - 1; k > 0; --k) {
+      acc.grow(bb[k]);
+      an += bc[k];
+      rb[k] = acc;
+      rc[k] = an;
+    }
+    Box la;
+    int ln = 0;
+    for (int k = 0; k < kBins - 1; ++k) {
+      la.grow(bb[k]);
+      ln += bc[k];
+      if (ln == 0 || rc[k + 1] == 0) continue;
+      const double cost = la.area() * ln + rb[k + 1].area() * rc[k + 1];
+      if (cost < best) {
+        best = cost;
+        bbin = k + 1;
+      }
+    }
+  }
+
   // split [b, e) by SAH over the centroids (binned, or swept for small ranges);
   // returns the split position (b < m < e) or -1 when a leaf is cheaper (only
   // allowed for e - b <= kMaxLeaf)
@@ -145,44 +208,30 @@ struct Builder {
     const int kBins = K.bins;
     Box cb;
     for (int i = b; i < e; ++i) cb.grow(&cen[3 * idx[i]]);
+    double cost[3];
+    int cbin[3];
+    bins.resize(6 * static_cast<size_t>(kBins));
+    bcount.resize(6 * static_cast<size_t>(kBins));
+    auto axis = [&](int ax) {
+      axis_best(b, e, cb, ax, bins.data() + 2 * kBins * ax, bcount.data() + 2 * kBins * ax, cost[ax], cbin[ax]);
+    };
+    if (n >= 8 * kParallelMin) {  // the top splits: one axis per thread
+      auto f1 = std::async(std::launch::async, axis, 1);
+      auto f2 = std::async(std::launch::async, axis, 2);
+      axis(0);
+      f1.get();
+      f2.get();
+    } else {
+      for (int ax = 0; ax < 3; ++ax) axis(ax);
+    }
     double best = INFINITY;
     int bax = -1, bbin = 0;
-    for (int ax = 0; ax < 3; ++ax) {
-      const float ext = cb.hi[ax] - cb.lo[ax];
-      if (!(ext > 0.f)) continue;
-      Box bb[kMaxBins];
-      int bc[kMaxBins] = {0};
-      const float sc = kBins / ext;
-      for (int i = b; i < e; ++i) {
-        int k = static_cast<int>((cen[3 * idx[i] + ax] - cb.lo[ax]) * sc);
-        k = std::min(kBins - 1, std::max(0, k));
-        bb[k].grow(box[idx[i]]);
-        ++bc[k];
+    for (int ax = 0; ax < 3; ++ax)
+      if (cbin[ax] >= 0 && cost[ax] < best) {
+        best = cost[ax];
+        bax = ax;
+        bbin = cbin[ax];
       }
-      Box rb[kMaxBins];
-      int rc[kMaxBins];
-      Box acc;
-      int an = 0;
-      for (int k = kBins - 1; k > 0; --k) {
-        acc.grow(bb[k]);
-        an += bc[k];
-        rb[k] = acc;
-        rc[k] = an;
-      }
-      Box la;
-      int ln = 0;
-      for (int k = 0; k < kBins - 1; ++k) {
-        la.grow(bb[k]);
-        ln += bc[k];
-        if (ln == 0 || rc[k + 1] == 0) continue;
-        const double cost = la.area() * ln + rb[k + 1].area() * rc[k + 1];
-        if (cost < best) {
-          best = cost;
-          bax = ax;
-          bbin = k + 1;
-        }
-      }
-    }
     if (n <= kMaxLeaf) {
       // leaf cost n tests vs 1 node + the children's tests
       const double leaf = nb.area() * n;
@@ -221,8 +270,40 @@ struct Builder {
     const int at = static_cast<int>(out.nodes.size());
     out.nodes.emplace_back();
     const Box l = bounds(b, m), r = bounds(m, e);
-    const int cl = child(b, m, l, depth + 1);
-    const int cr = child(m, e, r, depth + 1);
+    int cl, cr;
+    bool spawn = m - b >= kParallelMin && e - m >= kParallelMin;
+    if (spawn && threads.fetch_add(1) >= kMaxThreads) {
+      threads.fetch_sub(1);
+      spawn = false;
+    }
+    if (spawn) {
+      // [b, m) and [m, e) are disjoint ranges of idx: independent subtrees
+      FastHost sub;
+      sub.ok = true;
+      Builder rb{box, cen, idx, sub, s, tri_prim, leaf_off, threads};
+      int rl = 0;
+      auto fut = std::async(std::launch::async, [&] { rl = rb.child(m, e, r, depth + 1); });
+      cl = child(b, m, l, depth + 1);
+      fut.get();
+      threads.fetch_sub(1);
+      const int nbase = static_cast<int>(out.nodes.size()), tbase = static_cast<int>(out.tris.size());
+      for (BNode n : sub.nodes) {
+        n.c[0] = relocate(n.c[0], nbase, tbase);
+        n.c[1] = relocate(n.c[1], nbase, tbase);
+        out.nodes.push_back(n);
+      }
+      out.tris.insert(out.tris.end(), sub.tris.begin(), sub.tris.end());
+      out.leaves += sub.leaves;
+      out.depth = std::max(out.depth, sub.depth);
+      if (!sub.ok && out.ok) {
+        out.ok = false;
+        out.why = sub.why;
+      }
+      cr = relocate(rl, nbase, tbase);
+    } else {
+      cl = child(b, m, l, depth + 1);
+      cr = child(m, e, r, depth + 1);
+    }
     BNode& nd = out.nodes[static_cast<size_t>(at)];
     for (int k = 0; k < 3; ++k) {
       nd.b[k] = l.lo[k];
@@ -239,7 +320,14 @@ struct Builder {
 
 void kd_paths(const wr::Scene& s, FastHost& out) {
   const size_t np = s.prims.size();
-  std::vector<std::vector<std::pair<int32_t, int32_t>>> per(np);  // (path offset, position in the leaf)
+  // every (primitive, leaf record, position in the leaf) in walk order; grouped
+  // by primitive afterwards by a stable counting sort (the walk is pre-order,
+  // so each primitive's records come out ascending)
+  struct Ref {
+    int32_t prim, off, pos;
+  };
+  std::vector<Ref> refs;
+  refs.reserve(s.refs.size());
   std::vector<uint32_t> cur;  // entries of the current path
   struct Item {
     int node;
@@ -298,32 +386,47 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
         out.path.push_back(b);
       }
       out.path.insert(out.path.end(), cur.begin(), cur.end());
-      for (int i = 0; i < k.count; ++i) {
-        const int p = s.refs[static_cast<size_t>(k.first + i)];
-        if (per[static_cast<size_t>(p)].empty() || per[static_cast<size_t>(p)].back().first != off)
-          per[static_cast<size_t>(p)].emplace_back(off, i);
-      }
+      for (int i = 0; i < k.count; ++i) refs.push_back({s.refs[static_cast<size_t>(k.first + i)], off, i});
     }
   }
-  out.prim_leaf_off.assign(np + 1, 0);
-  for (size_t p = 0; p < np; ++p) out.prim_leaf_off[p + 1] = out.prim_leaf_off[p] + static_cast<int32_t>(per[p].size());
-  out.prim_leaf.reserve(static_cast<size_t>(out.prim_leaf_off[np]));
-  out.prim_leaf_pos.reserve(static_cast<size_t>(out.prim_leaf_off[np]));
-  for (size_t p = 0; p < np; ++p)
-    for (const auto& e : per[p]) {
-      out.prim_leaf.push_back(e.first);
-      out.prim_leaf_pos.push_back(e.second);
+  // a primitive listed twice in one leaf keeps its first position (the leaf
+  // tests it there first)
+  std::vector<int32_t> last(np, -1);
+  std::vector<int32_t> cnt(np + 1, 0);
+  size_t kept = 0;
+  for (Ref& r : refs) {
+    if (last[static_cast<size_t>(r.prim)] == r.off) {
+      r.prim = -1;
+      continue;
     }
+    last[static_cast<size_t>(r.prim)] = r.off;
+    ++cnt[static_cast<size_t>(r.prim) + 1];
+    ++kept;
+  }
+  out.prim_leaf_off.assign(np + 1, 0);
+  for (size_t p = 0; p < np; ++p) out.prim_leaf_off[p + 1] = out.prim_leaf_off[p] + cnt[p + 1];
+  out.prim_leaf.assign(kept, 0);
+  out.prim_leaf_pos.assign(kept, 0);
+  {
+    std::vector<int32_t> at(out.prim_leaf_off.begin(), out.prim_leaf_off.end() - 1);
+    for (const Ref& r : refs) {
+      if (r.prim < 0) continue;
+      const int32_t j = at[static_cast<size_t>(r.prim)]++;
+      out.prim_leaf[static_cast<size_t>(j)] = r.off;
+      out.prim_leaf_pos[static_cast<size_t>(j)] = r.pos;
+    }
+  }
   // the replay reads 8 entries at a time: pad past the last record
   out.path.resize(out.path.size() + 2 * 8, 0u);
   // per primitive: its first four leaves' cells and records in one line
   out.prim_rec.assign(np, PrimRec{});
   for (size_t p = 0; p < np; ++p) {
     PrimRec& r = out.prim_rec[p];
-    r.ln = static_cast<int32_t>(per[p].size());
+    const int32_t lb = out.prim_leaf_off[p];
+    r.ln = out.prim_leaf_off[p + 1] - lb;
     for (int k = 0; k < 4; ++k) {
       const bool have = k < r.ln;
-      const int32_t off = have ? per[p][static_cast<size_t>(k)].first : -1;
+      const int32_t off = have ? out.prim_leaf[static_cast<size_t>(lb + k)] : -1;
       r.off[k] = off;
       for (int a = 0; a < 6; ++a) {
         float v = a < 3 ? INFINITY : -INFINITY;
@@ -408,33 +511,45 @@ void build_fast(const wr::Scene& s, FastHost& out) {
   std::vector<Box> box(n);
   std::vector<float> cen(3 * n);
   std::vector<int> tri_prim(n), idx(n);
-  for (size_t i = 0; i < n; ++i) {
-    const wr::Prim& p = s.prims[i];
-    const float v[3][3] = {{p.p0.x, p.p0.y, p.p0.z}, {p.p1.x, p.p1.y, p.p1.z}, {p.p2.x, p.p2.y, p.p2.z}};
-    Box b;
-    for (auto& q : v) b.grow(q);
-    // the EPS-fattened triangle of Triangle::hit (hits lie within EPS x (|e1| + |e2|)
-    // of it), twice over; the float error of the solve is the per-ray margin's
-    auto len = [](const float* a, const float* c) {
-      const double x = a[0] - c[0], y = a[1] - c[1], z = a[2] - c[2];
-      return std::sqrt(x * x + y * y + z * z);
-    };
-    const double m = kBoxGrow * (len(v[0], v[1]) + len(v[0], v[2])) + 1e-6 * (1.0 + std::max({std::fabs(b.lo[0]),
-        std::fabs(b.lo[1]), std::fabs(b.lo[2]), std::fabs(b.hi[0]), std::fabs(b.hi[1]), std::fabs(b.hi[2])}));
-    for (int k = 0; k < 3; ++k) {
-      b.lo[k] = std::nextafter(static_cast<float>(b.lo[k] - m), -INFINITY);
-      b.hi[k] = std::nextafter(static_cast<float>(b.hi[k] + m), INFINITY);
-      cen[3 * i + k] = 0.5f * (b.lo[k] + b.hi[k]);
+  auto prep = [&](size_t i0, size_t i1) {
+    for (size_t i = i0; i < i1; ++i) {
+      const wr::Prim& p = s.prims[i];
+      const float v[3][3] = {{p.p0.x, p.p0.y, p.p0.z}, {p.p1.x, p.p1.y, p.p1.z}, {p.p2.x, p.p2.y, p.p2.z}};
+      Box b;
+      for (auto& q : v) b.grow(q);
+      // the EPS-fattened triangle of Triangle::hit (hits lie within EPS x (|e1| + |e2|)
+      // of it), twice over; the float error of the solve is the per-ray margin's
+      auto len = [](const float* a, const float* c) {
+        const double x = a[0] - c[0], y = a[1] - c[1], z = a[2] - c[2];
+        return std::sqrt(x * x + y * y + z * z);
+      };
+      const double m = kBoxGrow * (len(v[0], v[1]) + len(v[0], v[2])) + 1e-6 * (1.0 + std::max({std::fabs(b.lo[0]),
+          std::fabs(b.lo[1]), std::fabs(b.lo[2]), std::fabs(b.hi[0]), std::fabs(b.hi[1]), std::fabs(b.hi[2])}));
+      for (int k = 0; k < 3; ++k) {
+        b.lo[k] = std::nextafter(static_cast<float>(b.lo[k] - m), -INFINITY);
+        b.hi[k] = std::nextafter(static_cast<float>(b.hi[k] + m), INFINITY);
+        cen[3 * i + k] = 0.5f * (b.lo[k] + b.hi[k]);
+      }
+      box[i] = b;
+      tri_prim[i] = static_cast<int>(i);
+      idx[i] = static_cast<int>(i);
     }
-    box[i] = b;
-    tri_prim[i] = static_cast<int>(i);
-    idx[i] = static_cast<int>(i);
-  }
+  };
+  // the KD membership data first (the triangle records carry their
+  // prim_leaf range), beside the boxes in chunks of one thread each
+  auto kd = std::async(std::launch::async, [&] { kd_paths(s, out); });
+  const size_t chunk = 1 << 16;
+  std::vector<std::future<void>> parts;
+  for (size_t i0 = chunk; i0 < n; i0 += chunk)
+    parts.push_back(std::async(std::launch::async, prep, i0, std::min(n, i0 + chunk)));
+  prep(0, std::min(n, chunk));
+  for (auto& f : parts) f.get();
+  kd.get();
   out.ok = true;
-  kd_paths(s, out);  // first: the triangle records carry their prim_leaf range
   out.tris.reserve(n);
   out.nodes.reserve(2 * n / kMaxLeaf + 8);
-  Builder B{box, cen, idx, out, s, tri_prim};
+  std::atomic<int> threads{0};
+  Builder B{box, cen, idx, out, s, tri_prim, out.prim_leaf_off, threads};
   // node 0 is always inner (the traversal starts from its two children)
   const int nn = static_cast<int>(n);
   if (nn <= kMaxLeaf) {
