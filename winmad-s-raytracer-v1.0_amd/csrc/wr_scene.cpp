@@ -234,15 +234,21 @@ inline bool is_ws(char c) { return c == ' ' || c == '\t'; }
 int parse_obj(const char* path, ObjFile& of) {
   std::string text;
   if (!read_file(path, text)) return 1;
-  std::vector<std::vector<int>> group;  // faces of the current group
+  // lines are parsed in place: each '\n' becomes the line's terminator
+  for (char& c : text)
+    if (c == '\n') c = 0;
+  // faces of the current group, flat: face f is fidx[fbeg[f] .. fbeg[f + 1])
+  std::vector<int> fidx, fbeg(1, 0);
   std::string name;
   auto flush = [&]() -> bool {
-    if (group.empty()) return true;
+    if (fbeg.size() == 1) return true;
     ObjShape sh;
     sh.name = name;
     const int nv = static_cast<int>(of.verts.size() / 3);
-    for (const auto& face : group) {
-      for (size_t k = 2; k < face.size(); ++k) {
+    for (size_t f = 0; f + 1 < fbeg.size(); ++f) {
+      const int* face = fidx.data() + fbeg[f];
+      const int fn = fbeg[f + 1] - fbeg[f];
+      for (int k = 2; k < fn; ++k) {
         int i0 = face[0], i1 = face[k - 1], i2 = face[k];
         if (i0 < 0 || i1 < 0 || i2 < 0 || i0 >= nv || i1 >= nv || i2 >= nv) return false;
         sh.tri.push_back(i0);
@@ -251,17 +257,15 @@ int parse_obj(const char* path, ObjFile& of) {
       }
     }
     of.shapes.push_back(std::move(sh));
-    group.clear();
+    fidx.clear();
+    fbeg.assign(1, 0);
     return true;
   };
   size_t pos = 0;
-  std::string line;
-  while (pos < text.size()) {
-    size_t e = text.find('\n', pos);
-    if (e == std::string::npos) e = text.size();
-    line.assign(text, pos, e - pos);
-    pos = e + 1;
-    const char* t = line.c_str();
+  const size_t len = text.size();
+  while (pos < len) {
+    const char* t = text.c_str() + pos;
+    pos += std::strlen(t) + 1;
     t += std::strspn(t, " \t");
     if (!*t || *t == '#') continue;
     if (t[0] == 'v' && is_ws(t[1])) {
@@ -276,11 +280,10 @@ int parse_obj(const char* path, ObjFile& of) {
     if (t[0] == 'f' && is_ws(t[1])) {
       t += 2;
       t += std::strspn(t, " \t");
-      std::vector<int> face;
       const int vcount = static_cast<int>(of.verts.size() / 3);
       while (!(*t == '\r' || *t == '\n' || *t == 0)) {
         int raw = std::atoi(t);
-        face.push_back(raw > 0 ? raw - 1 : (raw == 0 ? 0 : vcount + raw));
+        fidx.push_back(raw > 0 ? raw - 1 : (raw == 0 ? 0 : vcount + raw));
         // skip the i / i/j / i//k / i/j/k triple (only the position index is used)
         for (int part = 0; part < 3; ++part) {
           t += std::strcspn(t, "/ \t\r");
@@ -290,7 +293,7 @@ int parse_obj(const char* path, ObjFile& of) {
         }
         t += std::strspn(t, " \t\r");
       }
-      group.push_back(std::move(face));
+      fbeg.push_back(static_cast<int>(fidx.size()));
       continue;
     }
     if ((t[0] == 'g' || t[0] == 'o') && is_ws(t[1])) {
