@@ -3,6 +3,7 @@
 #include "wr_scene.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -506,12 +507,20 @@ class Builder {
     out.nodes[me].axis = axis;
     out.nodes[me].split = split;
     out.nodes[me].count = nobj;
-    if (dep <= kParallelDepth) {
-      // independent subtrees: build the right one on another thread, splice after
+    // independent subtrees: the right one on another thread when both sides are
+    // large (by size, not depth: the SAH's top splits peel small parts off),
+    // spliced after the left one -- the serial layout
+    bool spawn = L.obj.size() >= kParallelMin && R.obj.size() >= kParallelMin;
+    if (spawn && threads_.fetch_add(1) >= kMaxThreads) {
+      threads_.fetch_sub(1);
+      spawn = false;
+    }
+    if (spawn) {
       Sub rs;
       auto fut = std::async(std::launch::async, [&] { build(std::move(R), dep + 1, rs); });
       build(std::move(L), dep + 1, out);
       fut.get();
+      threads_.fetch_sub(1);
       const int nbase = static_cast<int>(out.nodes.size());
       const int rbase = static_cast<int>(out.refs.size());
       out.nodes[me].right = nbase;
@@ -530,9 +539,11 @@ class Builder {
   }
 
  private:
-  static constexpr int kParallelDepth = 3;
+  static constexpr size_t kParallelMin = 4096;
+  static constexpr int kMaxThreads = 32;
   const Scene& s_;
   int dep_max_;
+  std::atomic<int> threads_{0};
 
   float sah(const Work& w, int axis, float plane, int nl, int nr) const {  // :64-80
     F3 v = w.br - w.bl, vl = v, vr = v;
