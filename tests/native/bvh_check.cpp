@@ -210,6 +210,21 @@ int main(int argc, char** argv) {
     big256 += ln > 256;
   }
   std::printf(" kd leaves per prim: max %d, >16: %zu, >256: %zu", maxln, big16, big256);
-  std::printf("\n");
+  // content hash (FNV-1a) of everything the device reads: equal builds, equal data
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](const void* data, size_t n) {
+    const unsigned char* c = static_cast<const unsigned char*>(data);
+    for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  };
+  mix(f.nodes.data(), f.nodes.size() * sizeof(f.nodes[0]));
+  mix(f.tris.data(), f.tris.size() * sizeof(f.tris[0]));
+  mix(f.prim_leaf_off.data(), f.prim_leaf_off.size() * 4);
+  mix(f.prim_leaf.data(), f.prim_leaf.size() * 4);
+  mix(f.prim_leaf_pos.data(), f.prim_leaf_pos.size() * 4);
+  mix(f.prim_rec.data(), f.prim_rec.size() * sizeof(f.prim_rec[0]));
+  mix(f.path.data(), f.path.size() * 4);
+  mix(f.node_path.data(), f.node_path.size() * 4);
+  mix(f.node_cell.data(), f.node_cell.size() * 4);
+  std::printf(" hash %016llx\n", static_cast<unsigned long long>(h));
   return 0;
 }

@@ -55,6 +55,19 @@ def test_bvh_build_knobs_keep_the_structure(knobs):
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
 
 
+def test_bvh_parallel_build_equals_serial():
+    """The threaded build (subtrees, top splits, boxes) lays out exactly the
+    serial build's data (WR_BVH_SERIAL=1), on a scene big enough to thread."""
+    scene = small_torus()
+    outs = []
+    for serial in ("0", "1"):
+        r = subprocess.run([checker(), scene], capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, WR_BVH_SERIAL=serial))
+        assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+        outs.append(r.stdout.split(" hash ")[1].strip())
+    assert outs[0] == outs[1]
+
+
 def test_bvh_wide_tree_structure():
     r = subprocess.run([checker(4), _scenes.torus(64, 64)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr

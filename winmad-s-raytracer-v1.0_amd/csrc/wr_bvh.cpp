@@ -45,11 +45,14 @@ constexpr int kMaxBins = 256;
 //   WR_BVH_BINS   SAH bins over the centroids of ranges above the sweep size
 //   WR_BVH_SWEEP  ranges of at most this many triangles take the exact SAH sweep
 //   WR_BVH_CT     cost of one node visit relative to one triangle test
+//   WR_BVH_SERIAL 1: no helper threads for subtrees and splits (the same tree)
 struct BuildKnobs {
   int bins = 16;
   int sweep = 0;
   double ct = 0.5;
+  bool serial = false;
   BuildKnobs() {
+    if (const char* e = std::getenv("WR_BVH_SERIAL")) serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("WR_BVH_BINS")) bins = std::max(2, std::min(kMaxBins, std::atoi(e)));
     if (const char* e = std::getenv("WR_BVH_SWEEP")) sweep = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("WR_BVH_CT")) ct = std::max(0.0, std::atof(e));
@@ -215,7 +218,7 @@ struct Builder {
     auto axis = [&](int ax) {
       axis_best(b, e, cb, ax, bins.data() + 2 * kBins * ax, bcount.data() + 2 * kBins * ax, cost[ax], cbin[ax]);
     };
-    if (n >= 8 * kParallelMin) {  // the top splits: one axis per thread
+    if (n >= 8 * kParallelMin && !K.serial) {  // the top splits: one axis per thread
       auto f1 = std::async(std::launch::async, axis, 1);
       auto f2 = std::async(std::launch::async, axis, 2);
       axis(0);
@@ -271,7 +274,7 @@ struct Builder {
     out.nodes.emplace_back();
     const Box l = bounds(b, m), r = bounds(m, e);
     int cl, cr;
-    bool spawn = m - b >= kParallelMin && e - m >= kParallelMin;
+    bool spawn = !K.serial && m - b >= kParallelMin && e - m >= kParallelMin;
     if (spawn && threads.fetch_add(1) >= kMaxThreads) {
       threads.fetch_sub(1);
       spawn = false;
