@@ -395,7 +395,9 @@ constexpr int kTieWaveLeaves = 65536;  // ... or, one ray per wave, up to this m
 #ifndef WR_TIE_DEFER
 // 1: in the one-ray-per-lane resolution, a near-tie with a many-leaf candidate
 // is handed back (kTieDeferred) and resolved by the lane's whole wave
-// afterwards (first_leaves_wave) instead of a pruned KD walk by the lane alone
+// afterwards (first_leaves_wave) instead of a pruned KD walk by the lane alone.
+// Off: the longest tie drops 6.2 -> 0.76 ms, but the 16-pipeline run loses
+// (C4 1,485 -> 1,176 Mrays/s)
 #define WR_TIE_DEFER 0
 #endif
 constexpr int kTieDeferred = -1;
