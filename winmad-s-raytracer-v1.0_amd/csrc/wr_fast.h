@@ -387,7 +387,10 @@ __device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtm
 // smallest hit so far (and cap), with the main search's box margins.  Returns
 // the number of hits <= cap found (> kTie: more exist beyond ct[kTie - 1]).
 constexpr int kTie = 8;
-constexpr int kTieLeaves = 16;  // resolve_tie: replay up to this many KD leaves per candidate, else a pruned walk
+#ifndef WR_TIE_LEAVES
+#define WR_TIE_LEAVES 16
+#endif
+constexpr int kTieLeaves = WR_TIE_LEAVES;  // resolve_tie: replay up to this many KD leaves per candidate, else a pruned walk
 #ifndef WR_TIE_WAVE_ALL
 #define WR_TIE_WAVE_ALL 0  // 1: every near-tie to the one-ray-per-wave resolution
 #endif
