@@ -205,6 +205,13 @@ def main():
                     help="skip the single-GPU comparison run in the other traversal mode")
     ap.add_argument("--no-cut", action="store_true",
                     help="c3/vcm: shadow rays run to the end of the walk (no occlusion cutoff)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo = the film reduction "
+                         "through host memory, for ranks sharing one GPU in tests)")
+    ap.add_argument("--iter-begin", type=int, default=0,
+                    help="global index of rank 0's first iteration (sample): one rank's shard of a bigger job, "
+                         "e.g. --config c4 --steps 512 --iter-begin 512 = rank 1 of SURVEY 8(d) C5")
+    ap.add_argument("--dump-film", default=None, help="rank 0 writes the reduced film here (.npy, float32 H x W x 3)")
     args = ap.parse_args()
     if args.no_cut:
         os.environ["WR_TRACE_NO_CUT"] = "1"  # read by wr_create
@@ -213,12 +220,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank; ranks beyond the visible GPUs share them round-robin
+    # (tests run 2 ranks on a one-GPU box with --backend gloo)
+    local = local % max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     from winmad_rt import native
     from winmad_rt import dist as wdist
 
@@ -247,8 +260,9 @@ def main():
             return ctx.render_vcm(W, H, iterations=count, seed=5489, iter_begin=begin, **kw)
         return ctx.render_bdpt(W, H, iterations=count, seed=5489, iter_begin=begin, **kw)
 
-    if pt and (world * K > args.spp or args.warmup > args.spp):
-        raise SystemExit(f"c3: --steps x ranks ({world * K}) must not exceed --spp ({args.spp})")
+    if pt and (args.iter_begin + world * K > args.spp or args.warmup > args.spp):
+        raise SystemExit(f"c3: --iter-begin + --steps x ranks ({args.iter_begin + world * K}) must not exceed "
+                         f"--spp ({args.spp})")
     if args.warmup > 0:  # warm-up samples / iterations outside the timed ones
         # run as the counting build of the traversal (k_trace<true, ...>): the
         # same caches and allocations warm up, and a rocprofv3 summary of this
@@ -261,7 +275,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    it0 = wdist.bdpt_iteration_begin(rank, K)
+    it0 = args.iter_begin + wdist.bdpt_iteration_begin(rank, K)
     _, st = render(it0, K, film_ptr=film.data_ptr(), time_kernels=1)
     wdist.reduce_film(film, dist)  # one film reduction per batch (RCCL)
     torch.cuda.synchronize()
@@ -270,6 +284,9 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
+    if args.dump_film and rank == 0:
+        import numpy as np
+        np.save(args.dump_film, film.cpu().numpy())
     rays = st.closest_rays + st.shadow_rays
     trace_ms = st.kernel_ms[native.K_TRACE]
     trace_launches = st.kernel_launches[native.K_TRACE]
@@ -378,7 +395,8 @@ def main():
                                    + ("" if pt else ", maxPathLength 10" if cfg["integrator"] == "vcm"
                                       else ", controlLength 3, maxPathLength 10"),
                        "scene_config": args.config.upper(), "width": W, "height": H,
-                       "steps_per_gpu": K, "parallelism": f"sample-batch x{world}", "trace": trace,
+                       "steps_per_gpu": K, "iter_begin": it0, "parallelism": f"sample-batch x{world}",
+                       "backend": args.backend if world > 1 else None, "trace": trace,
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
             "spp_per_sec": round(W * H * K * world / elapsed, 1),
             "rays_per_step": round(total_rays / (K * world)),

@@ -11,8 +11,10 @@
  *   - return 0 on success, a negative WR_E* code on failure; never throw;
  *     the message of the last failure on this thread is wr_last_error();
  *   - plain pointers and sizes only; the caller owns every input / output buffer;
- *   - a wr_context is used by one host thread at a time; it owns one HIP stream on
- *     one device.  Multi-GPU = one process (one context) per GPU; see DESIGN.md.
+ *   - a wr_context is used by one host thread at a time; it owns its HIP streams
+ *     on one device (wr_create) or on several (wr_create_multi).  Multi-GPU is
+ *     either one process per GPU (wr_comm_* below) or one context over the
+ *     node's GPUs (wr_create_multi); see DESIGN.md section 5.
  */
 #ifndef WINMAD_RT_H
 #define WINMAD_RT_H
@@ -22,7 +24,7 @@
 extern "C" {
 #endif
 
-#define WR_API_VERSION 4
+#define WR_API_VERSION 5
 
 enum {
   WR_OK = 0,
@@ -140,8 +142,32 @@ typedef struct {
   int64_t verify_mismatches; /* (t, primitive) pairs that differ bit for bit      */
 } wr_stats;
 
+/* The reference's in-memory Scene (scene/scene.h:35-42) as flat host arrays,
+ * for callers that build or already hold it instead of a .scene file.  The
+ * caller keeps ownership; wr_scene_from_desc copies what it needs and builds
+ * the KD tree (KDtreeAccel::init + buildTree, KDtreeAccel.cpp:12-307), so the
+ * result is the scene wr_scene_load makes from a file with the same content. */
+typedef struct {
+  int32_t n_prims;             /* Scene::objs, in order (the KD tree's tie order)          */
+  const int32_t* prim_type;    /* 0 Triangle (triangle.h:14-31), 1 Sphere (sphere.h:16-21) */
+  const float* prim_data;      /* 9 floats each: triangle p0 p1 p2; sphere centre xyz, radius, 5 unused */
+  const int32_t* prim_mat;     /* matId: >= 0 materials[]; < 0 emitter of AreaLight -matId-1
+                                  (scene.cpp:412-427); 0 = black, ends paths                  */
+  int32_t n_lights;            /* Scene::lights: AreaLight(p0, p1, p2, intensity) (light.h:90-103) */
+  const float* light_tri;      /* 9 floats each: p0 p1 p2                                    */
+  const float* light_le;       /* 3 floats each: intensity (RGB)                             */
+  int32_t n_materials;         /* Scene::materials (material.h:7-31)                          */
+  const float* materials;      /* 11 floats each: diffuse rgb, phong rgb, specular rgb, phongExp, refracIndex */
+  float cam_pos[3], cam_fwd[3], cam_up[3]; /* Camera::setup (camera.cpp:3-29); fwd / up normalised there */
+  float cam_xres, cam_yres;    /* raster size; the reference takes xRes from the XML height (scene.cpp:292-295) */
+  float cam_hfov;              /* horizontal field of view, degrees                          */
+} wr_scene_desc;
+
 /* ---- scene (Scene::init, scene/scene.cpp:469-489 + loadScene :259-467) ---- */
 int wr_scene_load(const char* scene_path, wr_scene** out);
+/* Scene::init from the in-memory arrays above (WR_E_ARG on a malformed desc:
+ * null arrays, bad type, an emitter matId without its light). */
+int wr_scene_from_desc(const wr_scene_desc* desc, wr_scene** out);
 int wr_scene_info_get(const wr_scene* scene, wr_scene_info* out);
 /* Text dump in the format of oracle/ref_driver.cpp `scene` (parity tests). */
 int wr_scene_dump(const wr_scene* scene, const char* out_path);
@@ -150,7 +176,36 @@ void wr_scene_free(wr_scene* scene);
 /* ---- device context ---- */
 int wr_device_count(void);
 int wr_create(const wr_scene* scene, int hip_device, wr_context** out);
+/* Several GPUs of one node behind one context: the scene is uploaded to each
+ * of devices[0..n) and every later call is shared out --
+ *   wr_render_bdpt: equal contiguous shares of the render's path-iterations
+ *     (iteration-major; one iteration still spreads over every device),
+ *   wr_render_vcm: contiguous iteration ranges (a merge grid per iteration),
+ *   wr_render_path: contiguous sample ranges of the spp grid,
+ *   wr_trace_closest / wr_occluded: contiguous ray ranges;
+ *   wr_path_radiance runs on devices[0].
+ * The devices render concurrently into films of their own, which are summed on
+ * devices[0] by one RCCL reduce over xGMI (a device listed twice, or env
+ * WR_MULTI_REDUCE=peer: peer copies + an add kernel), then returned like a
+ * single-device render (a device film lives on devices[0]).  The reference's
+ * render loop over iterations (bidirPathTracing.cpp:25-26) is what is shared
+ * out; the result equals one device's up to float summation order. */
+int wr_create_multi(const wr_scene* scene, const int* hip_devices, int n_devices, wr_context** out);
+/* Devices of a context (devices[0] first); returns their number, writes up to max_n. */
+int wr_context_devices(const wr_context* ctx, int* devices, int max_n);
 void wr_destroy(wr_context* ctx);
+
+/* ---- one process per GPU: each rank renders its own
+ * iterations into a device film; one reduce(sum) of the films over RCCL per
+ * sample batch.  Rank 0 calls wr_comm_unique_id and hands the 128 bytes to the
+ * other ranks (any channel: MPI, a file, torch.distributed); every rank then
+ * calls wr_comm_init on its context. */
+int wr_comm_unique_id(uint8_t id[128]);
+int wr_comm_init(wr_context* ctx, const uint8_t id[128], int nranks, int rank);
+/* Sum the ranks' device films (nfloat floats on the context's device) into
+ * rank `root`'s film, in place; collective (every rank calls it).  Ordered
+ * after the caller's work on the legacy null stream; returns when done. */
+int wr_film_reduce(wr_context* ctx, float* film_dev, int64_t nfloat, int root);
 /* Concurrent render pipelines (HIP streams, each with its own work buffers,
  * ~5 GB per pair of iterations at 1080p): iterations / samples are dealt
  * round-robin to them so that one stream's late-bounce traversal tail overlaps
@@ -226,6 +281,25 @@ int wr_film_write_ppm(const float* film, int height, int width, float scale, flo
  * Other extensions: WR_E_ARG. */
 int wr_film_write_image(const float* film, int height, int width, float scale, float gamma, int transpose,
                         const char* path);
+
+/* ---- film checkpoint / resume.  The reference keeps the film in
+ * memory only while it loops over iterations (bidirPathTracing.cpp:23-27).
+ * Iterations / samples are keyed by their global index, so a render resumes
+ * exactly: load the film, render the indices [done, total) (iter_begin /
+ * sample_begin = done) into it.  The file carries the accumulated, unscaled
+ * film and a checksum; it is replaced atomically (write + rename). */
+enum { WR_CKPT_BDPT = 1, WR_CKPT_VCM = 2, WR_CKPT_PT = 3 };
+typedef struct {
+  int32_t width, height;
+  int32_t kind;         /* WR_CKPT_*                                         */
+  int32_t done, total;  /* iterations (samples) summed in the film / wanted */
+  uint32_t seed;
+  int32_t reserved[2];
+} wr_checkpoint_info; /* 32 bytes */
+int wr_checkpoint_save(const char* path, const wr_checkpoint_info* info, const float* film);
+/* film == NULL reads the header only; else film_floats must be height*width*3.
+ * WR_E_IO for a missing, foreign, truncated or corrupt file. */
+int wr_checkpoint_load(const char* path, wr_checkpoint_info* info, float* film, int64_t film_floats);
 
 const char* wr_last_error(void);
 int wr_api_version(void);

@@ -1,0 +1,139 @@
+#!/usr/bin/env python3
+"""Distribution of GPU-vs-oracle film differences (counter RNG, same streams)
+over the parity cases of tests/test_gpu*.py plus the larger C3 / C4 films --
+the data the film gates in tests/_parity.py are set from.
+
+Per case: relative RMSE (RMSE / RMS(oracle)), per-channel RMSE, and the
+fraction of film values whose relative difference exceeds 1e-6 .. 1e-3
+(relative to max(|oracle|, 1e-3 x mean |oracle|)), plus ray-count deltas.
+Writes one JSON line per case to stdout (and --out).
+
+    python scripts/parity_stats.py [--out gpurun_out/parity_stats.jsonl] [--quick]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "winmad-s-raytracer-v1.0_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import numpy as np  # noqa: E402
+
+import _oracle  # noqa: E402
+import _parity  # noqa: E402
+import _scenes  # noqa: E402
+from winmad_rt import native, scenes  # noqa: E402
+
+
+def stats(a, b):
+    a = a.astype(np.float64)
+    b = b.astype(np.float64)
+    d = np.abs(a - b)
+    rmse = float(np.sqrt((d ** 2).mean()))
+    rms = float(np.sqrt((b ** 2).mean()))
+    floor = 1e-3 * float(np.abs(b).mean()) + 1e-30
+    rel = d / np.maximum(np.abs(b), floor)
+    out = {"rel_rmse": rmse / rms if rms > 0 else None, "rms": rms,
+           "ch_rmse": [float(x) for x in np.sqrt((d ** 2).mean(axis=(0, 1)))],
+           "max_rel": float(rel.max())}
+    for k in (6, 5, 4, 3, 2):
+        out[f"frac_rel_gt_1e-{k}"] = float((rel > 10.0 ** -k).mean())
+    # pixels (any channel) above 1e-3
+    out["pix_rel_gt_1e-3"] = int((rel > 1e-3).any(axis=2).sum())
+    out["npix"] = int(rel.shape[0] * rel.shape[1])
+    g = _parity.film_stats(a, b)
+    for k in ("bias", "bad_pixels", "trimmed_rel_rmse", "trimmed_bias"):
+        out[k] = g[k]
+    return out
+
+
+def big_torus(W, H):
+    p = os.path.join(_scenes._DIR, "torus1m.obj")
+    if not os.path.exists(p):
+        scenes.synth_torus_obj(p)
+    return _scenes.path(f"torus1m_{W}x{H}.scene", scenes.torus_scene(W, H, "bdpt", torus_obj=p))
+
+
+def cases(quick):
+    # (name, kind, scene maker, W, H, gpu kwargs, oracle call)
+    c = [
+        ("bdpt_torus64_i4", "bdpt", lambda: _scenes.torus(64, 64), 64, 64, dict(iterations=4, seed=5489)),
+        ("bdpt_torus96x64_i2", "bdpt", lambda: _scenes.torus(96, 64), 96, 64, dict(iterations=2, seed=5489)),
+        ("bdpt_torus64_ctl0", "bdpt", lambda: _scenes.torus(64, 64), 64, 64,
+         dict(iterations=2, seed=11, control_length=0)),
+        ("bdpt_spheres64_i4", "bdpt", lambda: _scenes.spheres(64, 64), 64, 64, dict(iterations=4, seed=5489)),
+        ("bdpt_torus256_i2", "bdpt", lambda: _scenes.torus(256, 256), 256, 256, dict(iterations=2, seed=5)),
+        ("pt_cbox64x48_s16", "pt", lambda: _scenes.cbox(64, 48), 64, 48, dict(spp=16, max_depth=7, seed=5489)),
+        ("pt_spheres64_s16", "pt", lambda: _scenes.spheres(64, 64), 64, 64, dict(spp=16, max_depth=7, seed=5489)),
+        ("pt_cbox40x30_s12", "pt", lambda: _scenes.cbox(40, 30), 40, 30, dict(spp=12, max_depth=7, seed=31)),
+        ("vcm_torus64_i3", "vcm", lambda: _scenes.torus(64, 64), 64, 64,
+         dict(iterations=3, seed=3, radius_factor=0.05)),
+        ("vcm_tent64_i2", "vcm", lambda: _scenes.tent(64, 64), 64, 64, dict(iterations=2, seed=3, radius_factor=0.05)),
+    ]
+    if not quick:
+        c += [
+            ("bdpt_torus1080p_i1", "bdpt", lambda: _scenes.torus(1920, 1080), 1920, 1080,
+             dict(iterations=1, seed=5489)),
+            ("pt_cbox480x270_s4", "pt", lambda: _scenes.cbox(480, 270), 480, 270, dict(spp=4, max_depth=7, seed=5489)),
+            ("bdpt_torus1m_384x216_i1", "bdpt", lambda: big_torus(384, 216), 384, 216, dict(iterations=1, seed=5489)),
+            ("vcm_torus1080p_i1", "vcm", lambda: _scenes.torus(1920, 1080), 1920, 1080, dict(iterations=1, seed=5489)),
+        ]
+    return c
+
+
+def run_case(name, kind, maker, W, H, kw, trace):
+    path = maker()
+    s = native.Scene(path)
+    c = native.Context(s, 0)
+    if trace == "bvh":
+        try:
+            c.set_trace_mode(native.TRACE_BVH)
+        except native.WrError:
+            pass
+    o = _oracle.Scene(path)
+    t0 = time.time()
+    if kind == "bdpt":
+        film, st = c.render_bdpt(W, H, **kw)
+        ref, rst = o.bdpt(W, H, kw["iterations"], kw["seed"], mode=1, control_length=kw.get("control_length", 3))
+    elif kind == "vcm":
+        film, st = c.render_vcm(W, H, **kw)
+        ref, rst = o.vcm(W, H, kw["iterations"], kw["seed"], mode=1, radius_factor=kw.get("radius_factor", 0.003))
+    else:
+        film, st = c.render_path(W, H, **kw)
+        film = film * np.float32(1.0 / kw["spp"])
+        ref, rst = o.pt(W, H, kw["spp"], kw["max_depth"], kw["seed"], mode=1)
+    r = {"case": name, "trace": trace, "seconds": round(time.time() - t0, 2)}
+    r.update(stats(film, ref))
+    r["d_closest"] = int(st.closest_rays - rst.closest_rays)
+    r["d_shadow"] = int(st.shadow_rays - rst.shadow_rays)
+    r["rays"] = int(rst.closest_rays + rst.shadow_rays)
+    try:
+        (_parity.assert_vcm_parity if kind == "vcm" else _parity.assert_film_parity)(film, ref)
+        r["gate"] = "pass"
+    except AssertionError as e:
+        r["gate"] = "FAIL " + str(e)[:300]
+    c.close()
+    return r
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--trace", default="reference", choices=["reference", "bvh"])
+    args = ap.parse_args()
+    f = open(args.out, "a") if args.out else None
+    for cs in cases(args.quick):
+        r = run_case(*cs, trace=args.trace)
+        line = json.dumps(r)
+        print(line, flush=True)
+        if f:
+            f.write(line + "\n")
+            f.flush()
+
+
+if __name__ == "__main__":
+    main()

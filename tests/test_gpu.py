@@ -5,9 +5,11 @@ Tolerances
   * traversal (wr_trace_closest / wr_occluded): bit-exact vs the reference's own
     outputs (tests/golden/rays_*.txt) -- same float ops, no FMA contraction;
   * films: the GPU and the oracle draw the same counter-RNG numbers; they differ
-    only where OCML and glibc cosf/sinf/powf round differently, so the gate is
-    relative RMSE (RMSE / RMS(oracle)) < 1e-2 plus per-channel RMSE < 1e-3
-    (north_star), and ray counts within 0.5 %;
+    only where OCML and glibc cosf/sinf/powf round differently.  The gates
+    (tests/_parity.py, set from scripts/parity_stats.py's measurements): a few
+    pixels of "split" paths may differ freely, every other pixel agrees to
+    1e-5 (relative RMSE and summed bias), per-channel RMSE < 1e-3 (north_star),
+    ray counts equal up to the split paths' rays;
   * full-size runs: size-independent properties (finite, non-negative,
     iteration additivity == sharding invariance, determinism of the ray set).
 """
@@ -18,6 +20,7 @@ import pytest
 
 import _oracle
 import _scenes
+from _parity import assert_film_parity, assert_ray_counts
 from test_oracle import parse_rays
 from winmad_rt import native
 
@@ -102,20 +105,15 @@ def test_bdpt_matches_oracle_counter_rng(W, H, it):
     path = _scenes.torus(W, H)
     film, st = ctx(path).render_bdpt(W, H, iterations=it, seed=5489)
     ref, rst = _oracle.Scene(path).bdpt(W, H, it, 5489, mode=1)
-    rmse, rms, ch = film_err(film, ref)
-    assert np.all(np.isfinite(film)) and film.min() >= 0
-    assert rmse / rms < 1e-2, (rmse, rms)
-    assert np.all(ch < 1e-3), ch
-    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
-    assert abs(st.shadow_rays - rst.shadow_rays) <= 0.005 * rst.shadow_rays + 2
+    assert_film_parity(film, ref)
+    assert_ray_counts(st, rst)
 
 
 def test_bdpt_all_lengths_and_control_length_filter():
     path = _scenes.torus(64, 64)
     f_all, _ = ctx(path).render_bdpt(64, 64, iterations=2, seed=11, control_length=0)
     r_all, _ = _oracle.Scene(path).bdpt(64, 64, 2, 11, mode=1, control_length=0)
-    rmse, rms, _ = film_err(f_all, r_all)
-    assert rmse / rms < 1e-2
+    assert_film_parity(f_all, r_all)
     f3, _ = ctx(path).render_bdpt(64, 64, iterations=2, seed=11)
     assert f_all.mean() > f3.mean()  # the length-3 filter drops energy
 
@@ -138,9 +136,8 @@ def test_pt_matches_oracle_counter_rng():
     film, st = ctx(path).render_path(64, 48, spp=16, max_depth=7, seed=5489)
     ref, rst = _oracle.Scene(path).pt(64, 48, 16, 7, 5489, mode=1)
     film = film * np.float32(1.0 / 16)  # the oracle (like the reference) scales by 1/spp
-    rmse, rms, ch = film_err(film, ref)
-    assert rmse / rms < 1e-2, (rmse, rms)
-    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+    assert_film_parity(film, ref)
+    assert_ray_counts(st, rst)
 
 
 def test_pt_sample_sharding_is_additive():
@@ -158,9 +155,8 @@ def test_pt_sample_range_matches_oracle():
     path = _scenes.cbox(64, 48)
     film, st = ctx(path).render_path(64, 48, spp=9, max_depth=7, seed=8, sample_begin=3, sample_count=5)
     ref, rst = _oracle.Scene(path).pt_samples(64, 48, 9, 3, 5, 7, 8)
-    rmse, rms, ch = film_err(film, ref)
-    assert rmse / rms < 1e-2, (rmse, rms)
-    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+    assert_film_parity(film, ref)
+    assert_ray_counts(st, rst)
 
 
 def test_bdpt_1080p_properties_and_sharding():
@@ -227,11 +223,8 @@ def test_bdpt_1080p_matches_oracle_counter_rng():
     path = _scenes.torus(W, H)
     film, st = ctx(path).render_bdpt(W, H, iterations=1, seed=5489)
     ref, rst = _oracle.Scene(path).bdpt(W, H, 1, 5489, mode=1)
-    rmse, rms, ch = film_err(film, ref)
-    assert rmse / rms < 1e-2, (rmse, rms)
-    assert np.all(ch < 1e-3), ch
-    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
-    assert abs(st.shadow_rays - rst.shadow_rays) <= 0.005 * rst.shadow_rays
+    assert_film_parity(film, ref)
+    assert_ray_counts(st, rst)
 
 
 def test_path_radiance_per_ray_matches_oracle():
@@ -397,6 +390,38 @@ def test_pipeline_count_does_not_change_the_render(pipes):
         c.set_pipelines(0)
 
 
+@pytest.mark.parametrize("W,H", [(256, 256), (100, 60)])
+def test_bdpt_pieces_render_like_whole_iterations(W, H, monkeypatch):
+    """Iterations cut into path-range pieces over 8 pipelines (plan_pieces:
+    light path i and camera path i stay together, lightPathNum stays W*H):
+    the same rays as whole iterations on one pipeline, the same film up to the
+    order of float atomics, and the oracle's film.  100x60 is not a multiple of
+    the 8x8 camera tiles (64-path units instead of 8-row bands)."""
+    path = _scenes.torus(W, H)
+    s = native.Scene(path)
+    monkeypatch.setenv("WR_PIECE_MIN", "1024")
+    monkeypatch.setenv("WR_PIECE_CAP", "4096")
+    cut = native.Context(s, 0)
+    cut.set_pipelines(8)
+    got, gs = cut.render_bdpt(W, H, iterations=3, seed=21)
+    one, os_ = cut.render_bdpt(W, H, iterations=1, seed=21, iter_begin=2)  # one iteration over 8 pipelines
+    cut.close()
+    monkeypatch.setenv("WR_PIECE_MIN", str(1 << 30))
+    monkeypatch.setenv("WR_PIECE_CAP", str(1 << 21))
+    whole = native.Context(s, 0)
+    whole.set_pipelines(1)
+    ref, rs = whole.render_bdpt(W, H, iterations=3, seed=21)
+    ref1, rs1 = whole.render_bdpt(W, H, iterations=1, seed=21, iter_begin=2)
+    whole.close()
+    assert gs.closest_rays == rs.closest_rays and gs.shadow_rays == rs.shadow_rays
+    assert os_.closest_rays == rs1.closest_rays and os_.shadow_rays == rs1.shadow_rays
+    assert np.allclose(got, ref, rtol=1e-4, atol=1e-6)
+    assert np.allclose(one, ref1, rtol=1e-4, atol=1e-6)
+    orc, ost = _oracle.Scene(path).bdpt(W, H, 3, 21, mode=1)
+    assert_film_parity(got, orc)
+    assert_ray_counts(gs, ost)
+
+
 @pytest.mark.parametrize("mode,W,H", [("-bpt", 64, 64), ("-vcm", 64, 64), ("-p", 64, 48)])
 def test_cli_renders_like_the_reference_main(mode, W, H, tmp_path):
     """wr_tot (the C++ mirror of main.cpp's -bpt / -p branches) end to end on the GPU."""
@@ -421,15 +446,12 @@ def test_spheres_bdpt_and_pt_match_oracle_counter_rng():
     path = _scenes.spheres(64, 64)
     film, st = ctx(path).render_bdpt(64, 64, iterations=4, seed=5489)
     ref, rst = _oracle.Scene(path).bdpt(64, 64, 4, 5489, mode=1)
-    rmse, rms, ch = film_err(film, ref)
-    assert rmse / rms < 1e-2, (rmse, rms)
-    assert np.all(ch < 1e-3), ch
-    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+    assert_film_parity(film, ref)
+    assert_ray_counts(st, rst)
     film, st = ctx(path).render_path(64, 64, spp=16, max_depth=7, seed=5489)
     ref, rst = _oracle.Scene(path).pt(64, 64, 16, 7, 5489, mode=1)
-    rmse, rms, _ = film_err(film * np.float32(1.0 / 16), ref)
-    assert rmse / rms < 1e-2, (rmse, rms)
-    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+    assert_film_parity(film * np.float32(1.0 / 16), ref)
+    assert_ray_counts(st, rst)
 
 
 def test_render_argument_and_scene_errors(tmp_path):
@@ -464,8 +486,8 @@ def test_bdpt_tiny_and_ragged_films_match_oracle(W, H):
     path = _scenes.torus(W, H)
     film, st = ctx(path).render_bdpt(W, H, iterations=3, seed=17)
     ref, rst = _oracle.Scene(path).bdpt(W, H, 3, 17, mode=1)
-    assert st.closest_rays == rst.closest_rays or abs(st.closest_rays - rst.closest_rays) <= 2
-    assert np.allclose(film, ref, rtol=1e-3, atol=1e-5)
+    assert_ray_counts(st, rst)
+    assert_film_parity(film, ref)
 
 
 def test_zero_iterations_and_depth_zero():
@@ -476,7 +498,7 @@ def test_zero_iterations_and_depth_zero():
     film, st = ctx(path).render_path(16, 12, spp=4, max_depth=0, seed=2)
     ref, rst = _oracle.Scene(path).pt(16, 12, 4, 0, 2, mode=1)
     assert st.closest_rays == rst.closest_rays
-    assert np.allclose(film / 4, ref, rtol=1e-3, atol=1e-6)
+    assert_film_parity(film * np.float32(1.0 / 4), ref)
 
 
 @pytest.mark.parametrize("spp", [8, 12])
@@ -487,6 +509,29 @@ def test_pt_non_square_spp_stratification_matches_oracle(spp):
     path = _scenes.cbox(40, 30)
     film, st = ctx(path).render_path(40, 30, spp=spp, max_depth=7, seed=31)
     ref, rst = _oracle.Scene(path).pt(40, 30, spp, 7, 31, mode=1)
-    rmse, rms, _ = film_err(film * np.float32(1.0 / spp), ref)
-    assert rmse / rms < 1e-2, (rmse, rms)
-    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+    assert_film_parity(film * np.float32(1.0 / spp), ref)
+    assert_ray_counts(st, rst)
+
+
+def test_bdpt_1m_scene_film_matches_oracle():
+    """C4's scene (the 1M-triangle torus: deep KD tree, wide-stack traversal),
+    BDPT at 384x216 (a fifth of the C4 frame per axis), one iteration, against
+    the oracle's film: the same gates as every BDPT film."""
+    from test_gpu_bvh import big_torus
+    W, H = 384, 216
+    path = big_torus(W, H)
+    film, st = ctx(path).render_bdpt(W, H, iterations=1, seed=5489)
+    ref, rst = _oracle.Scene(path).bdpt(W, H, 1, 5489, mode=1)
+    assert_film_parity(film, ref)
+    assert_ray_counts(st, rst)
+
+
+def test_pt_c3_film_480x270_matches_oracle():
+    """C3 (Cornell box + dragon, PT, MAX_TRACING_DEPTH 7) at 480x270 with 4
+    stratified samples against the oracle's film."""
+    W, H = 480, 270
+    path = _scenes.cbox(W, H)
+    film, st = ctx(path).render_path(W, H, spp=4, max_depth=7, seed=5489)
+    ref, rst = _oracle.Scene(path).pt(W, H, 4, 7, 5489, mode=1)
+    assert_film_parity(film * np.float32(1.0 / 4), ref)
+    assert_ray_counts(st, rst)

@@ -5,8 +5,10 @@ The GPU and the oracle draw the same counter-RNG numbers.  Differences come
 from OCML vs glibc cosf/sinf/powf rounding (as for BDPT) and from the order in
 which merged contributions are summed (hash grid vs the reference's KD tree:
 the SET of merged light vertices is the same, tests/test_oracle.py
-test_vcm_kdtree_search_is_the_brute_force_set).  Gates: relative film RMSE
-< 1e-2 and per-channel RMSE < 1e-3 (north_star), ray counts within 0.5 %,
+test_vcm_kdtree_search_is_the_brute_force_set).  Gates: whole-film relative
+RMSE < 5e-3 and summed bias < 1e-3 (tests/_parity.py: an ulp of vertex
+position flips merges at the radius, so per-pixel gates do not apply),
+per-channel RMSE < 1e-3 (north_star), ray counts equal up to split paths,
 merge counts (vertices found in radius, merges) within 1 %.
 """
 import numpy as np
@@ -14,20 +16,17 @@ import pytest
 
 import _oracle
 import _scenes
-from test_gpu import ctx, film_err
+from _parity import assert_vcm_parity
+from test_gpu import ctx
 from winmad_rt import native
 
 pytestmark = pytest.mark.gpu
 
 
-def _check(film, st, ref, rst, rel=1e-2):
-    rmse, rms, ch = film_err(film, ref)
-    assert np.all(np.isfinite(film)) and film.min() >= 0
-    assert rms > 0
-    assert rmse / rms < rel, (rmse, rms)
-    assert np.all(ch < 1e-3), ch
-    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
-    assert abs(st.shadow_rays - rst.shadow_rays) <= 0.005 * rst.shadow_rays + 2
+def _check(film, st, ref, rst):
+    assert_vcm_parity(film, ref)
+    assert abs(st.closest_rays - rst.closest_rays) <= 16 + 2e-6 * rst.closest_rays
+    assert abs(st.shadow_rays - rst.shadow_rays) <= 16 + 2e-6 * rst.shadow_rays
     assert abs(st.vm_queries - rst.vm_queries) <= 0.005 * rst.vm_queries + 2
     assert abs(st.vm_found - rst.vm_found) <= 0.01 * rst.vm_found + 4
     assert abs(st.vm_merged - rst.vm_merged) <= 0.01 * rst.vm_merged + 4
@@ -91,7 +90,7 @@ def test_vcm_tiny_films_and_errors():
     film, st = ctx(path).render_vcm(7, 5, iterations=3, seed=17, radius_factor=0.05)
     ref, rst = _oracle.Scene(path).vcm(7, 5, 3, 17, mode=1, radius_factor=0.05)
     assert abs(st.closest_rays - rst.closest_rays) <= 2
-    assert np.allclose(film, ref, rtol=1e-3, atol=1e-5)
+    assert_vcm_parity(film, ref)
     c = ctx(_scenes.torus(16, 16))
     film, st = c.render_vcm(16, 16, iterations=0)
     assert st.closest_rays == 0 and not film.any()

@@ -1,5 +1,6 @@
 #include "integrators.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -34,8 +35,51 @@ SurfaceIntegrator::~SurfaceIntegrator() {
 
 void SurfaceIntegrator::load(const char* filename) {
   ok(wr_scene_load(filename, &scene_));
-  ok(wr_create(scene_, device, &ctx_));
+  if (devices.size() > 1)
+    ok(wr_create_multi(scene_, devices.data(), static_cast<int>(devices.size()), &ctx_));
+  else
+    ok(wr_create(scene_, devices.empty() ? device : devices[0], &ctx_));
+  if (traceMode >= 0) ok(wr_set_trace_mode(ctx_, traceMode));
   film.assign(static_cast<size_t>(height) * width * 3, 0.f);
+}
+
+void SurfaceIntegrator::setTraceMode(int mode) {
+  ok(wr_set_trace_mode(ctx_, mode));
+  traceMode = mode;
+}
+
+template <class Batch>
+void SurfaceIntegrator::batched(int kind, int total, uint32_t seed, Batch batch) {
+  int done = 0;
+  stopped = false;
+  wr_checkpoint_info want{width, height, kind, 0, total, seed, {0, 0}};
+  if (!checkpointPath.empty()) {
+    wr_checkpoint_info have{};
+    if (FILE* f = std::fopen(checkpointPath.c_str(), "rb")) {  // resume
+      std::fclose(f);
+      ok(wr_checkpoint_load(checkpointPath.c_str(), &have, nullptr, 0));
+      if (have.width != width || have.height != height || have.kind != kind || have.total != total ||
+          have.seed != seed)
+        throw std::runtime_error("checkpoint " + checkpointPath + " belongs to another render");
+      ok(wr_checkpoint_load(checkpointPath.c_str(), &have, film.data(), static_cast<int64_t>(film.size())));
+      done = have.done;
+    }
+  }
+  while (done < total) {
+    int n = total - done;
+    if (checkpointEvery > 0) n = std::min(n, checkpointEvery);
+    if (stopAfter >= 0) n = std::min(n, stopAfter - done);
+    if (n <= 0) {
+      stopped = true;
+      return;
+    }
+    batch(done, n);
+    done += n;
+    if (!checkpointPath.empty()) {
+      want.done = done;
+      ok(wr_checkpoint_save(checkpointPath.c_str(), &want, film.data()));
+    }
+  }
 }
 
 void BidirPathTracing::init(const char* filename, Parameters& para) {
@@ -46,16 +90,18 @@ void BidirPathTracing::init(const char* filename, Parameters& para) {
 }
 
 void BidirPathTracing::render() {
-  wr_bdpt_params p{};
-  p.width = width;
-  p.height = height;
-  p.iterations = iterations;
-  p.iter_begin = 0;
-  p.control_length = controlLength;
-  p.max_path_length = maxPathLength;
-  p.seed = seed;
-  p.faithful = 1;
-  ok(wr_render_bdpt(ctx_, &p, film.data(), 0, &stats));
+  batched(WR_CKPT_BDPT, iterations, seed, [&](int begin, int count) {  // :25-26
+    wr_bdpt_params p{};
+    p.width = width;
+    p.height = height;
+    p.iterations = count;
+    p.iter_begin = begin;
+    p.control_length = controlLength;
+    p.max_path_length = maxPathLength;
+    p.seed = seed;
+    p.faithful = 1;
+    ok(wr_render_bdpt(ctx_, &p, film.data(), 0, &stats));
+  });
 }
 
 void BidirPathTracing::outputImage(const char* filename) {
@@ -72,17 +118,19 @@ void VertexCM::init(const char* filename, Parameters& para) {
 }
 
 void VertexCM::render() {
-  wr_vcm_params p{};
-  p.width = width;
-  p.height = height;
-  p.iterations = iterations;
-  p.iter_begin = 0;
-  p.min_path_length = minPathLength;
-  p.max_path_length = maxPathLength;
-  p.radius_factor = baseRadiusFactor;
-  p.radius_alpha = radiusAlpha;
-  p.seed = seed;
-  ok(wr_render_vcm(ctx_, &p, film.data(), 0, &stats));
+  batched(WR_CKPT_VCM, iterations, seed, [&](int begin, int count) {
+    wr_vcm_params p{};
+    p.width = width;
+    p.height = height;
+    p.iterations = count;
+    p.iter_begin = begin;  // the merge radius follows the global iteration index (:53-58)
+    p.min_path_length = minPathLength;
+    p.max_path_length = maxPathLength;
+    p.radius_factor = baseRadiusFactor;
+    p.radius_alpha = radiusAlpha;
+    p.seed = seed;
+    ok(wr_render_vcm(ctx_, &p, film.data(), 0, &stats));
+  });
 }
 
 void VertexCM::outputImage(const char* filename) {
@@ -101,15 +149,18 @@ void PathIntegrator::init(const char* filename, Parameters& para) {
 }
 
 void PathIntegrator::render() {
-  wr_path_params p{};
-  p.width = width;
-  p.height = height;
-  p.spp = samplesPerPixel;
-  p.max_depth = maxTracingDepth;
-  p.sample_begin = 0;
-  p.sample_count = samplesPerPixel;
-  p.seed = seed;
-  ok(wr_render_path(ctx_, &p, film.data(), 0, &stats));
+  batched(WR_CKPT_PT, samplesPerPixel, seed, [&](int begin, int count) {
+    wr_path_params p{};
+    p.width = width;
+    p.height = height;
+    p.spp = samplesPerPixel;
+    p.max_depth = maxTracingDepth;
+    p.sample_begin = begin;  // sample k of the stratification grid (surfaceIntegrator.cpp:26-32)
+    p.sample_count = count;
+    p.seed = seed;
+    ok(wr_render_path(ctx_, &p, film.data(), 0, &stats));
+  });
+  if (stopped) return;
   const float inv = 1.f / samplesPerPixel;  // film->scale(1.f / samplesPerPixel) (:45)
   for (float& v : film) v = v * inv;
 }

@@ -28,17 +28,34 @@ class SurfaceIntegrator {
  public:
   int width = 0, height = 0, samplesPerPixel = 0;
   int device = 0;
+  std::vector<int> devices;  // more than one: the GPUs of this node share the render (wr_create_multi)
+  int traceMode = -1;        // -1: the library's default (WR_TRACE_REFERENCE); WR_TRACE_REFERENCE / WR_TRACE_BVH
+  // Film checkpoint (the reference keeps the film in memory only,
+  // bidirPathTracing.cpp:23-27): with a path set, render() resumes from a
+  // matching checkpoint and saves one every checkpointEvery iterations
+  // (samples) and at the end.  stopAfter >= 0 stops once that many are done
+  // (an interruption, for tests); `stopped` then says the film is partial.
+  std::string checkpointPath;
+  int checkpointEvery = 0;
+  int stopAfter = -1;
+  bool stopped = false;
   std::vector<float> film;  // ImageFilm color[height][width] (r, g, b)
   wr_stats stats{};
   virtual ~SurfaceIntegrator();
   virtual void init(const char* filename, Parameters& para) = 0;
   virtual void render() = 0;
   virtual void outputImage(const char* filename) = 0;
+  // wr_set_trace_mode after init (throws, e.g. WR_TRACE_BVH on a scene with spheres)
+  void setTraceMode(int mode);
 
  protected:
   wr_scene* scene_ = nullptr;
   wr_context* ctx_ = nullptr;
   void load(const char* filename);
+  // the render loop in batches: renders [done, total) through batch(begin, count),
+  // resuming from / saving checkpoints of `kind`
+  template <class Batch>
+  void batched(int kind, int total, uint32_t seed, Batch batch);
 };
 
 // src/surfaceIntegrator/bidirPathTracing.{h,cpp}

@@ -44,7 +44,9 @@ struct BdptArgs {
   DevCounters* ctr;
   StepCounters* sc;  // this iteration's queue counters
   float* film;
-  int W, H, P;
+  int W, H, P;     // film; P = W * H = lightPathNum (MIS, :55) -- global, whatever the piece
+  int base, n;     // this piece of the iteration: global paths [base, base + n); buffers hold
+                   // them at local index l = p - base (stride B.P >= n)
   uint32_t seed, iter;
   int ctl, maxlen, faithful;
 };
@@ -53,15 +55,23 @@ struct BdptGroup {
 };
 
 __device__ __forceinline__ bool len_ok(int ctl, int L) { return ctl <= 0 || L == ctl; }
+// Numerator of connectVertices' MIS weight (:658-664): 1 in every product
+// build.  scripts/perturbation_check.sh builds a variant with 1.001 to show
+// that the film parity gates (tests/_parity.py) catch a 1e-3 weight error.
+#ifndef WR_TEST_CONN_W
+#define WR_TEST_CONN_W 1.f
+#endif
 
 // generateLightSample (:267-311) + the first extension ray
 __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_light_gen(BdptGroup G_) {
   const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
-  const int P = A.P;
+  const int P = B.P;  // buffer stride
   const float lpp = 1.f / static_cast<float>(A.S.nlights);
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-    Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), 0};
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < A.n; p += gridDim.x * blockDim.x) {
+    // local index p, global light path A.base + p (the RNG key pairs it with
+    // the camera path of the same global index, :130, :222-229)
+    Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), 0};
     const int id = min(static_cast<int>(rng.f() * static_cast<float>(A.S.nlights)), A.S.nlights - 1);
     const DLight L = A.S.lights[id];
     V3 pos, dir, rad;
@@ -92,7 +102,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_light_gen(BdptGro
     st3(B.q_d[0], P, p, normalize(dir));
     B.q_path[0][p] = p;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = P;
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = A.n;
 }
 
 // sampleScattering (:370-416).  Returns false when the subpath ends.
@@ -128,7 +138,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
   const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
-  const int P = A.P, cur = slot & 1, nxt = cur ^ 1;
+  const int P = B.P, cur = slot & 1, nxt = cur ^ 1;  // P: buffer stride (local paths)
   const int n = A.sc->ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = gridDim.x * blockDim.x;
@@ -188,9 +198,9 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
                     const float i2s = i2sa * fabsf(cos_to) / d2;
                     const float pdf_a = i2s;
                     const float s2i = 1.f / i2s;
-                    const V3 res = div_plain(mul(thr, f), static_cast<float>(P) * s2i);
+                    const V3 res = div_plain(mul(thr, f), static_cast<float>(A.P) * s2i);
                     if (!black(res)) {
-                      const float wl = (pdf_a / static_cast<float>(P)) * (dvcm + rp * dvc);
+                      const float wl = (pdf_a / static_cast<float>(A.P)) * (dvcm + rp * dvc);
                       const float w = 1.f / (wl + 1.f);
                       splat = true;
                       s_o = h.p;
@@ -204,7 +214,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
             }
           }
           if (!(len + 2 > A.maxlen)) {  // (:123-127)
-            Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), B.l_ctr[p]};
+            Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), B.l_ctr[p]};
             V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
             if (sample_scatter(S, rng, b, h.p, lo, ld, thr, dvcm, dvc, nspec)) {
               ext = true;
@@ -244,27 +254,28 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
   }
 }
 
-// generateCameraSample (:418-452) + first extension ray, for queue entry s;
-// returns the path index.  (VertexCM::generateCameraSample, vertexcm.cpp:446-479,
-// is the same plus dVM = 0.)
+// generateCameraSample (:418-452) + first extension ray, for queue entry s of
+// the piece; returns the path's local index.  (VertexCM::generateCameraSample,
+// vertexcm.cpp:446-479, is the same plus dVM = 0.)
 __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
   const BdptBuf& B = A.B;
   const DCam& cam = A.S.cam;
-  const int P = A.P;
+  const int P = B.P;  // buffer stride
   // queue order: 8x8 raster tiles per wave (coherent primary rays); the
-  // path <-> pixel mapping stays the reference's (x = p / W, y = p % W, :422-423)
+  // path <-> pixel mapping stays the reference's (x = p / W, y = p % W, :422-423).
+  // A tiled piece is whole 8-row bands (base and n multiples of 8 W), so the
+  // tiles are the piece's own.
   const bool tiled = (A.W % 8) == 0 && (A.H % 8) == 0;
   const int tiles_y = A.W / 8;
-  int x, y;
+  int l;
   if (tiled) {
     const int t = s >> 6, w = s & 63;
-    x = (t / tiles_y) * 8 + (w >> 3);
-    y = (t % tiles_y) * 8 + (w & 7);
+    l = ((t / tiles_y) * 8 + (w >> 3)) * A.W + (t % tiles_y) * 8 + (w & 7);
   } else {
-    x = s / A.W;
-    y = s % A.W;
+    l = s;
   }
-  const int p = x * A.W + y;
+  const int p = A.base + l;
+  const int x = p / A.W, y = p % A.W;
   Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), 0};
   const V3 jit = rng.v();
   const float sx = static_cast<float>(x) + jit.x, sy = static_cast<float>(y) + jit.y;
@@ -273,24 +284,24 @@ __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
   const float cos_at = dot(cam.fwd, d);
   const float ipd = cam.plane_dist / cos_at;
   const float i2sa = (ipd * ipd) / cos_at;
-  st3(B.c_o, P, p, cam.pos);
-  st3(B.c_d, P, p, d);
-  st3(B.c_thr, P, p, v3(1.f, 1.f, 1.f));
-  B.c_dvcm[p] = static_cast<float>(P) / i2sa;
-  B.c_dvc[p] = 0.f;
-  B.c_len[p] = 1;
-  B.c_nspec[p] = 0;
-  B.c_ctr[p] = rng.ctr;
-  B.c_pix[p] = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
+  st3(B.c_o, P, l, cam.pos);
+  st3(B.c_d, P, l, d);
+  st3(B.c_thr, P, l, v3(1.f, 1.f, 1.f));
+  B.c_dvcm[l] = static_cast<float>(A.P) / i2sa;  // lightPathNum / cameraPdf
+  B.c_dvc[l] = 0.f;
+  B.c_len[l] = 1;
+  B.c_nspec[l] = 0;
+  B.c_ctr[l] = rng.ctr;
+  B.c_pix[l] = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
   st3(B.q_o[0], P, s, cam.pos + d * WR_EPS);
   st3(B.q_d[0], P, s, normalize(d));
-  B.q_path[0][s] = p;
-  return p;
+  B.q_path[0][s] = l;
+  return l;
 }
 __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGroup G_) {
   const BdptArgs& A = G_.a[blockIdx.y];
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < A.P; s += gridDim.x * blockDim.x) camera_gen_one(A, s);
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[kCamSlot] = A.P;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < A.n; s += gridDim.x * blockDim.x) camera_gen_one(A, s);
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[kCamSlot] = A.n;
 }
 
 // One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
@@ -298,7 +309,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGr
 __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, int bid, int nblk) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
-  const int P = A.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;
+  const int P = B.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;  // P: buffer stride
   const int n = A.sc->ext[slot];
   if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = nblk * blockDim.x;
@@ -355,7 +366,7 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
             }
           } else if (len < A.maxlen) {
             live = true;
-            Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), B.c_ctr[p]};
+            Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(A.base + p)), B.c_ctr[p]};
             if (!b.delta && len_ok(A.ctl, len + 1)) {  // getDirectIllumination (:205-217, :484-608)
               const float wlen = 1.f / (static_cast<float>(len) + 1.f - static_cast<float>(nspec));
               const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
@@ -505,7 +516,7 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
                   if (!black(res)) {
                     const float wl = cdpa * (B.v_dvcm[slot] + lrp * B.v_dvc[slot]);
                     const float wc = ldpa * (cdvcm + crp * cdvc);
-                    const float w = 1.f / (wl + 1.f + wc);
+                    const float w = WR_TEST_CONN_W / (wl + 1.f + wc);
                     const bool counts = len_ok(A.ctl, llen + 1 + len);
                     if (counts || A.faithful) {
                       shoot = true;
@@ -564,7 +575,7 @@ __device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int
   const DevScene& S = A.S;
   const BdptBuf::Sq& Q = B.sq[slot & 1];
   const BdptBuf::Di& D = B.di[slot & 1];
-  const int n = A.sc->sq[slot], cap = B.cap_sq, P = A.P;
+  const int n = A.sc->sq[slot], cap = B.cap_sq, P = B.P;  // P: buffer stride
   const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
   for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {

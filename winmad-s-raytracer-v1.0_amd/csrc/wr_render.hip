@@ -14,8 +14,10 @@
 // Work is keyed by (iteration, path index) through the counter RNG, never by the
 // device or launch geometry, so any sharding of iterations over GPUs renders the
 // same film up to float summation order.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -24,6 +26,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "winmad_rt.h"
@@ -434,6 +438,10 @@ struct wr_context {
   bool api_dense = false;         // test knob WR_TRACE_DENSE=1: API launches in TRACE_DENSE
   bool no_cut = false;            // WR_TRACE_NO_CUT=1: shadow rays run to the end (no occl_cut)
   bool timing = false;
+  // BDPT pieces (plan_pieces): at most piece_cap paths per buffer set, shares of
+  // at least piece_min paths per pipeline (env WR_PIECE_CAP / WR_PIECE_MIN)
+  int piece_cap = 1 << 21;
+  int piece_min = 16384;
   // verified-BVH traversal (wr_fast.h): built at wr_create for triangle scenes
   FastScene fs{};
   Arena fast_mem;
@@ -444,9 +452,71 @@ struct wr_context {
   float* api_t2 = nullptr;  // t2 scratch of the API path
   size_t api_t2_cap = 0;
   int2* api_spill = nullptr;  // the API path's search stack spill area
+  // ---- several GPUs (wr_create_multi): this context drives devices[0], `subs`
+  // the others; work is dealt to all of them and their films are summed on
+  // devices[0] (RCCL reduce over xGMI when the devices are distinct)
+  std::vector<wr_context*> subs;
+  std::vector<ncclComm_t> dev_comms;  // one per device (ncclCommInitAll), empty: peer copies
+  float* red_buf = nullptr;  // this device's film of a multi-device render
+  size_t red_n = 0;
+  float* stage_buf = nullptr;  // devices[0]: a peer film copied in before it is added
+  size_t stage_n = 0;
+  // ---- one process per GPU (wr_comm_init): this rank's communicator
+  ncclComm_t comm = nullptr;
+  int comm_ranks = 0, comm_rank = 0;
 };
 
 namespace {
+
+// RCCL, bound at first use: the copy already in the process (PyTorch's) when
+// its symbols are global, else ROCm's librccl.so.1.  Single-device contexts
+// never load it.
+struct RcclApi {
+  bool ok = false;
+  std::string why;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t,
+                         hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  const char* (*err_str)(ncclResult_t) = nullptr;
+};
+const RcclApi& rccl() {
+  static const RcclApi api = [] {
+    RcclApi a;
+    void* h = dlsym(RTLD_DEFAULT, "ncclCommInitRank") ? RTLD_DEFAULT : nullptr;
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* e = dlerror();
+      a.why = std::string("RCCL not loadable: ") + (e ? e : "librccl.so.1");
+      return a;
+    }
+    auto sym = [&](auto& f, const char* name) {
+      f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+      return f != nullptr;
+    };
+    a.ok = sym(a.get_unique_id, "ncclGetUniqueId") && sym(a.init_rank, "ncclCommInitRank") &&
+           sym(a.init_all, "ncclCommInitAll") && sym(a.reduce, "ncclReduce") && sym(a.group_start, "ncclGroupStart") &&
+           sym(a.group_end, "ncclGroupEnd") && sym(a.destroy, "ncclCommDestroy") && sym(a.err_str, "ncclGetErrorString");
+    if (!a.ok) a.why = "RCCL lacks an entry point";
+    return a;
+  }();
+  return api;
+}
+#define NCCLCHK(expr)                                                                           \
+  do {                                                                                          \
+    ncclResult_t r_ = (expr);                                                                   \
+    if (r_ != ncclSuccess) return fail(WR_E_HIP, std::string(#expr ": ") + rccl().err_str(r_)); \
+  } while (0)
+
+// films of a multi-device render, summed on devices[0] (peer-copy path)
+__global__ void __launch_bounds__(256) k_film_accumulate(float* dst, const float* src, size_t n) {
+  for (size_t i = blockIdx.x * size_t(256) + threadIdx.x; i < n; i += size_t(gridDim.x) * 256) dst[i] += src[i];
+}
 
 void layout_bdpt(Arena& a, BdptBuf& B, int P) {
   B.P = P;
@@ -851,6 +921,72 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
 
 int shade_grid(wr_context* c, int n) { return std::max(1, std::min(c->grid, (n + kShadeBlock - 1) / kShadeBlock)); }
 
+// ---- BDPT work split.  A render is iterations x (W*H) paths; light path i
+// pairs only with camera path i of the same iteration (:130, :222-229), MIS
+// uses the global lightPathNum (:55), and splats are film atomics, so any
+// partition of an iteration's path range renders the same film (up to the order
+// of float atomics).  The render's path-iterations, flattened iteration-major,
+// are split into one contiguous, equal share per pipeline (whole 8-row bands in
+// the tiled camera order); a share is cut at iteration boundaries and into
+// pieces of at most `cap` paths, and each pipeline runs its pieces in groups of
+// kGroup.  Few iterations then still fill every pipeline (the reference's own
+// default is 1 iteration, bidirPathTracing.cpp:9), and work buffers are sized by
+// the piece, not the frame.
+struct Piece {
+  int iter;  // iteration index within the render
+  int base;  // first global path
+  int n;     // paths
+};
+struct PiecePlan {
+  std::vector<std::vector<Piece>> per_pipe;
+  int pipes() const { return std::max(1, static_cast<int>(per_pipe.size())); }
+  int max_groups() const {
+    size_t m = 0;
+    for (const auto& v : per_pipe) m = std::max(m, v.size());
+    return static_cast<int>((m + kGroup - 1) / kGroup);
+  }
+};
+// a position in the flattened (iteration-major) path order, moved to the
+// nearest whole unit of its iteration (an iteration's end is a boundary)
+int64_t flat_round(int64_t f, int P, int unit) {
+  const int64_t it = f / P, off = f % P;
+  return it * P + std::min<int64_t>(P, (off + unit / 2) / unit * unit);
+}
+// the flattened path-iterations [lo, hi) (lo, hi whole units) over np pipelines
+PiecePlan plan_pieces(int64_t lo, int64_t hi, int P, int unit, int cap, int np, int min_piece) {
+  PiecePlan plan;
+  const int64_t T = hi - lo;
+  if (T <= 0) {
+    plan.per_pipe.resize(1);
+    return plan;
+  }
+  const int64_t shares = std::max<int64_t>(1, std::min<int64_t>(np, T / std::max(1, min_piece)));
+  auto bound = [&](int64_t k) { return k == shares ? hi : flat_round(lo + k * T / shares, P, unit); };
+  for (int64_t k = 0; k < shares; ++k) {
+    std::vector<Piece> mine;
+    for (int64_t a = bound(k), b = bound(k + 1); a < b;) {
+      const int64_t it = a / P, off = a % P;
+      const int64_t len = std::min<int64_t>(b - a, P - off);  // up to the iteration's end
+      const int64_t cuts = (len + cap - 1) / cap;
+      for (int64_t j = 0; j < cuts; ++j) {  // near-equal unit-aligned cuts of <= cap paths
+        int64_t lo_j = off + (len * j / cuts) / unit * unit, hi_j = off + (len * (j + 1) / cuts) / unit * unit;
+        if (j == cuts - 1) hi_j = off + len;
+        if (hi_j > lo_j) mine.push_back(Piece{static_cast<int>(it), static_cast<int>(lo_j), static_cast<int>(hi_j - lo_j)});
+      }
+      a += len;
+    }
+    if (!mine.empty()) plan.per_pipe.push_back(std::move(mine));
+  }
+  if (plan.per_pipe.empty()) plan.per_pipe.resize(1);
+  return plan;
+}
+// paths one buffer set holds: the frame, or WR_PIECE_CAP (default 2^21: a
+// 1920x1080 frame is one piece, 4K frames are four) rounded up to whole units
+int piece_capacity(const wr_context* c, int P, int unit) {
+  const int64_t want = std::min<int64_t>(P, std::max<int64_t>(unit, c->piece_cap));
+  return static_cast<int>(std::min<int64_t>(P, (want + unit - 1) / unit * unit));
+}
+
 double host_now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1020,6 +1156,23 @@ int wr_scene_load(const char* path, wr_scene** out) {
   return WR_OK;
 }
 
+int wr_scene_from_desc(const wr_scene_desc* d, wr_scene** out) {
+  if (!d || !out) return fail(WR_E_ARG, "null argument");
+  *out = nullptr;
+  auto* s = new (std::nothrow) wr_scene();
+  if (!s) return fail(WR_E_ARG, "out of host memory");
+  wr::SceneArrays a{d->n_prims, d->prim_type, d->prim_data, d->prim_mat, d->n_lights, d->light_tri, d->light_le,
+                    d->n_materials, d->materials, d->cam_pos, d->cam_fwd, d->cam_up, d->cam_xres, d->cam_yres,
+                    d->cam_hfov};
+  std::string err;
+  if (!wr::scene_from_arrays(a, s->s, err)) {
+    delete s;
+    return fail(WR_E_ARG, err);
+  }
+  *out = s;
+  return WR_OK;
+}
+
 int wr_scene_info_get(const wr_scene* sc, wr_scene_info* o) {
   if (!sc || !o) return fail(WR_E_ARG, "null argument");
   const wr::Scene& s = sc->s;
@@ -1106,6 +1259,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     c->npipes = std::max(1, std::min(kMaxPipes, hwq));
   }
   if (const char* e = std::getenv("WR_PIPES")) c->npipes = std::max(1, std::min(kMaxPipes, std::atoi(e)));
+  if (const char* e = std::getenv("WR_PIECE_CAP")) c->piece_cap = std::max(64, std::atoi(e));
+  if (const char* e = std::getenv("WR_PIECE_MIN")) c->piece_min = std::max(1, std::atoi(e));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
     // grid-stride vertex / resolve kernels: blocks per CU (knob WR_SHADE_GRID).
@@ -1408,17 +1563,25 @@ int wr_set_trace_mode(wr_context* c, int mode) {
   if (!c || (mode != WR_TRACE_REFERENCE && mode != WR_TRACE_BVH)) return fail(WR_E_ARG, "bad trace mode");
   if (mode == WR_TRACE_BVH && !c->fast_ok) return fail(WR_E_SCENE, "the BVH mode covers triangle scenes only");
   c->fast_on = mode == WR_TRACE_BVH;
+  for (wr_context* d : c->subs) d->fast_on = c->fast_on;
   return WR_OK;
 }
 
 int wr_set_pipelines(wr_context* c, int n) {
   if (!c || n < 1 || n > kMaxPipes) return fail(WR_E_ARG, "pipelines must be in 1.." + std::to_string(kMaxPipes));
   c->npipes = n;
+  for (wr_context* d : c->subs) d->npipes = n;
   return WR_OK;
 }
 
 void wr_destroy(wr_context* c) {
   if (!c) return;
+  for (wr_context* d : c->subs) wr_destroy(d);
+  c->subs.clear();
+  for (ncclComm_t m : c->dev_comms) (void)rccl().destroy(m);
+  c->dev_comms.clear();
+  if (c->comm) (void)rccl().destroy(c->comm);
+  c->comm = nullptr;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (Pipe& p : c->pipes) {
@@ -1440,6 +1603,8 @@ void wr_destroy(wr_context* c) {
     if (p.t2buf) (void)hipFree(p.t2buf);
     if (p.spill) (void)hipFree(p.spill);
   }
+  if (c->red_buf) (void)hipFree(c->red_buf);
+  if (c->stage_buf) (void)hipFree(c->stage_buf);
   c->fast_mem.release();
   c->scene_mem.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1515,14 +1680,53 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   return WR_OK;
 }
 
+extern "C++" {
+// ---- several devices: run fn(device context, index) on every device of c at
+// once (devices[0] on the calling thread), first error wins
+template <class Fn>
+static int for_each_device(wr_context* c, Fn fn) {
+  std::vector<wr_context*> dev{c};
+  dev.insert(dev.end(), c->subs.begin(), c->subs.end());
+  const int n = static_cast<int>(dev.size());
+  std::vector<int> rc(n, WR_OK);
+  std::vector<std::string> msg(n);
+  std::vector<std::thread> th;
+  for (int k = 1; k < n; ++k)
+    th.emplace_back([&, k] {
+      rc[k] = fn(dev[k], k);
+      if (rc[k] != WR_OK) msg[k] = wr::last_error();
+    });
+  rc[0] = fn(dev[0], 0);
+  if (rc[0] != WR_OK) msg[0] = wr::last_error();
+  for (auto& t : th) t.join();
+  for (int k = 0; k < n; ++k)
+    if (rc[k] != WR_OK) return fail(rc[k], "device " + std::to_string(dev[k]->device) + ": " + msg[k]);
+  return WR_OK;
+}
+
+}  // extern "C++"
+
+static int trace_multi(wr_context* c, const wr_ray* rays, const float* targets, int64_t n, wr_hit* hits,
+                       uint8_t* occ) {
+  if (c->subs.empty() || n < 1024) return trace_api(c, rays, targets, n, hits, occ);
+  const int64_t nd = 1 + static_cast<int64_t>(c->subs.size());
+  return for_each_device(c, [&](wr_context* d, int k) {  // contiguous ray ranges
+    const int64_t lo = n * k / nd, hi = n * (k + 1) / nd;
+    return trace_api(d, rays + lo, targets ? targets + 3 * lo : nullptr, hi - lo, hits ? hits + lo : nullptr,
+                     occ ? occ + lo : nullptr);
+  });
+}
+
 int wr_trace_closest(wr_context* c, const wr_ray* rays, int64_t n, wr_hit* hits) {
   if (!hits && n) return fail(WR_E_ARG, "null hits");
-  return trace_api(c, rays, nullptr, n, hits, nullptr);
+  if (!c || (!rays && n) || n < 0) return fail(WR_E_ARG, "bad argument");
+  return trace_multi(c, rays, nullptr, n, hits, nullptr);
 }
 
 int wr_occluded(wr_context* c, const wr_ray* rays, const float* targets, int64_t n, uint8_t* occluded) {
   if ((!targets || !occluded) && n) return fail(WR_E_ARG, "null targets / output");
-  return trace_api(c, rays, targets, n, nullptr, occluded);
+  if (!c || (!rays && n) || n < 0) return fail(WR_E_ARG, "bad argument");
+  return trace_multi(c, rays, targets, n, nullptr, occluded);
 }
 
 static int film_target(wr_context* c, float* film, int film_on_device, size_t nfloat, float** dev) {
@@ -1551,7 +1755,7 @@ static int film_return(wr_context* c, float* film, int film_on_device, size_t nf
   return WR_OK;
 }
 
-int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int film_on_device, wr_stats* st) {
+static int check_bdpt(const wr_context* c, const wr_bdpt_params* prm, const float* film) {
   if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
   if (prm->width <= 0 || prm->height <= 0 || prm->iterations < 0) return fail(WR_E_ARG, "bad film size");
   if (static_cast<int64_t>(prm->width) * prm->height >= (1 << 30) / (kVMax + 2))
@@ -1559,16 +1763,30 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
   if (prm->max_path_length > kVMax + 1)
     return fail(WR_E_ARG, "max_path_length > 10 is not supported (light-vertex store sized for the reference's 10)");
   if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "BDPT needs at least one area light");
+  return WR_OK;
+}
+// camera-order unit of a BDPT piece: whole 8-row bands when the film is tiled
+// (camera_gen_one), else 64 paths
+static int bdpt_unit(const wr_bdpt_params* prm) {
+  return ((prm->width % 8) == 0 && (prm->height % 8) == 0) ? 8 * prm->width : 64;
+}
+// One device: the flattened path-iterations [f_lo, f_hi) of the render
+// (iteration iter_begin + f / P, path f % P; whole units).
+static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_lo, int64_t f_hi, float* film,
+                           int film_on_device, wr_stats* st) {
   HIPCHK(hipSetDevice(c->device));
   const double t0 = host_now();
   const int P = prm->width * prm->height;
-  const int ngroups = (prm->iterations + kGroup - 1) / kGroup;
-  const int fit = pipelines_that_fit(c, 1, P, kGroup, c->npipes);
+  // pieces of (iteration, path range) per pipeline, buffers sized for the largest
+  const int unit = bdpt_unit(prm);
+  const int cap = piece_capacity(c, P, unit);
+  const int fit = pipelines_that_fit(c, 1, cap, kGroup, c->npipes);
   if (fit < 1) return WR_E_HIP;  // message set by the allocation
-  const int np = std::max(1, std::min(fit, ngroups));
+  const PiecePlan plan = plan_pieces(f_lo, f_hi, P, unit, cap, fit, c->piece_min);
+  const int np = plan.pipes();
   {  // WR_TRACE_BVH t2 scratch: a launch takes <= kGroup x (shadow / aux + extension) queues
     const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
-    const size_t per = kGroup * (std::max(cap_sq, size_t(P)) + size_t(P));
+    const size_t per = kGroup * (std::max(cap_sq, size_t(cap)) + size_t(cap));
     for (int i = 0; i < np; ++i)
       if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
   }
@@ -1588,69 +1806,79 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
   A0.faithful = prm->faithful;
   const int maxlen = A0.maxlen;
   const bool count = prm->count_work != 0;
-  const int g = shade_grid(c, P);
-  for (int gi = 0; gi < ngroups; ++gi) {
-    // a group of gn iterations in lockstep on pipeline gi % np
-    Pipe& pp = c->pipes[gi % np];
-    const hipStream_t sm = pp.stream;
-    Timer tm(c, &pp);
-    const int it0 = gi * kGroup, gn = std::min(kGroup, prm->iterations - it0);
-    BdptGroup GA;
-    BdptArgs* A = GA.a;
-    for (int m = 0; m < gn; ++m) {
-      A[m] = A0;
-      A[m].B = pp.bb[m];
-      A[m].ctr = pp.ctr;
-      A[m].sc = pp.sc + m;
-      A[m].iter = static_cast<uint32_t>(prm->iter_begin + it0 + m);
+  // groups are issued round-robin over the pipelines (each stream runs its own
+  // in order), so every pipeline has work queued from the start
+  for (int r = 0; r < plan.max_groups(); ++r)
+    for (int pi = 0; pi < np; ++pi) {
+      const std::vector<Piece>& mine = plan.per_pipe[pi];
+      const int first = r * kGroup;
+      if (first >= static_cast<int>(mine.size())) continue;
+      const int gn = std::min<int>(kGroup, static_cast<int>(mine.size()) - first);
+      Pipe& pp = c->pipes[pi];
+      const hipStream_t sm = pp.stream;
+      Timer tm(c, &pp);
+      BdptGroup GA;
+      BdptArgs* A = GA.a;
+      int nmax = 0;
+      for (int m = 0; m < gn; ++m) {
+        const Piece& pc = mine[first + m];
+        A[m] = A0;
+        A[m].B = pp.bb[m];
+        A[m].ctr = pp.ctr;
+        A[m].sc = pp.sc + m;
+        A[m].iter = static_cast<uint32_t>(prm->iter_begin + pc.iter);
+        A[m].base = pc.base;
+        A[m].n = pc.n;
+        nmax = std::max(nmax, pc.n);
+      }
+      auto sq = [&](int m, int slot) {
+        const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
+        return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut);
+      };
+      auto ext = [&](int m, int slot) {
+        const BdptBuf& B = pp.bb[m];
+        const int q = slot & 1;
+        return rq(B.q_o[q], B.q_d[q], B.P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
+      };
+      const int sq_max = nmax * (kVMax + 2);  // <= cap_sq
+      const int g = shade_grid(c, nmax);
+      HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
+      // ---------------- light pass (:67-131)
+      hipLaunchKernelGGL(k_light_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
+      tm.mark(WR_K_GEN);
+      for (int b = 0; b < maxlen - 1; ++b) {
+        QueueList ql;
+        for (int m = 0; m < gn; ++m) ql.add(ext(m, b), A[m].n);
+        trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
+        hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
+        tm.mark(WR_K_SHADE);
+      }
+      // ---------------- camera pass (:133-264).  The light pass's splat rays
+      // (connectToCamera) ride along with the primary rays; afterwards each
+      // bounce's shadow / aux rays ride along with the next bounce's extension rays.
+      hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
+      tm.mark(WR_K_GEN);
+      for (int b = 0; b <= maxlen; ++b) {
+        const int slot = kCamSlot + b;
+        const bool more = b < maxlen;  // extension rays of bounce b exist
+        QueueList ql;
+        for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), A[m].n * (kVMax + 2));
+        if (more)
+          for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), A[m].n);
+        trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
+        // resolve this step's shadow / aux rays and shade its vertices in one launch
+        const int nres = shade_grid(c, sq_max);
+        hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot, nres,
+                           more ? 1 : 0);
+        tm.mark(WR_K_SHADE);
+      }
     }
-    auto sq = [&](int m, int slot) {
-      const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
-      return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut);
-    };
-    auto ext = [&](int m, int slot) {
-      const BdptBuf& B = pp.bb[m];
-      const int q = slot & 1;
-      return rq(B.q_o[q], B.q_d[q], P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
-    };
-    const int sq_max = pp.bb[0].cap_sq;
-    HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
-    // ---------------- light pass (:67-131)
-    hipLaunchKernelGGL(k_light_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
-    tm.mark(WR_K_GEN);
-    for (int b = 0; b < maxlen - 1; ++b) {
-      QueueList ql;
-      for (int m = 0; m < gn; ++m) ql.add(ext(m, b), P);
-      trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
-      hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
-      tm.mark(WR_K_SHADE);
-    }
-    // ---------------- camera pass (:133-264).  The light pass's splat rays
-    // (connectToCamera) ride along with the primary rays; afterwards each
-    // bounce's shadow / aux rays ride along with the next bounce's extension rays.
-    hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
-    tm.mark(WR_K_GEN);
-    for (int b = 0; b <= maxlen; ++b) {
-      const int slot = kCamSlot + b;
-      const bool more = b < maxlen;  // extension rays of bounce b exist
-      QueueList ql;
-      for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), sq_max);
-      if (more)
-        for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), P);
-      trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
-      // resolve this step's shadow / aux rays and shade its vertices in one launch
-      const int nres = shade_grid(c, sq_max);
-      hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot, nres,
-                         more ? 1 : 0);
-      tm.mark(WR_K_SHADE);
-    }
-  }
   HIPCHK(hipGetLastError());
   if (int rc = finish_render(c, np, st, t0)) return rc;
   return film_return(c, film, film_on_device, nf);
 }
 
-int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film_on_device, wr_stats* st) {
+static int check_vcm(const wr_context* c, const wr_vcm_params* prm, const float* film) {
   if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
   if (prm->width <= 0 || prm->height <= 0 || prm->iterations < 0) return fail(WR_E_ARG, "bad film size");
   if (static_cast<int64_t>(prm->width) * prm->height >= (1 << 30) / (kVMax + 2))
@@ -1660,6 +1888,9 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
   if (prm->min_path_length < 0 || !(prm->radius_factor > 0.f) || !(prm->radius_alpha <= 1.f))
     return fail(WR_E_ARG, "bad min_path_length / radius_factor / radius_alpha");
   if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "VCM needs at least one area light");
+  return WR_OK;
+}
+static int render_vcm_one(wr_context* c, const wr_vcm_params* prm, float* film, int film_on_device, wr_stats* st) {
   HIPCHK(hipSetDevice(c->device));
   const double t0 = host_now();
   const int P = prm->width * prm->height;
@@ -1688,6 +1919,10 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
   A0.ctl = 0;
   A0.maxlen = prm->max_path_length;
   A0.faithful = 1;
+  // VCM renders whole iterations: every camera vertex merges with the light
+  // vertices of the whole iteration (:152, :265-276)
+  A0.base = 0;
+  A0.n = P;
   X0.minlen = prm->min_path_length;
   X0.N = static_cast<float>(prm->height * prm->width);
   X0.org = c->ds.root_l;
@@ -1787,12 +2022,15 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
   return film_return(c, film, film_on_device, nf);
 }
 
-int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max_depth, uint32_t seed,
-                     int32_t sample, float* rgb, wr_stats* st) {
+static int check_radiance(const wr_context* c, const wr_ray* rays, int64_t n64, int32_t max_depth, const float* rgb) {
   if (!c || ((!rays || !rgb) && n64) || n64 < 0) return fail(WR_E_ARG, "bad argument");
   if (max_depth < 0 || max_depth > kSlots - 3) return fail(WR_E_ARG, "max_depth must be in 0..61");
   if (n64 > (1 << 26)) return fail(WR_E_ARG, "at most 2^26 rays per call");
   if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "path tracing needs at least one area light");
+  return WR_OK;
+}
+static int path_radiance_one(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max_depth, uint32_t seed,
+                             int32_t sample, float* rgb, wr_stats* st) {
   if (n64 == 0) return WR_OK;
   HIPCHK(hipSetDevice(c->device));
   const double t0 = host_now();
@@ -1846,7 +2084,7 @@ int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max
   return film_return(c, rgb, 0, nf);
 }
 
-int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int film_on_device, wr_stats* st) {
+static int check_path(const wr_context* c, const wr_path_params* prm, const float* film) {
   if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
   if (prm->width <= 0 || prm->height <= 0 || prm->spp <= 0) return fail(WR_E_ARG, "bad film size / spp");
   // path-state arrays are indexed up to 3 * P in 32-bit ints
@@ -1859,6 +2097,9 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
       prm->sample_begin > prm->spp)
     return fail(WR_E_ARG, "samples [sample_begin, sample_begin + sample_count) must lie in [0, spp)");
   if (c->ds.nlights <= 0) return fail(WR_E_SCENE, "path tracing needs at least one area light");
+  return WR_OK;
+}
+static int render_path_one(wr_context* c, const wr_path_params* prm, float* film, int film_on_device, wr_stats* st) {
   HIPCHK(hipSetDevice(c->device));
   const double t0 = host_now();
   const int P = prm->width * prm->height;
@@ -1938,5 +2179,275 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
   return film_return(c, film, film_on_device, nf);
 }
 
+
+// ---- multi-device renders (wr_create_multi)
+static void add_stats(wr_stats* d, const wr_stats& s) {
+  d->closest_rays += s.closest_rays;
+  d->shadow_rays += s.shadow_rays;
+  d->inner_visits += s.inner_visits;
+  d->leaf_visits += s.leaf_visits;
+  d->prim_refs += s.prim_refs;
+  for (int k = 0; k < WR_K_NUM; ++k) {
+    d->kernel_ms[k] += s.kernel_ms[k];
+    d->kernel_launches[k] += s.kernel_launches[k];
+  }
+  d->vm_queries += s.vm_queries;
+  d->vm_found += s.vm_found;
+  d->vm_merged += s.vm_merged;
+  d->prim_tests += s.prim_tests;
+  d->bvh_nodes += s.bvh_nodes;
+  d->bvh_tests += s.bvh_tests;
+  d->kd_replay_steps += s.kd_replay_steps;
+  d->fallback_rays += s.fallback_rays;
+  d->verify_rays += s.verify_rays;
+  d->verify_mismatches += s.verify_mismatches;
+}
+
+static int ensure_dev_film(wr_context* d, float** buf, size_t* have, size_t nf) {
+  if (*have >= nf) return WR_OK;
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *have = 0;
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipMalloc(buf, nf * sizeof(float)));
+  *have = nf;
+  return WR_OK;
+}
+
+// films[k] (on device k) summed into films[0]: one RCCL reduce over the
+// devices' communicators, or peer copies to devices[0] + an add kernel
+static int reduce_films(wr_context* c, const std::vector<wr_context*>& dev, const std::vector<float*>& films,
+                        size_t nf) {
+  const int n = static_cast<int>(dev.size());
+  if (n == 1) return WR_OK;
+  if (static_cast<int>(c->dev_comms.size()) == n) {
+    NCCLCHK(rccl().group_start());
+    for (int k = 0; k < n; ++k) {
+      HIPCHK(hipSetDevice(dev[k]->device));
+      // in place on the root; the receive buffer is ignored elsewhere
+      NCCLCHK(rccl().reduce(films[k], films[k], nf, ncclFloat32, ncclSum, 0, c->dev_comms[k], dev[k]->stream));
+    }
+    NCCLCHK(rccl().group_end());
+    for (int k = 0; k < n; ++k) {
+      HIPCHK(hipSetDevice(dev[k]->device));
+      HIPCHK(hipStreamSynchronize(dev[k]->stream));
+    }
+    return WR_OK;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const int g = static_cast<int>(std::min<size_t>(4096, (nf + 255) / 256));
+  for (int k = 1; k < n; ++k) {
+    const float* src = films[k];
+    if (dev[k]->device != c->device) {
+      if (int rc = ensure_dev_film(c, &c->stage_buf, &c->stage_n, nf)) return rc;
+      HIPCHK(hipMemcpyPeerAsync(c->stage_buf, c->device, films[k], dev[k]->device, nf * sizeof(float), c->stream));
+      src = c->stage_buf;
+    }
+    hipLaunchKernelGGL(k_film_accumulate, dim3(g), dim3(256), 0, c->stream, films[0], src, nf);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WR_OK;
+}
+
+extern "C++" {
+// Every device renders its share (fn) into a film of its own (devices[0]:
+// the caller's device film, if given), the films are summed on devices[0],
+// and a host film gets the sum added.  Stats: counts summed, seconds = the
+// call's wall time, trace_wall_ms = the largest device's.
+template <class Fn>
+static int multi_render(wr_context* c, size_t nf, float* film, int film_on_device, wr_stats* st, Fn fn) {
+  const double t0 = host_now();
+  std::vector<wr_context*> dev{c};
+  dev.insert(dev.end(), c->subs.begin(), c->subs.end());
+  const int n = static_cast<int>(dev.size());
+  std::vector<float*> buf(n, nullptr);
+  for (int k = 0; k < n; ++k) {
+    if (k == 0 && film_on_device) {
+      buf[0] = film;
+      continue;
+    }
+    if (int rc = ensure_dev_film(dev[k], &dev[k]->red_buf, &dev[k]->red_n, nf)) return rc;
+    HIPCHK(hipMemsetAsync(dev[k]->red_buf, 0, nf * sizeof(float), dev[k]->stream));
+    buf[k] = dev[k]->red_buf;
+  }
+  std::vector<wr_stats> s(n);
+  for (auto& x : s) std::memset(&x, 0, sizeof x);
+  if (int rc = for_each_device(c, [&](wr_context* d, int k) { return fn(d, k, n, buf[k], &s[k]); })) return rc;
+  if (int rc = reduce_films(c, dev, buf, nf)) return rc;
+  if (!film_on_device) {
+    std::vector<float> tmp(nf);
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(tmp.data(), buf[0], nf * sizeof(float), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nf; ++i) film[i] = film[i] + tmp[i];
+  }
+  if (st) {
+    double wall = 0.0;
+    for (const auto& x : s) {
+      add_stats(st, x);
+      wall = std::max(wall, x.trace_wall_ms);
+    }
+    st->trace_wall_ms += wall;
+    st->seconds += host_now() - t0;
+  }
+  return WR_OK;
+}
+
+}  // extern "C++"
+
+int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int film_on_device, wr_stats* st) {
+  if (int rc = check_bdpt(c, prm, film)) return rc;
+  const int P = prm->width * prm->height;
+  const int64_t T = static_cast<int64_t>(prm->iterations) * P;
+  if (c->subs.empty()) return render_bdpt_one(c, prm, 0, T, film, film_on_device, st);
+  // devices take equal contiguous shares of the flattened path-iterations:
+  // a single iteration (the reference's default, bidirPathTracing.cpp:9)
+  // still spreads over every device
+  const int unit = bdpt_unit(prm);
+  return multi_render(c, size_t(P) * 3, film, film_on_device, st,
+                      [&](wr_context* d, int k, int n, float* buf, wr_stats* s) {
+                        const int64_t lo = k == 0 ? 0 : flat_round(T * k / n, P, unit);
+                        const int64_t hi = k == n - 1 ? T : flat_round(T * (k + 1) / n, P, unit);
+                        return render_bdpt_one(d, prm, lo, hi, buf, 1, s);
+                      });
+}
+
+int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film_on_device, wr_stats* st) {
+  if (int rc = check_vcm(c, prm, film)) return rc;
+  if (c->subs.empty()) return render_vcm_one(c, prm, film, film_on_device, st);
+  // whole iterations per device: an iteration's merge grid holds all of its
+  // light vertices (vertexcm.cpp:152)
+  const int I = prm->iterations;
+  return multi_render(c, size_t(prm->width) * prm->height * 3, film, film_on_device, st,
+                      [&](wr_context* d, int k, int n, float* buf, wr_stats* s) {
+                        wr_vcm_params q = *prm;
+                        const int lo = I * k / n, hi = I * (k + 1) / n;
+                        if (hi <= lo) return static_cast<int>(WR_OK);
+                        q.iter_begin = prm->iter_begin + lo;
+                        q.iterations = hi - lo;
+                        return render_vcm_one(d, &q, buf, 1, s);
+                      });
+}
+
+int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int film_on_device, wr_stats* st) {
+  if (int rc = check_path(c, prm, film)) return rc;
+  if (c->subs.empty()) return render_path_one(c, prm, film, film_on_device, st);
+  const int k0 = prm->sample_begin, k1 = prm->sample_count > 0 ? k0 + prm->sample_count : prm->spp;
+  return multi_render(c, size_t(prm->width) * prm->height * 3, film, film_on_device, st,
+                      [&](wr_context* d, int k, int n, float* buf, wr_stats* s) {
+                        wr_path_params q = *prm;  // contiguous sample ranges of the spp grid
+                        const int lo = k0 + (k1 - k0) * k / n, hi = k0 + (k1 - k0) * (k + 1) / n;
+                        if (hi <= lo) return static_cast<int>(WR_OK);
+                        q.sample_begin = lo;
+                        q.sample_count = hi - lo;
+                        return render_path_one(d, &q, buf, 1, s);
+                      });
+}
+
+int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max_depth, uint32_t seed,
+                     int32_t sample, float* rgb, wr_stats* st) {
+  if (int rc = check_radiance(c, rays, n64, max_depth, rgb)) return rc;
+  return path_radiance_one(c, rays, n64, max_depth, seed, sample, rgb, st);  // devices[0]
+}
+
+int wr_create_multi(const wr_scene* sc, const int* devices, int n, wr_context** out) {
+  if (!sc || !devices || !out || n < 1 || n > 64) return fail(WR_E_ARG, "bad argument (1..64 devices)");
+  *out = nullptr;
+  if (int rc = check_device()) return rc;
+  int have = 0;
+  (void)hipGetDeviceCount(&have);
+  for (int k = 0; k < n; ++k)
+    if (devices[k] < 0 || devices[k] >= have)
+      return fail(WR_E_ARG, "device " + std::to_string(devices[k]) + " not visible (" + std::to_string(have) + ")");
+  // one context per device, created concurrently (scene upload + BVH build each)
+  std::vector<wr_context*> ctx(n, nullptr);
+  std::vector<int> rc(n, WR_OK);
+  std::vector<std::string> msg(n);
+  {
+    std::vector<std::thread> th;
+    for (int k = 0; k < n; ++k)
+      th.emplace_back([&, k] {
+        rc[k] = wr_create(sc, devices[k], &ctx[k]);
+        if (rc[k] != WR_OK) msg[k] = wr::last_error();
+      });
+    for (auto& t : th) t.join();
+  }
+  for (int k = 0; k < n; ++k)
+    if (rc[k] != WR_OK) {
+      for (wr_context* x : ctx) wr_destroy(x);
+      return fail(rc[k], "device " + std::to_string(devices[k]) + ": " + msg[k]);
+    }
+  wr_context* c = ctx[0];
+  c->subs.assign(ctx.begin() + 1, ctx.end());
+  // RCCL communicators over the devices when they are distinct (a device
+  // listed twice -- tests on one GPU -- sums by copies); WR_MULTI_REDUCE=peer
+  // forces the copies
+  bool distinct = true;
+  for (int a = 0; a < n; ++a)
+    for (int b = a + 1; b < n; ++b) distinct = distinct && devices[a] != devices[b];
+  const char* mode = std::getenv("WR_MULTI_REDUCE");
+  const bool want = !(mode && std::string(mode) == "peer");
+  if (n > 1 && distinct && want) {
+    if (!rccl().ok) {
+      wr_destroy(c);
+      return fail(WR_E_HIP, rccl().why);
+    }
+    std::vector<ncclComm_t> comms(n, nullptr);
+    const ncclResult_t r = rccl().init_all(comms.data(), n, devices);
+    if (r != ncclSuccess) {
+      wr_destroy(c);
+      return fail(WR_E_HIP, std::string("ncclCommInitAll: ") + rccl().err_str(r));
+    }
+    c->dev_comms = comms;
+  }
+  *out = c;
+  return WR_OK;
+}
+
+int wr_context_devices(const wr_context* c, int* devices, int max_n) {
+  if (!c || max_n < 0 || (max_n > 0 && !devices)) return fail(WR_E_ARG, "bad argument");
+  const int n = 1 + static_cast<int>(c->subs.size());
+  for (int k = 0; k < n && k < max_n; ++k) devices[k] = k == 0 ? c->device : c->subs[k - 1]->device;
+  return n;
+}
+
+// ---- one process per GPU: this rank's RCCL communicator and the film reduce
+int wr_comm_unique_id(uint8_t id[128]) {
+  if (!id) return fail(WR_E_ARG, "null argument");
+  if (!rccl().ok) return fail(WR_E_HIP, rccl().why);
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  ncclUniqueId u;
+  NCCLCHK(rccl().get_unique_id(&u));
+  std::memcpy(id, &u, sizeof u);
+  return WR_OK;
+}
+
+int wr_comm_init(wr_context* c, const uint8_t id[128], int nranks, int rank) {
+  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(WR_E_ARG, "bad argument");
+  if (!c->subs.empty()) return fail(WR_E_ARG, "a multi-device context reduces over its own devices");
+  if (!rccl().ok) return fail(WR_E_HIP, rccl().why);
+  HIPCHK(hipSetDevice(c->device));
+  if (c->comm) (void)rccl().destroy(c->comm);
+  c->comm = nullptr;
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  NCCLCHK(rccl().init_rank(&c->comm, nranks, u, rank));
+  c->comm_ranks = nranks;
+  c->comm_rank = rank;
+  return WR_OK;
+}
+
+int wr_film_reduce(wr_context* c, float* film, int64_t nfloat, int root) {
+  if (!c || (!film && nfloat) || nfloat < 0) return fail(WR_E_ARG, "bad argument");
+  if (!c->comm) return fail(WR_E_ARG, "no communicator: call wr_comm_init first");
+  if (root < 0 || root >= c->comm_ranks) return fail(WR_E_ARG, "bad root rank");
+  HIPCHK(hipSetDevice(c->device));
+  // ordered after the caller's work on the legacy null stream, like a render
+  (void)hipEventRecord(c->t_null, nullptr);
+  (void)hipStreamWaitEvent(c->stream, c->t_null, 0);
+  NCCLCHK(rccl().reduce(film, film, static_cast<size_t>(nfloat), ncclFloat32, ncclSum, root, c->comm, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return WR_OK;
+}
 
 }  // extern "C"

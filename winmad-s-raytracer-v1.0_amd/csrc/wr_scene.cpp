@@ -764,6 +764,52 @@ bool load_scene(const char* path, Scene& s, std::string& err) {
   return true;
 }
 
+bool scene_from_arrays(const SceneArrays& a, Scene& s, std::string& err) {
+  if (a.n_prims < 0 || a.n_lights < 0 || a.n_materials < 0) {
+    err = "negative count";
+    return false;
+  }
+  if ((a.n_prims && (!a.prim_type || !a.prim_data || !a.prim_mat)) || (a.n_lights && (!a.light_tri || !a.light_le)) ||
+      (a.n_materials && !a.materials)) {
+    err = "null array with a nonzero count";
+    return false;
+  }
+  s = Scene();
+  auto v = [](const float* q) { return f3(q[0], q[1], q[2]); };
+  for (int i = 0; i < a.n_materials; ++i) {  // scene.cpp:305-332
+    const float* m = a.materials + 11 * static_cast<size_t>(i);
+    s.mats.push_back(Material{v(m), v(m + 3), v(m + 6), m[9], m[10]});
+  }
+  for (int i = 0; i < a.n_lights; ++i) {  // AreaLight(p0, p1, p2, intensity) (light.h:90-103)
+    const float* t = a.light_tri + 9 * static_cast<size_t>(i);
+    s.lights.push_back(make_light(v(t), v(t + 3), v(t + 6), v(a.light_le + 3 * static_cast<size_t>(i))));
+  }
+  for (int i = 0; i < a.n_prims; ++i) {  // Scene::addGeometry in objs order (scene.cpp:5-9)
+    const float* q = a.prim_data + 9 * static_cast<size_t>(i);
+    const int mat = a.prim_mat[i];
+    if (mat < 0 && -mat - 1 >= a.n_lights) {
+      err = "primitive " + std::to_string(i) + ": emitter matId " + std::to_string(mat) + " names no area light";
+      return false;
+    }
+    if (a.prim_type[i] == kTri) {
+      add_prim(s, make_tri(v(q), v(q + 3), v(q + 6), mat));
+    } else if (a.prim_type[i] == kSphere) {
+      if (!(q[3] > 0.f)) {
+        err = "primitive " + std::to_string(i) + ": sphere radius must be > 0";
+        return false;
+      }
+      add_prim(s, make_sphere(v(q), q[3], mat));
+    } else {
+      err = "primitive " + std::to_string(i) + ": type must be 0 (triangle) or 1 (sphere)";
+      return false;
+    }
+  }
+  setup_camera(s.cam, v(a.cam_pos), v(a.cam_fwd), v(a.cam_up), a.cam_xres, a.cam_yres, a.cam_hfov);
+  s.has_camera = true;
+  build_kdtree(s);
+  return true;
+}
+
 namespace {
 void hx(std::string& o, float v) {
   char b[40];

@@ -77,6 +77,25 @@ struct Scene {
 // reference (tiny_obj_loader.cpp:467-474) and counted in missing_files.
 bool load_scene(const char* path, Scene& out, std::string& err);
 
+// The reference's in-memory Scene (scene.h:35-42) as flat arrays
+// (wr_scene_desc of include/winmad_rt.h): primitives in objs order, area
+// lights, materials, and Camera::setup's arguments.  The KD tree is built
+// here, as Scene::init does after loading (scene.cpp:469-489).
+struct SceneArrays {
+  int n_prims;
+  const int* prim_type;    // kTri / kSphere
+  const float* prim_data;  // 9 per primitive: p0 p1 p2 | centre, radius
+  const int* prim_mat;
+  int n_lights;
+  const float* light_tri;  // 9 per light: p0 p1 p2
+  const float* light_le;   // 3 per light
+  int n_materials;
+  const float* materials;  // 11 per material: diffuse, phong, specular, phongExp, refracIndex
+  const float *cam_pos, *cam_fwd, *cam_up;
+  float cam_xres, cam_yres, cam_hfov;
+};
+bool scene_from_arrays(const SceneArrays& a, Scene& out, std::string& err);
+
 // The reference's tree, built with its exact SAH sweep, event order and
 // straddler clipping, but freeing each node's event lists as soon as the
 // children own theirs.

@@ -33,10 +33,21 @@ def pt_sample_range(rank, world, spp):
     return begin, q + (1 if rank < r else 0)
 
 
+def _host_backend(dist):
+    """gloo reduces host tensors only: device films go through host memory."""
+    return dist.get_backend() == "gloo"
+
+
 def reduce_film(film, dist, dst=0):
     """Sum the ranks' films into rank `dst` (in place there)."""
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.reduce(film, dst=dst, op=dist.ReduceOp.SUM)
+        if _host_backend(dist) and film.device.type != "cpu":
+            h = film.cpu()
+            dist.reduce(h, dst=dst, op=dist.ReduceOp.SUM)
+            if dist.get_rank() == dst:
+                film.copy_(h)
+        else:
+            dist.reduce(film, dst=dst, op=dist.ReduceOp.SUM)
     return film
 
 
@@ -46,6 +57,8 @@ def job_totals(elapsed_s, rays, dist, device="cpu"):
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return float(elapsed_s), float(rays)
     import torch
+    if _host_backend(dist):
+        device = "cpu"
     t = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     r = torch.tensor([float(rays)], dtype=torch.float64, device=device)

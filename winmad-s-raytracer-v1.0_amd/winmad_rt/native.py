@@ -18,10 +18,12 @@ K_TRACE, K_SHADE, K_RESOLVE, K_GEN, K_OTHER = 0, 1, 2, 3, 4
 TRACE_REFERENCE, TRACE_BVH = 0, 1
 
 # every entry point declared in include/winmad_rt.h
-EXPORTS = ["wr_scene_load", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free", "wr_device_count",
-           "wr_create", "wr_destroy", "wr_set_pipelines", "wr_set_trace_mode", "wr_trace_closest", "wr_occluded", "wr_render_bdpt", "wr_render_path",
-           "wr_render_vcm", "wr_path_radiance",
-           "wr_film_write_ppm", "wr_film_write_image", "wr_last_error", "wr_api_version"]
+EXPORTS = ["wr_scene_load", "wr_scene_from_desc", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free",
+           "wr_device_count", "wr_create", "wr_create_multi", "wr_context_devices", "wr_destroy", "wr_comm_unique_id",
+           "wr_comm_init", "wr_film_reduce", "wr_set_pipelines", "wr_set_trace_mode", "wr_trace_closest", "wr_occluded",
+           "wr_render_bdpt", "wr_render_path", "wr_render_vcm", "wr_path_radiance", "wr_film_write_ppm",
+           "wr_film_write_image", "wr_checkpoint_save", "wr_checkpoint_load", "wr_last_error", "wr_api_version"]
+CKPT_BDPT, CKPT_VCM, CKPT_PT = 1, 2, 3
 
 
 class WrRay(C.Structure):
@@ -39,6 +41,19 @@ class WrSceneInfo(C.Structure):
                 ("kd_inner", C.c_int32), ("kd_leaves", C.c_int32), ("kd_refs", C.c_int64),
                 ("kd_max_stack", C.c_int32), ("missing_files", C.c_int32), ("camera_xres", C.c_float),
                 ("camera_yres", C.c_float), ("device_bytes", C.c_int64)]
+
+
+class WrSceneDesc(C.Structure):
+    _fields_ = [("n_prims", C.c_int32), ("prim_type", C.POINTER(C.c_int32)), ("prim_data", C.POINTER(C.c_float)),
+                ("prim_mat", C.POINTER(C.c_int32)), ("n_lights", C.c_int32), ("light_tri", C.POINTER(C.c_float)),
+                ("light_le", C.POINTER(C.c_float)), ("n_materials", C.c_int32), ("materials", C.POINTER(C.c_float)),
+                ("cam_pos", C.c_float * 3), ("cam_fwd", C.c_float * 3), ("cam_up", C.c_float * 3),
+                ("cam_xres", C.c_float), ("cam_yres", C.c_float), ("cam_hfov", C.c_float)]
+
+
+class WrCheckpointInfo(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("kind", C.c_int32), ("done", C.c_int32),
+                ("total", C.c_int32), ("seed", C.c_uint32), ("reserved", C.c_int32 * 2)]
 
 
 class WrBdptParams(C.Structure):
@@ -110,6 +125,14 @@ def lib():
         L = C.CDLL(LIB_PATH)
         P, I, I64 = C.c_void_p, C.c_int, C.c_int64
         L.wr_scene_load.argtypes = [C.c_char_p, C.POINTER(P)]
+        L.wr_scene_from_desc.argtypes = [C.POINTER(WrSceneDesc), C.POINTER(P)]
+        L.wr_create_multi.argtypes = [P, C.POINTER(C.c_int), I, C.POINTER(P)]
+        L.wr_context_devices.argtypes = [P, C.POINTER(C.c_int), I]
+        L.wr_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+        L.wr_comm_init.argtypes = [P, C.POINTER(C.c_uint8), I, I]
+        L.wr_film_reduce.argtypes = [P, P, I64, I]
+        L.wr_checkpoint_save.argtypes = [C.c_char_p, C.POINTER(WrCheckpointInfo), C.POINTER(C.c_float)]
+        L.wr_checkpoint_load.argtypes = [C.c_char_p, C.POINTER(WrCheckpointInfo), C.POINTER(C.c_float), I64]
         L.wr_scene_info_get.argtypes = [P, C.POINTER(WrSceneInfo)]
         L.wr_scene_dump.argtypes = [P, C.c_char_p]
         L.wr_scene_free.argtypes = [P]
@@ -146,10 +169,45 @@ def device_count():
 class Scene:
     """Scene::init (scene.cpp:469-489): .scene + .obj + KD tree, host side."""
 
-    def __init__(self, path):
+    def __init__(self, path=None, _handle=None):
+        if _handle is not None:
+            self.h = _handle
+            return
         h = C.c_void_p()
         check(lib().wr_scene_load(os.fsencode(path), C.byref(h)))
         self.h = h
+
+    @classmethod
+    def from_desc(cls, prim_type, prim_data, prim_mat, light_tri, light_le, materials, cam_pos, cam_fwd, cam_up,
+                  cam_xres, cam_yres, cam_hfov):
+        """wr_scene_from_desc: the reference's in-memory Scene as flat arrays
+        (include/winmad_rt.h wr_scene_desc): prim_type (n,) int32 0/1,
+        prim_data (n, 9) float32, prim_mat (n,) int32, light_tri (m, 9),
+        light_le (m, 3), materials (k, 11), camera vectors and raster / FOV."""
+        pt = np.ascontiguousarray(prim_type, np.int32).reshape(-1)
+        pd = np.ascontiguousarray(prim_data, np.float32).reshape(-1, 9)
+        pm = np.ascontiguousarray(prim_mat, np.int32).reshape(-1)
+        lt = np.ascontiguousarray(light_tri, np.float32).reshape(-1, 9)
+        le = np.ascontiguousarray(light_le, np.float32).reshape(-1, 3)
+        mt = np.ascontiguousarray(materials, np.float32).reshape(-1, 11)
+        if not (pt.size == pd.shape[0] == pm.size) or lt.shape[0] != le.shape[0]:
+            raise ValueError("inconsistent primitive / light array lengths")
+        d = WrSceneDesc()
+        d.n_prims = pt.size
+        d.prim_type = pt.ctypes.data_as(C.POINTER(C.c_int32))
+        d.prim_data = pd.ctypes.data_as(C.POINTER(C.c_float))
+        d.prim_mat = pm.ctypes.data_as(C.POINTER(C.c_int32))
+        d.n_lights = lt.shape[0]
+        d.light_tri = lt.ctypes.data_as(C.POINTER(C.c_float))
+        d.light_le = le.ctypes.data_as(C.POINTER(C.c_float))
+        d.n_materials = mt.shape[0]
+        d.materials = mt.ctypes.data_as(C.POINTER(C.c_float))
+        for k in range(3):
+            d.cam_pos[k], d.cam_fwd[k], d.cam_up[k] = float(cam_pos[k]), float(cam_fwd[k]), float(cam_up[k])
+        d.cam_xres, d.cam_yres, d.cam_hfov = float(cam_xres), float(cam_yres), float(cam_hfov)
+        h = C.c_void_p()
+        check(lib().wr_scene_from_desc(C.byref(d), C.byref(h)))
+        return cls(_handle=h)
 
     def close(self):
         if getattr(self, "h", None):
@@ -203,13 +261,34 @@ def rays_from_arrays(o, d, tmin=0.0, tmax=1e7):
 
 
 class Context:
-    """Scene resident in HBM on one device + one HIP stream."""
+    """Scene resident in HBM on one device (or on several: `devices`, a list of
+    HIP device ids, wr_create_multi) + its HIP streams."""
 
-    def __init__(self, scene, device=0):
+    def __init__(self, scene, device=0, devices=None):
         h = C.c_void_p()
-        check(lib().wr_create(scene.h, device, C.byref(h)))
+        if devices is not None:
+            ids = (C.c_int * len(devices))(*devices)
+            check(lib().wr_create_multi(scene.h, ids, len(devices), C.byref(h)))
+        else:
+            check(lib().wr_create(scene.h, device, C.byref(h)))
         self.h = h
         self.scene = scene
+
+    def devices(self):
+        buf = (C.c_int * 64)()
+        n = lib().wr_context_devices(self.h, buf, 64)
+        if n < 0:
+            check(n)
+        return list(buf[:n])
+
+    def comm_init(self, unique_id, nranks, rank):
+        """wr_comm_init: this rank's RCCL communicator (one process per GPU)."""
+        idb = (C.c_uint8 * 128)(*bytes(unique_id))
+        check(lib().wr_comm_init(self.h, idb, nranks, rank))
+
+    def film_reduce(self, film_ptr, nfloat, root=0):
+        """wr_film_reduce: sum the ranks' device films into rank `root`'s, in place."""
+        check(lib().wr_film_reduce(self.h, C.c_void_p(film_ptr), nfloat, root))
 
     def set_pipelines(self, n):
         """Concurrent render pipelines (streams) for render_bdpt / render_path."""
@@ -300,6 +379,32 @@ class Context:
         film = _host_film(film, height, width)
         check(lib().wr_render_path(self.h, C.byref(p), film.ctypes.data_as(C.c_void_p), 0, C.byref(st)))
         return film, st
+
+
+def comm_unique_id():
+    """wr_comm_unique_id: 128 bytes rank 0 hands to every rank's comm_init."""
+    buf = (C.c_uint8 * 128)()
+    check(lib().wr_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def checkpoint_save(path, film, kind, done, total, seed):
+    """wr_checkpoint_save: the accumulated film + how many iterations it sums."""
+    film = np.ascontiguousarray(film, np.float32)
+    if film.ndim != 3 or film.shape[2] != 3:
+        raise ValueError(f"film must have shape (height, width, 3), got {film.shape}")
+    info = WrCheckpointInfo(film.shape[1], film.shape[0], kind, done, total, seed)
+    check(lib().wr_checkpoint_save(os.fsencode(path), C.byref(info), film.ctypes.data_as(C.POINTER(C.c_float))))
+
+
+def checkpoint_load(path):
+    """wr_checkpoint_load -> (film, dict(width, height, kind, done, total, seed))."""
+    info = WrCheckpointInfo()
+    check(lib().wr_checkpoint_load(os.fsencode(path), C.byref(info), None, 0))
+    film = np.zeros((info.height, info.width, 3), np.float32)
+    check(lib().wr_checkpoint_load(os.fsencode(path), C.byref(info), film.ctypes.data_as(C.POINTER(C.c_float)),
+                                   film.size))
+    return film, {k: getattr(info, k) for k in ("width", "height", "kind", "done", "total", "seed")}
 
 
 def write_ppm(film, path, scale=1.0, gamma=2.2, transpose=False):
