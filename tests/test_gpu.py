@@ -513,6 +513,17 @@ def test_pt_non_square_spp_stratification_matches_oracle(spp):
     assert_ray_counts(st, rst)
 
 
+def test_cbox_bdpt_film_matches_oracle():
+    """BDPT on the Cornell box (unit-scale geometry: vertex connections carry
+    12 % of this film, where on torus.scene they add nothing -- DESIGN.md 8)."""
+    path = _scenes.cbox(64, 48, "bdpt")
+    for ctl in (3, 0):
+        film, st = ctx(path).render_bdpt(64, 48, iterations=3, seed=5489, control_length=ctl)
+        ref, rst = _oracle.Scene(path).bdpt(64, 48, 3, 5489, mode=1, control_length=ctl)
+        assert_film_parity(film, ref)
+        assert_ray_counts(st, rst)
+
+
 def test_bdpt_1m_scene_film_matches_oracle():
     """C4's scene (the 1M-triangle torus: deep KD tree, wide-stack traversal),
     BDPT at 384x216 (a fifth of the C4 frame per axis), one iteration, against

@@ -55,11 +55,19 @@ struct BdptGroup {
 };
 
 __device__ __forceinline__ bool len_ok(int ctl, int L) { return ctl <= 0 || L == ctl; }
-// Numerator of connectVertices' MIS weight (:658-664): 1 in every product
-// build.  scripts/perturbation_check.sh builds a variant with 1.001 to show
-// that the film parity gates (tests/_parity.py) catch a 1e-3 weight error.
+// Numerators of three MIS weights -- connectVertices (:658-664),
+// getDirectIllumination's outer weight (:529) and connectToCamera's (:360):
+// 1 in every product build.  scripts/perturbation_check.sh builds variants
+// with 1.001 to show that the film parity gates (tests/_parity.py) catch a
+// 1e-3 error in any of them.
 #ifndef WR_TEST_CONN_W
 #define WR_TEST_CONN_W 1.f
+#endif
+#ifndef WR_TEST_DI_W
+#define WR_TEST_DI_W 1.f
+#endif
+#ifndef WR_TEST_SPLAT_W
+#define WR_TEST_SPLAT_W 1.f
 #endif
 
 // generateLightSample (:267-311) + the first extension ray
@@ -201,7 +209,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
                     const V3 res = div_plain(mul(thr, f), static_cast<float>(A.P) * s2i);
                     if (!black(res)) {
                       const float wl = (pdf_a / static_cast<float>(A.P)) * (dvcm + rp * dvc);
-                      const float w = 1.f / (wl + 1.f);
+                      const float w = WR_TEST_SPLAT_W / (wl + 1.f);
                       splat = true;
                       s_o = h.p;
                       s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
@@ -391,7 +399,7 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
                     nee_tgt = hp + dtl * dist;
                     const float wl = bdp / (dpdf * lpp);
                     const float wc = (epdf * cos_to / (dpdf * cal)) * (dvcm + brp * dvc);
-                    nee_w = 1.f / (wl + 1.f + wc);
+                    nee_w = WR_TEST_DI_W / (wl + 1.f + wc);
                     nee_val = tmp * (dpdf / (dpdf + bdp));
                   }
                 }

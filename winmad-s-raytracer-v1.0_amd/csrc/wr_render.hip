@@ -248,18 +248,28 @@ k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const f
 #else
 #define WR_HARD_OCC
 #endif
+// blocks [0, hard_blocks): the tie list; the rest: the scan list, one ray per
+// wave.  WAVE: one tie per wave (the API paths).  Otherwise the launch adapts
+// to the tie count it finds: up to wave_max ties (a late bounce's launch:
+// its slowest tie is the step's latency) one per wave -- a wave lasts as long
+// as its own tie, and the candidates' replays are shared by its lanes -- and
+// more (full launches, where other pipelines hide the latency) one per lane
+// on the first lane_blocks blocks.
 template <bool COUNT, bool WAVE>
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32 WR_HARD_OCC
 k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const int* hard, const int* hard_n, int hcap,
-            int hard_blocks) {
-  // blocks [0, hard_blocks): the tie list; the rest: the scan list, one ray per wave
+            int hard_blocks, int lane_blocks, int wave_max) {
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
   const int b = static_cast<int>(blockIdx.x);
-  if (b < hard_blocks)
-    hard_fast<COUNT, WAVE>(S, F, Q, hard, hard_n, b, hard_blocks, smem, fc);
-  else
+  if (b < hard_blocks) {
+    if (WAVE || hard_n[0] <= wave_max)  // wave_max <= hard_blocks
+      hard_fast<COUNT, true>(S, F, Q, hard, hard_n, b, hard_blocks, smem, fc);
+    else if (b < lane_blocks)
+      hard_fast<COUNT, false>(S, F, Q, hard, hard_n, b, lane_blocks, smem, fc);
+  } else {
     scan_fast<COUNT>(S, F, Q, hard, hard_n, hcap, b - hard_blocks, static_cast<int>(gridDim.x) - hard_blocks, smem, fc);
+  }
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 
@@ -442,6 +452,9 @@ struct wr_context {
   // at least piece_min paths per pipeline (env WR_PIECE_CAP / WR_PIECE_MIN)
   int piece_cap = 1 << 21;
   int piece_min = 16384;
+  // pipelines' k_fast_hard: launches with at most this many ties resolve them
+  // one per wave (env WR_TIE_WAVE_MAX; 0: always one per lane)
+  int tie_wave_max = 512;
   // verified-BVH traversal (wr_fast.h): built at wr_create for triangle scenes
   FastScene fs{};
   Arena fast_mem;
@@ -849,7 +862,10 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     if (c->trace_log) (void)hipEventRecord(fb, stream);
     // the hard rays are a few in 10^4: a small grid drains any count (one
     // ray per wave for the API calls: up to 2048 at once, 8 waves per CU)
-    const int hgrid = hard_wave ? std::max(1, std::min(2048, max_rays)) : std::max(1, std::min(256, blocks));
+    // (pipelines: up to c->tie_wave_max ties one per wave, more one per lane)
+    const int lgrid = std::max(1, std::min(256, blocks));
+    const int hgrid = hard_wave ? std::max(1, std::min(2048, max_rays))
+                                : std::max(lgrid, std::min(c->tie_wave_max, max_rays));
 #ifndef WR_SCAN_WAVES
 #define WR_SCAN_WAVES 256
 #endif
@@ -858,7 +874,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
                         : (count ? k_fast_hard<true, false> : k_fast_hard<false, false>);
     hipLaunchKernelGGL(hk, dim3(hgrid + sgrid),
                        dim3(kTraceBlock), lds, stream, c->ds, c->fs, Q, ctr, hard, ts.hard_n,
-                       static_cast<int>(ts.t2_cap), hgrid);
+                       static_cast<int>(ts.t2_cap), hgrid, lgrid, std::min(hgrid, c->tie_wave_max));
     if (c->verify)
       hipLaunchKernelGGL(k_fast_verify, dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), lds,
                          stream, c->ds, c->fs, Q, ctr);
@@ -938,12 +954,12 @@ struct Piece {
   int n;     // paths
 };
 struct PiecePlan {
-  std::vector<std::vector<Piece>> per_pipe;
+  std::vector<std::vector<std::vector<Piece>>> per_pipe;  // [pipeline][group][member]
   int pipes() const { return std::max(1, static_cast<int>(per_pipe.size())); }
   int max_groups() const {
     size_t m = 0;
     for (const auto& v : per_pipe) m = std::max(m, v.size());
-    return static_cast<int>((m + kGroup - 1) / kGroup);
+    return static_cast<int>(m);
   }
 };
 // a position in the flattened (iteration-major) path order, moved to the
@@ -952,7 +968,26 @@ int64_t flat_round(int64_t f, int P, int unit) {
   const int64_t it = f / P, off = f % P;
   return it * P + std::min<int64_t>(P, (off + unit / 2) / unit * unit);
 }
-// the flattened path-iterations [lo, hi) (lo, hi whole units) over np pipelines
+// [a, b) cut at iteration ends and into near-equal unit-aligned pieces of at
+// most cap paths
+void cut_pieces(int64_t a, int64_t b, int P, int unit, int cap, std::vector<Piece>& out) {
+  while (a < b) {
+    const int64_t it = a / P, off = a % P;
+    const int64_t len = std::min<int64_t>(b - a, P - off);  // up to the iteration's end
+    const int64_t cuts = (len + cap - 1) / cap;
+    for (int64_t j = 0; j < cuts; ++j) {
+      int64_t lo = off + (len * j / cuts) / unit * unit, hi = off + (len * (j + 1) / cuts) / unit * unit;
+      if (j == cuts - 1) hi = off + len;
+      if (hi > lo) out.push_back(Piece{static_cast<int>(it), static_cast<int>(lo), static_cast<int>(hi - lo)});
+    }
+    a += len;
+  }
+}
+// The flattened path-iterations [lo, hi) (lo, hi whole units) over np
+// pipelines, in groups of kGroup pieces.  (Splitting a short render's share
+// unevenly into two groups per pipeline, so that the pipelines' late bounces
+// fall at different times, measured worse: C2 at 20 iterations 2,292 ->
+// 1,850 Mrays/s -- each extra group pays the bounce tails again.)
 PiecePlan plan_pieces(int64_t lo, int64_t hi, int P, int unit, int cap, int np, int min_piece) {
   PiecePlan plan;
   const int64_t T = hi - lo;
@@ -962,20 +997,17 @@ PiecePlan plan_pieces(int64_t lo, int64_t hi, int P, int unit, int cap, int np, 
   }
   const int64_t shares = std::max<int64_t>(1, std::min<int64_t>(np, T / std::max(1, min_piece)));
   auto bound = [&](int64_t k) { return k == shares ? hi : flat_round(lo + k * T / shares, P, unit); };
+  auto groups_of = [&](const std::vector<Piece>& pcs, std::vector<std::vector<Piece>>& gs) {
+    for (size_t i = 0; i < pcs.size(); i += kGroup)
+      gs.emplace_back(pcs.begin() + i, pcs.begin() + std::min(pcs.size(), i + kGroup));
+  };
   for (int64_t k = 0; k < shares; ++k) {
-    std::vector<Piece> mine;
-    for (int64_t a = bound(k), b = bound(k + 1); a < b;) {
-      const int64_t it = a / P, off = a % P;
-      const int64_t len = std::min<int64_t>(b - a, P - off);  // up to the iteration's end
-      const int64_t cuts = (len + cap - 1) / cap;
-      for (int64_t j = 0; j < cuts; ++j) {  // near-equal unit-aligned cuts of <= cap paths
-        int64_t lo_j = off + (len * j / cuts) / unit * unit, hi_j = off + (len * (j + 1) / cuts) / unit * unit;
-        if (j == cuts - 1) hi_j = off + len;
-        if (hi_j > lo_j) mine.push_back(Piece{static_cast<int>(it), static_cast<int>(lo_j), static_cast<int>(hi_j - lo_j)});
-      }
-      a += len;
-    }
-    if (!mine.empty()) plan.per_pipe.push_back(std::move(mine));
+    const int64_t a = bound(k), b = bound(k + 1);
+    std::vector<Piece> pcs;
+    cut_pieces(a, b, P, unit, cap, pcs);
+    std::vector<std::vector<Piece>> gs;
+    groups_of(pcs, gs);
+    if (!gs.empty()) plan.per_pipe.push_back(std::move(gs));
   }
   if (plan.per_pipe.empty()) plan.per_pipe.resize(1);
   return plan;
@@ -1261,6 +1293,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   if (const char* e = std::getenv("WR_PIPES")) c->npipes = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   if (const char* e = std::getenv("WR_PIECE_CAP")) c->piece_cap = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("WR_PIECE_MIN")) c->piece_min = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("WR_TIE_WAVE_MAX")) c->tie_wave_max = std::max(0, std::atoi(e));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
     // grid-stride vertex / resolve kernels: blocks per CU (knob WR_SHADE_GRID).
@@ -1810,10 +1843,10 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   // in order), so every pipeline has work queued from the start
   for (int r = 0; r < plan.max_groups(); ++r)
     for (int pi = 0; pi < np; ++pi) {
-      const std::vector<Piece>& mine = plan.per_pipe[pi];
-      const int first = r * kGroup;
-      if (first >= static_cast<int>(mine.size())) continue;
-      const int gn = std::min<int>(kGroup, static_cast<int>(mine.size()) - first);
+      if (r >= static_cast<int>(plan.per_pipe[pi].size())) continue;
+      const std::vector<Piece>& grp = plan.per_pipe[pi][r];
+      const int gn = static_cast<int>(grp.size());
+      if (gn == 0) continue;
       Pipe& pp = c->pipes[pi];
       const hipStream_t sm = pp.stream;
       Timer tm(c, &pp);
@@ -1821,7 +1854,7 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
       BdptArgs* A = GA.a;
       int nmax = 0;
       for (int m = 0; m < gn; ++m) {
-        const Piece& pc = mine[first + m];
+        const Piece& pc = grp[m];
         A[m] = A0;
         A[m].B = pp.bb[m];
         A[m].ctr = pp.ctr;
