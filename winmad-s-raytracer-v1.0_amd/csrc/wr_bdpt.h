@@ -158,6 +158,13 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
     if (j < n) {
       p = B.q_path[cur][j];
       const int prim = B.q_prim[cur][j];
+#ifdef WR_DEBUG_PATH
+      if (A.base + p == WR_DEBUG_PATH && A.iter == WR_DEBUG_ITER) {
+        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
+        printf("[dbg gpu] light step %d ray o %a %a %a d %a %a %a prim %d t %a\n", slot, o.x, o.y, o.z, d.x, d.y, d.z, prim,
+               B.q_t[cur][j]);
+      }
+#endif
       if (prim >= 0) {
         const float t = B.q_t[cur][j];
         const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
@@ -207,6 +214,12 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
                     const float pdf_a = i2s;
                     const float s2i = 1.f / i2s;
                     const V3 res = div_plain(mul(thr, f), static_cast<float>(A.P) * s2i);
+#ifdef WR_DEBUG_PATH
+                    if (A.base + p == WR_DEBUG_PATH && A.iter == WR_DEBUG_ITER)
+                      printf("[dbg gpu] len %d hit %a %a %a t %a prim %d thr %a %a %a f %a %a %a cos_to %a d2 %a i2s %a res %a %a %a black %d rp %a dvcm %a dvc %a\n",
+                             len, h.p.x, h.p.y, h.p.z, t, prim, thr.x, thr.y, thr.z, f.x, f.y, f.z, cos_to, d2, i2s,
+                             res.x, res.y, res.z, (int)black(res), rp, dvcm, dvc);
+#endif
                     if (!black(res)) {
                       const float wl = (pdf_a / static_cast<float>(A.P)) * (dvcm + rp * dvc);
                       const float w = WR_TEST_SPLAT_W / (wl + 1.f);
@@ -256,7 +269,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
       st3(Q.tgt, B.cap_sq, si, S.cam.pos);
       st3(Q.val, B.cap_sq, si, s_val);
       Q.cut[si] = occl_cut(s_o, S.cam.pos, dot(S.cam.pos - s_o, s_d));
-      Q.meta[si] = SQ_SPLAT << 30;
+      Q.meta[si] = (SQ_SPLAT << 30) | p;  // (the local path: diagnostics only)
       Q.pix[si] = s_pix;
     }
   }
@@ -609,6 +622,13 @@ __device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int
           const V3 o = ld3(Q.o, cap, j), d = ld3(Q.d, cap, j);
           unocc = near_eq(o + d * t, ld3(Q.tgt, cap, j));
         }
+#ifdef WR_DEBUG_PATH
+        if (kind == SQ_SPLAT && A.base + p == WR_DEBUG_PATH && A.iter == WR_DEBUG_ITER) {
+          const V3 o = ld3(Q.o, cap, j), d = ld3(Q.d, cap, j), v = ld3(Q.val, cap, j);
+          printf("[dbg gpu] splat o %a %a %a d %a %a %a prim %d t %a unocc %d val %a %a %a pix %d\n", o.x, o.y, o.z, d.x,
+                 d.y, d.z, prim, t, (int)unocc, v.x, v.y, v.z, Q.pix[j]);
+        }
+#endif
         if (kind == SQ_NEE) {
           di_bits = unocc ? DI_VIS : 0;
         } else if (unocc) {

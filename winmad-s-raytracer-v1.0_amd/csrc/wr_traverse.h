@@ -403,6 +403,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
     }
   }
   const int n = qend[kMaxQueues - 1];
+  // waves past the ones the rays need leave before touching the cursor (trace_fast)
+  if (static_cast<int>(blockIdx.x) * kRayGrab >= n) return;
   int qi = 0;            // queue of the lane's ray
   // field of queue q (selects, no dynamic indexing of the kernel argument)
   auto selq = [&](int q, auto field) {
