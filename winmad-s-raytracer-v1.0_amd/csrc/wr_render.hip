@@ -1128,6 +1128,10 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
   st->seconds += host_now() - t0_host;
   if (c->timing) {
     std::vector<std::pair<float, float>> spans;  // traversal launches, ms from t_ref
+    // diagnostics: WR_TIMELINE=<file> appends every timed launch (pipeline,
+    // category, start ms, end ms from the render's start), no profiler needed
+    FILE* tl = nullptr;
+    if (const char* e = std::getenv("WR_TIMELINE")) tl = std::fopen(e, "a");
     for (int i = 0; i < n; ++i) {
       const Pipe& p = c->pipes[i];
       float prev = 0.f;
@@ -1139,9 +1143,11 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
         st->kernel_ms[cat] += at - prev;
         st->kernel_launches[cat] += 1;
         if (cat == WR_K_TRACE) spans.emplace_back(prev, at);
+        if (tl) std::fprintf(tl, "%d,%d,%.4f,%.4f\n", i, cat, prev, at);
         prev = at;
       }
     }
+    if (tl) std::fclose(tl);
     std::sort(spans.begin(), spans.end());
     double wall = 0.0, lo = 0.0, hi = -1.0;
     for (const auto& sp : spans) {
@@ -1839,73 +1845,103 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   A0.faithful = prm->faithful;
   const int maxlen = A0.maxlen;
   const bool count = prm->count_work != 0;
-  // groups are issued round-robin over the pipelines (each stream runs its own
-  // in order), so every pipeline has work queued from the start
-  for (int r = 0; r < plan.max_groups(); ++r)
-    for (int pi = 0; pi < np; ++pi) {
-      if (r >= static_cast<int>(plan.per_pipe[pi].size())) continue;
-      const std::vector<Piece>& grp = plan.per_pipe[pi][r];
-      const int gn = static_cast<int>(grp.size());
-      if (gn == 0) continue;
-      Pipe& pp = c->pipes[pi];
-      const hipStream_t sm = pp.stream;
-      Timer tm(c, &pp);
-      BdptGroup GA;
-      BdptArgs* A = GA.a;
-      int nmax = 0;
-      for (int m = 0; m < gn; ++m) {
-        const Piece& pc = grp[m];
-        A[m] = A0;
-        A[m].B = pp.bb[m];
-        A[m].ctr = pp.ctr;
-        A[m].sc = pp.sc + m;
-        A[m].iter = static_cast<uint32_t>(prm->iter_begin + pc.iter);
-        A[m].base = pc.base;
-        A[m].n = pc.n;
-        nmax = std::max(nmax, pc.n);
-      }
-      auto sq = [&](int m, int slot) {
-        const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
-        return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut);
-      };
-      auto ext = [&](int m, int slot) {
-        const BdptBuf& B = pp.bb[m];
-        const int q = slot & 1;
-        return rq(B.q_o[q], B.q_d[q], B.P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
-      };
-      const int sq_max = nmax * (kVMax + 2);  // <= cap_sq
-      const int g = shade_grid(c, nmax);
+  // One group of pieces on one pipeline, issued step by step: step 0 clears
+  // the counters and starts the light subpaths, steps 1 .. maxlen-1 are the
+  // light bounces, step maxlen starts the camera subpaths, and steps
+  // maxlen+1 .. 2 maxlen+1 are the camera bounces.
+  struct GroupIssue {
+    Pipe* pp = nullptr;
+    BdptGroup GA;
+    int gn = 0, nmax = 0;
+  };
+  const int nsteps = 2 * maxlen + 2;
+  auto issue = [&](GroupIssue& G, int step) -> int {
+    Pipe& pp = *G.pp;
+    const hipStream_t sm = pp.stream;
+    Timer tm(c, &pp);
+    const int gn = G.gn;
+    const BdptArgs* A = G.GA.a;
+    auto sq = [&](int m, int slot) {
+      const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
+      return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut);
+    };
+    auto ext = [&](int m, int slot) {
+      const BdptBuf& B = pp.bb[m];
+      const int q = slot & 1;
+      return rq(B.q_o[q], B.q_d[q], B.P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
+    };
+    const int sq_max = G.nmax * (kVMax + 2);  // <= cap_sq
+    const int g = shade_grid(c, G.nmax);
+    if (step == 0) {
       HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
       // ---------------- light pass (:67-131)
-      hipLaunchKernelGGL(k_light_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
+      hipLaunchKernelGGL(k_light_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA);
       tm.mark(WR_K_GEN);
-      for (int b = 0; b < maxlen - 1; ++b) {
-        QueueList ql;
-        for (int m = 0; m < gn; ++m) ql.add(ext(m, b), A[m].n);
-        trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
-        hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA, b);
-        tm.mark(WR_K_SHADE);
-      }
+    } else if (step < maxlen) {
+      const int b = step - 1;
+      QueueList ql;
+      for (int m = 0; m < gn; ++m) ql.add(ext(m, b), A[m].n);
+      trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
+      hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA, b);
+      tm.mark(WR_K_SHADE);
+    } else if (step == maxlen) {
       // ---------------- camera pass (:133-264).  The light pass's splat rays
       // (connectToCamera) ride along with the primary rays; afterwards each
       // bounce's shadow / aux rays ride along with the next bounce's extension rays.
-      hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, GA);
+      hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA);
       tm.mark(WR_K_GEN);
-      for (int b = 0; b <= maxlen; ++b) {
-        const int slot = kCamSlot + b;
-        const bool more = b < maxlen;  // extension rays of bounce b exist
-        QueueList ql;
-        for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), A[m].n * (kVMax + 2));
-        if (more)
-          for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), A[m].n);
-        trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
-        // resolve this step's shadow / aux rays and shade its vertices in one launch
-        const int nres = shade_grid(c, sq_max);
-        hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, GA, slot, nres,
-                           more ? 1 : 0);
-        tm.mark(WR_K_SHADE);
-      }
+    } else {
+      const int b = step - maxlen - 1;
+      const int slot = kCamSlot + b;
+      const bool more = b < maxlen;  // extension rays of bounce b exist
+      QueueList ql;
+      for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), A[m].n * (kVMax + 2));
+      if (more)
+        for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), A[m].n);
+      trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
+      // resolve this step's shadow / aux rays and shade its vertices in one launch
+      const int nres = shade_grid(c, sq_max);
+      hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, G.GA, slot, nres,
+                         more ? 1 : 0);
+      tm.mark(WR_K_SHADE);
     }
+    return WR_OK;
+  };
+  // Round r takes every pipeline's r-th group, and the launches go out step by
+  // step across the pipelines: each stream runs its own in order, and all of
+  // them get their first launches at once instead of one pipeline's ~90
+  // launches after another's (host issue time: ~2 us per call)
+  std::vector<GroupIssue> round(np);
+  for (int r = 0; r < plan.max_groups(); ++r) {
+    int live = 0;
+    for (int pi = 0; pi < np; ++pi) {
+      GroupIssue& G = round[pi];
+      G.gn = 0;
+      if (r >= static_cast<int>(plan.per_pipe[pi].size())) continue;
+      const std::vector<Piece>& grp = plan.per_pipe[pi][r];
+      G.pp = &c->pipes[pi];
+      G.gn = static_cast<int>(grp.size());
+      G.nmax = 0;
+      for (int m = 0; m < G.gn; ++m) {
+        const Piece& pc = grp[m];
+        BdptArgs& a = G.GA.a[m];
+        a = A0;
+        a.B = G.pp->bb[m];
+        a.ctr = G.pp->ctr;
+        a.sc = G.pp->sc + m;
+        a.iter = static_cast<uint32_t>(prm->iter_begin + pc.iter);
+        a.base = pc.base;
+        a.n = pc.n;
+        G.nmax = std::max(G.nmax, pc.n);
+      }
+      live += G.gn > 0;
+    }
+    if (!live) continue;
+    for (int step = 0; step < nsteps; ++step)
+      for (GroupIssue& G : round)
+        if (G.gn > 0)
+          if (int rc = issue(G, step)) return rc;
+  }
   HIPCHK(hipGetLastError());
   if (int rc = finish_render(c, np, st, t0)) return rc;
   return film_return(c, film, film_on_device, nf);
