@@ -44,7 +44,7 @@ L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2, 8 XCDs x 4 MiB, ~34.5 TB/s agg
 # (scripts/profile_round.sh + scripts/summarize_profile.py; counters cannot be
 # read from inside the timed run); the newest round's file wins
 PROFILES = os.path.join(REPO, "profiles")
-TRAFFIC_JSON = next((p for p in (os.path.join(PROFILES, r, "traffic.json") for r in ("r2", "r1"))
+TRAFFIC_JSON = next((p for p in (os.path.join(PROFILES, r, "traffic.json") for r in ("r3", "r2", "r1"))
                      if os.path.exists(p)), os.path.join(PROFILES, "r1", "traffic.json"))
 
 

@@ -99,6 +99,10 @@ constexpr bool kSearchSpills = (WR_BVH_WIDE == 4 ? 3 * wrf::kMaxBvhDepth + 1 : w
 #ifndef WR_BVH_SPEC
 #define WR_BVH_SPEC 1
 #endif
+// the tie resolution's leaf searches: calls (WR_HARD_CALL=__noinline__) or inlined
+#ifndef WR_HARD_CALL
+#define WR_HARD_CALL __forceinline__  // calls: 560-752 B of scratch per lane
+#endif
 __device__ __forceinline__ uint16_t t_down16(float t) {
   return static_cast<uint16_t>(__float_as_uint(fmaxf(t, 0.f)) >> 16);  // truncation: down for t >= 0
 }
@@ -525,7 +529,7 @@ __device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3
 // The first leaf of primitive p that the reference's traversal visits, as its
 // visit key (kd_reaches) and p's position in that leaf's list; key = ~0: p is
 // not visited.  (pos < 256, so (key, pos) orders the visits of one ray.)
-__device__ __noinline__ void first_leaf(const FastScene& F, int p, V3 o, V3 d, V3 inv, float tmin0, float tmax0,
+__device__ WR_HARD_CALL void first_leaf(const FastScene& F, int p, V3 o, V3 d, V3 inv, float tmin0, float tmax0,
                                         float rtmax, unsigned long long& key, int& pos, uint32_t& steps) {
   key = ~0ull;
   pos = 0;
@@ -640,7 +644,7 @@ __device__ __forceinline__ void first_leaves_wave(const FastScene& F, const int 
 // none of their leaves.  Leaves are numbered in visit order; at a leaf each
 // unresolved primitive is looked up in its (ascending) leaf list.  want: mask
 // of the candidates to find; vis / pos get (visit number, position in list).
-__device__ __noinline__ void kd_first_leaves(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmax,
+__device__ WR_HARD_CALL void kd_first_leaves(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmax,
                                              const int* cp, unsigned want, int* stk_node, float* stk_tmin,
                                              int* vis, int* pos, uint32_t& steps) {
   float tmin, tmax;
@@ -900,7 +904,13 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   // the first reservations cover every index, and a launch of few rays (a
   // late bounce) no longer pays one device-scope atomic on a single address
   // per resident wave (5,120 of them: ~150 us per launch, measured)
-  if (static_cast<int>(blockIdx.x) * kRayGrab >= n) return;
+  // A launch of at most one ray per resident lane reserves 64 at a time (one
+  // ray per lane: the launch lasts one ray's traversal, not two)
+#ifndef WR_GRAB_ADAPT
+#define WR_GRAB_ADAPT 1
+#endif
+  const int grab = WR_GRAB_ADAPT && n <= 64 * static_cast<int>(gridDim.x) ? 64 : kRayGrab;
+  if (static_cast<int>(blockIdx.x) * grab >= n) return;
   int r = -1, qi = 0, lidx = 0;
   bool pool = true;
   int pb = 0, pe = 0;
@@ -921,12 +931,12 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
     if (need == 0) return idx;
     if (pe - pb < need) {
       int got = 0;
-      if (lane == 0) got = atomicAdd(fetch, kRayGrab);
+      if (lane == 0) got = atomicAdd(fetch, grab);
       got = __builtin_amdgcn_readlane(got, 0);
       const int rem = pe - pb;
       if (rank >= rem) idx = got + (rank - rem);
       pb = got + (need - rem);
-      pe = got + kRayGrab;
+      pe = got + grab;
     } else {
       pb += need;
     }

@@ -455,6 +455,9 @@ struct wr_context {
   // pipelines' k_fast_hard: launches with at most this many ties resolve them
   // one per wave (env WR_TIE_WAVE_MAX; 0: always one per lane)
   int tie_wave_max = 512;
+  // host threads issuing a render's launches (env WR_ISSUE_THREADS): the
+  // pipelines are dealt out to them, each thread issues its pipelines' steps
+  int issue_threads = 1;
   // verified-BVH traversal (wr_fast.h): built at wr_create for triangle scenes
   FastScene fs{};
   Arena fast_mem;
@@ -1048,11 +1051,15 @@ void begin_render(wr_context* c, int n, const int time_kernels) {
 // counters and (time_kernels) the per-launch durations of every pipeline.
 // stats->trace_wall_ms is the union of all traversal launch intervals.
 int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
+  const double t_issued = host_now();
   for (int i = 0; i < n; ++i) {
     (void)hipEventRecord(c->pipes[i].done, c->pipes[i].stream);
     (void)hipStreamWaitEvent(c->stream, c->pipes[i].done, 0);
   }
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (std::getenv("WR_ISSUE_LOG"))  // diagnostics: host issue time vs the render's
+    std::fprintf(stderr, "[wr issue] %d pipelines: issued in %.3f ms, done at %.3f ms\n", n,
+                 (t_issued - t0_host) * 1e3, (host_now() - t0_host) * 1e3);
   HIPCHK(hipGetLastError());
   if (!st) return WR_OK;
   DevCounters sum{};
@@ -1300,6 +1307,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   if (const char* e = std::getenv("WR_PIECE_CAP")) c->piece_cap = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("WR_PIECE_MIN")) c->piece_min = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("WR_TIE_WAVE_MAX")) c->tie_wave_max = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("WR_ISSUE_THREADS")) c->issue_threads = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
     // grid-stride vertex / resolve kernels: blocks per CU (knob WR_SHADE_GRID).
@@ -1794,6 +1802,40 @@ static int film_return(wr_context* c, float* film, int film_on_device, size_t nf
   return WR_OK;
 }
 
+// Issues one round of launches: step by step across the pipelines [0, np),
+// on c->issue_threads host threads (pipeline i on thread i % T, each thread
+// stepping through its own pipelines; their streams are independent).
+// fn(pipeline, step) issues one step of one pipeline.
+extern "C++" {
+template <class Fn>
+static int issue_round(wr_context* c, int live, int nsteps, Fn&& fn, int np) {
+  const int T = std::min(c->issue_threads, std::max(1, live));
+  auto run = [&](int t) -> int {
+    for (int step = 0; step < nsteps; ++step)
+      for (int pi = t; pi < np; pi += T)
+        if (int rc = fn(pi, step)) return rc;
+    return WR_OK;
+  };
+  if (T <= 1) return run(0);
+  std::vector<int> rcs(T, WR_OK);
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (int t = 1; t < T; ++t)
+    th.emplace_back([&, t] {
+      if (hipSetDevice(c->device) != hipSuccess) {
+        rcs[t] = WR_E_HIP;
+        return;
+      }
+      rcs[t] = run(t);
+    });
+  rcs[0] = run(0);
+  for (auto& x : th) x.join();
+  for (int rc : rcs)
+    if (rc) return rc;
+  return WR_OK;
+}
+}  // extern "C++"
+
 static int check_bdpt(const wr_context* c, const wr_bdpt_params* prm, const float* film) {
   if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
   if (prm->width <= 0 || prm->height <= 0 || prm->iterations < 0) return fail(WR_E_ARG, "bad film size");
@@ -1937,12 +1979,15 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
       live += G.gn > 0;
     }
     if (!live) continue;
-    for (int step = 0; step < nsteps; ++step)
-      for (GroupIssue& G : round)
-        if (G.gn > 0)
-          if (int rc = issue(G, step)) return rc;
+    if (int rc = issue_round(c, live, nsteps, [&](int pi, int step) {
+          return round[pi].gn > 0 ? issue(round[pi], step) : WR_OK;
+        }, np))
+      return rc;
   }
   HIPCHK(hipGetLastError());
+  if (std::getenv("WR_ISSUE_LOG"))
+    std::fprintf(stderr, "[wr issue] kernel args: BdptGroup %zu B, TraceQueues %zu B, DevScene %zu B, FastScene %zu B\n",
+                 sizeof(BdptGroup), sizeof(TraceQueues), sizeof(DevScene), sizeof(c->fs));
   if (int rc = finish_render(c, np, st, t0)) return rc;
   return film_return(c, film, film_on_device, nf);
 }
