@@ -397,7 +397,7 @@ def main():
                        "scene_config": args.config.upper(), "width": W, "height": H,
                        "steps_per_gpu": K, "iter_begin": it0, "parallelism": f"sample-batch x{world}",
                        "backend": args.backend if world > 1 else None, "trace": trace,
-                       "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
+                       "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "pipelines": int(st.pipelines)},
             "spp_per_sec": round(W * H * K * world / elapsed, 1),
             "rays_per_step": round(total_rays / (K * world)),
             "roofline": roofline, "cpu_baseline": cpu,

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define WR_API_VERSION 5
+#define WR_API_VERSION 6
 
 enum {
   WR_OK = 0,
@@ -140,6 +140,8 @@ typedef struct {
    * traced again by the reference's KD walk and the two answers compared.     */
   int64_t verify_rays;
   int64_t verify_mismatches; /* (t, primitive) pairs that differ bit for bit      */
+  int64_t pipelines;         /* render calls: the most concurrent pipelines one
+                                device ran (API v6)                              */
 } wr_stats;
 
 /* The reference's in-memory Scene (scene/scene.h:35-42) as flat host arrays,

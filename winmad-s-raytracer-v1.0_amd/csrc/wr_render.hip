@@ -1098,6 +1098,7 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
   st->fallback_rays += static_cast<int64_t>(sum.fallback);
   st->verify_rays += static_cast<int64_t>(sum.verify_rays);
   st->verify_mismatches += static_cast<int64_t>(sum.verify_bad);
+  st->pipelines = std::max<int64_t>(st->pipelines, n);
   if (c->trace_log && c->fast_on) {
     unsigned long long mx[3] = {0, 0, 0};
     for (int i = 0; i < n; ++i) {
@@ -2315,6 +2316,7 @@ static void add_stats(wr_stats* d, const wr_stats& s) {
   d->fallback_rays += s.fallback_rays;
   d->verify_rays += s.verify_rays;
   d->verify_mismatches += s.verify_mismatches;
+  d->pipelines = std::max(d->pipelines, s.pipelines);
 }
 
 static int ensure_dev_film(wr_context* d, float** buf, size_t* have, size_t nf) {
