@@ -142,6 +142,9 @@ typedef struct {
   int64_t verify_mismatches; /* (t, primitive) pairs that differ bit for bit      */
   int64_t pipelines;         /* render calls: the most concurrent pipelines one
                                 device ran (API v6)                              */
+  int64_t deferred_rays;     /* WR_TRACE_BVH BDPT: rays settled off the pipeline's
+                                critical path, their paths shaded a step later
+                                (deferred hard rays; API v6)        */
 } wr_stats;
 
 /* The reference's in-memory Scene (scene/scene.h:35-42) as flat host arrays,
@@ -215,6 +218,15 @@ int wr_film_reduce(wr_context* ctx, float* film_dev, int64_t nfloat, int root);
  * (GPU_MAX_HW_QUEUES, HIP default 4) up to 16, or env WR_PIPES.
  * GPU-specific scheduling; no reference counterpart. */
 int wr_set_pipelines(wr_context* ctx, int n);
+
+/* Allocate now what renders of this integrator and film size on the context
+ * will use -- every pipeline's work buffers (each device of a multi-device
+ * context) -- instead of inside the first render call.  Optional; the
+ * counterpart of the allocations SurfaceIntegrator::init makes before render()
+ * (surfaceIntegrator/surfaceIntegrator.h:14-34).  Call after wr_set_pipelines /
+ * wr_set_trace_mode (API v6). */
+enum { WR_INTEGRATOR_BDPT = 0, WR_INTEGRATOR_VCM = 1, WR_INTEGRATOR_PATH = 2 };
+int wr_reserve(wr_context* ctx, int integrator, int32_t width, int32_t height);
 
 /* Traversal mode of every later call on the context.
  *   WR_TRACE_REFERENCE (default): the reference's KD tree, walked exactly as

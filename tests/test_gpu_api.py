@@ -1,4 +1,4 @@
-"""API version 5 on the GPU: several devices behind one context
+"""API versions 5-6 on the GPU: several devices behind one context
 (wr_create_multi), the one-process-per-GPU communicator (wr_comm_*), a scene
 handed over as flat arrays (wr_scene_from_desc), and checkpoint / resume in
 the reference-compatible CLI.  The box has one GPU, so the multi-device
@@ -146,3 +146,27 @@ def test_cli_checkpoint_resume_and_devices(mode, tmp_path):
     two = _tot([base[0], tmp_path / "two.pfm", *base[2:], "--devices", "0,0", "--trace", "reference"], tmp_path)
     assert "2 GPU(s)" in two and "trace reference" in two
     assert np.allclose(_pfm(tmp_path / "two.pfm"), _pfm(tmp_path / "full.pfm"), rtol=1e-4, atol=1e-6)
+
+
+def test_reserve_then_render_equals_render(multi):
+    """wr_reserve (API v6) allocates the work buffers ahead of the first render;
+    the render after it is the same render (rays, film) and reports how many
+    pipelines ran.  Bad arguments are refused."""
+    s, m = multi
+    a = native.Context(s, 0)
+    a.set_trace_mode(native.TRACE_BVH)
+    a.reserve(native.INTEGRATOR_BDPT, 256, 256)
+    fa, sa = a.render_bdpt(256, 256, iterations=2, seed=9)
+    b = native.Context(s, 0)
+    b.set_trace_mode(native.TRACE_BVH)
+    fb, sb = b.render_bdpt(256, 256, iterations=2, seed=9)
+    _same(fa, sa, fb, sb)
+    assert sa.pipelines >= 1 and sa.pipelines == sb.pipelines
+    for kind, (W, H) in ((native.INTEGRATOR_VCM, (64, 64)), (native.INTEGRATOR_PATH, (64, 48))):
+        a.reserve(kind, W, H)
+    m.reserve(native.INTEGRATOR_BDPT, 128, 128)  # every device of a multi-device context
+    for bad in ((3, 64, 64), (-1, 64, 64), (native.INTEGRATOR_BDPT, 0, 64)):
+        with pytest.raises(native.WrError):
+            a.reserve(*bad)
+    a.close()
+    b.close()

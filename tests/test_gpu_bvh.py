@@ -185,3 +185,44 @@ def test_bvh_verify_every_ray_against_the_kd_walk(name, maker, kind, monkeypatch
         _, st = c.render_bdpt(256, 256, iterations=4, seed=3)
     assert st.verify_rays == st.closest_rays + st.shadow_rays > 0
     assert st.verify_mismatches == 0, (st.verify_mismatches, st.verify_rays)
+
+
+@pytest.mark.parametrize("name,maker,W,H,its", [("torus", lambda: _scenes.torus(256, 256), 256, 256, 3),
+                                                ("cbox", lambda: _scenes.cbox(96, 72, "bdpt"), 96, 72, 3),
+                                                ("torus1m", lambda: big_torus(192, 108), 192, 108, 1)])
+def test_deferred_hard_rays_render_the_same_film(name, maker, W, H, its, monkeypatch):
+    """BDPT hard rays off the critical path (WR_DEFER=1): the
+    deferred rays get the same answers (WR_BVH_VERIFY checks them against the KD
+    walk), their paths are shaded a step later with their own state and random
+    numbers, so the render has the same rays and the same film as the
+    synchronous one (up to the order of float atomics) and as the oracle."""
+    import _oracle
+    from _parity import assert_film_parity, assert_ray_counts
+    path = maker()
+    s = native.Scene(path)
+    films = {}
+    for defer in ("1", "0"):
+        monkeypatch.setenv("WR_DEFER", defer)
+        c = native.Context(s, 0)
+        c.set_trace_mode(native.TRACE_BVH)
+        c.set_pipelines(4)
+        films[defer] = c.render_bdpt(W, H, iterations=its, seed=5489)
+        c.close()
+    (fa, sa), (fb, sb) = films["1"], films["0"]
+    assert sa.deferred_rays > 0 and sb.deferred_rays == 0, (sa.deferred_rays, sb.deferred_rays)
+    assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
+    assert _film_close(fa, fb)
+    ref, rst = _oracle.Scene(path).bdpt(W, H, its, 5489, mode=1)
+    assert_film_parity(fa, ref, max_bad_frac=0.01)
+    assert_ray_counts(sa, rst, slack=64)
+    # and every deferred answer is the KD walk's, bit for bit
+    monkeypatch.setenv("WR_DEFER", "1")
+    monkeypatch.setenv("WR_BVH_VERIFY", "1")
+    c = native.Context(s, 0)
+    c.set_trace_mode(native.TRACE_BVH)
+    c.set_pipelines(4)
+    _, st = c.render_bdpt(W, H, iterations=its, seed=5489)
+    c.close()
+    assert st.deferred_rays > 0
+    assert st.verify_rays == st.closest_rays + st.shadow_rays
+    assert st.verify_mismatches == 0, (st.verify_mismatches, st.verify_rays)

@@ -48,6 +48,8 @@ void SurfaceIntegrator::setTraceMode(int mode) {
   traceMode = mode;
 }
 
+void SurfaceIntegrator::reserve() { ok(wr_reserve(ctx_, integrator_, width, height)); }
+
 template <class Batch>
 void SurfaceIntegrator::batched(int kind, int total, uint32_t seed, Batch batch) {
   int done = 0;
@@ -84,6 +86,7 @@ void SurfaceIntegrator::batched(int kind, int total, uint32_t seed, Batch batch)
 
 void BidirPathTracing::init(const char* filename, Parameters& para) {
   samplesPerPixel = para.SAMPLES_PER_PIXEL;  // stored, unused by BDPT (:11)
+  integrator_ = WR_INTEGRATOR_BDPT;
   height = para.HEIGHT;
   width = para.WIDTH;
   load(filename);
@@ -112,6 +115,7 @@ void BidirPathTracing::outputImage(const char* filename) {
 
 void VertexCM::init(const char* filename, Parameters& para) {
   samplesPerPixel = para.SAMPLES_PER_PIXEL;  // stored, unused (:9)
+  integrator_ = WR_INTEGRATOR_VCM;
   height = para.HEIGHT;
   width = para.WIDTH;
   load(filename);
@@ -143,6 +147,7 @@ void PathIntegrator::init(const char* filename, Parameters& para) {
   samplesPerPixel = para.SAMPLES_PER_PIXEL;
   samplesOfLight = para.SAMPLES_OF_LIGHT;
   samplesOfHemisphere = para.SAMPLES_OF_HEMISPHERE;
+  integrator_ = WR_INTEGRATOR_PATH;
   height = para.HEIGHT;
   width = para.WIDTH;
   load(filename);

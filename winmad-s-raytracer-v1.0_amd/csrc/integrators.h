@@ -47,8 +47,12 @@ class SurfaceIntegrator {
   virtual void outputImage(const char* filename) = 0;
   // wr_set_trace_mode after init (throws, e.g. WR_TRACE_BVH on a scene with spheres)
   void setTraceMode(int mode);
+  // wr_reserve after init / setTraceMode: the render's GPU buffers now, so that
+  // render() only renders (optional; render() allocates them otherwise)
+  void reserve();
 
  protected:
+  int integrator_ = WR_INTEGRATOR_BDPT;  // set by init: what reserve() allocates for
   wr_scene* scene_ = nullptr;
   wr_context* ctx_ = nullptr;
   void load(const char* filename);

@@ -119,6 +119,7 @@ int main(int argc, char** argv) {
         bvh = false;
       }
     }
+    integ->reserve();  // the GPU work buffers, before the render (as init's allocations in the reference)
     integ->render();
     if (integ->stopped) {
       std::printf("stopped after --stop-after %d; checkpoint %s\n", stop_after, checkpoint);

@@ -141,23 +141,140 @@ __device__ __forceinline__ bool sample_scatter(const DevScene& S, Rng& rng, cons
   return true;
 }
 
-// One light-subpath vertex (:77-128)
+// One light-subpath vertex (:77-128): path p's ray (o, d) hit prim at t
+// (prim < 0: a miss, or a pending hard ray -- nothing to do).  Every lane of
+// the wave calls it (queue appends).  oslot: the step whose queue gets the
+// extension ray -- slot + 1, or slot + 2 for a deferred vertex (k_late_light).
+__device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim, float t, V3 o, V3 d, int oslot) {
+  const BdptBuf& B = A.B;
+  const DevScene& S = A.S;
+  const int P = B.P, nxt = oslot & 1;  // P: buffer stride (local paths)
+  bool ext = false, splat = false;
+  V3 e_o, e_d, s_o, s_d, s_val;
+  int s_pix = -1;
+  if (prim >= 0) {
+    {
+      const Hit h = rebuild_hit(S, prim, t, o, d);
+      Bsdf b;
+      bsdf_init(b, -d, h.n, h.mat, S.mats);
+      if (b.mat != 0) {
+        float dvcm = B.l_dvcm[p], dvc = B.l_dvc[p];
+        int len = B.l_len[p], nspec = B.l_nspec[p];
+        V3 thr = ld3(B.l_thr, P, p);
+        dvcm *= (t * t);  // pathLength > 1 || isFiniteLight: always for area lights (:94-97)
+        dvcm /= fabsf(b.wi.z);
+        dvc /= fabsf(b.wi.z);
+        if (!b.delta) {  // lightStates.push_back (:101-102)
+          const int k = B.v_count[p];
+          const int slot = k * P + p;
+          st3(B.v_pos, kVMax * P, slot, h.p);
+          st3(B.v_n, kVMax * P, slot, h.n);
+          st3(B.v_wi, kVMax * P, slot, b.wi);
+          st3(B.v_thr, kVMax * P, slot, thr);
+          B.v_dvcm[slot] = dvcm;
+          B.v_dvc[slot] = dvc;
+          B.v_cont[slot] = b.cont;
+          B.v_pd[slot] = b.pd;
+          B.v_pg[slot] = b.pg;
+          B.v_len[slot] = len;
+          B.v_nspec[slot] = nspec;
+          B.v_mat[slot] = b.mat;
+          B.v_count[p] = k + 1;
+          if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
+            const DCam& cam = S.cam;
+            const V3 ip = t_point(cam.w2r, h.p);
+            if (check_raster(cam, ip.x, ip.y)) {
+              V3 dtc = cam.pos - h.p;
+              if (dot(-dtc, cam.fwd) > 0) {
+                const float d2 = sqr_len(dtc);
+                const float dist = sqrtf(d2);
+                dtc = div_guarded(dtc, dist);
+                float cos_to = 0.f, dp, rp;
+                const V3 f = bsdf_f(b, S.mats, dtc, &cos_to, &dp, &rp);
+                if (!black(f)) {
+                  rp *= b.cont;
+                  const float cos_at = dot(-dtc, cam.fwd);
+                  const float ipd = cam.plane_dist / cos_at;
+                  const float i2sa = (ipd * ipd) / cos_at;
+                  const float i2s = i2sa * fabsf(cos_to) / d2;
+                  const float pdf_a = i2s;
+                  const float s2i = 1.f / i2s;
+                  const V3 res = div_plain(mul(thr, f), static_cast<float>(A.P) * s2i);
+#ifdef WR_DEBUG_PATH
+                  if (A.base + p == WR_DEBUG_PATH && A.iter == WR_DEBUG_ITER)
+                    printf("[dbg gpu] len %d hit %a %a %a t %a prim %d thr %a %a %a f %a %a %a cos_to %a d2 %a i2s %a res %a %a %a black %d rp %a dvcm %a dvc %a\n",
+                           len, h.p.x, h.p.y, h.p.z, t, prim, thr.x, thr.y, thr.z, f.x, f.y, f.z, cos_to, d2, i2s,
+                           res.x, res.y, res.z, (int)black(res), rp, dvcm, dvc);
+#endif
+                  if (!black(res)) {
+                    const float wl = (pdf_a / static_cast<float>(A.P)) * (dvcm + rp * dvc);
+                    const float w = WR_TEST_SPLAT_W / (wl + 1.f);
+                    splat = true;
+                    s_o = h.p;
+                    s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
+                    s_val = res * w;
+                    s_pix = pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W);
+                  }
+                }
+              }
+            }
+          }
+        }
+        if (!(len + 2 > A.maxlen)) {  // (:123-127)
+          Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), B.l_ctr[p]};
+          V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
+          if (sample_scatter(S, rng, b, h.p, lo, ld, thr, dvcm, dvc, nspec)) {
+            ext = true;
+            ++len;
+            e_o = lo + ld * WR_EPS;
+            e_d = normalize(ld);
+            st3(B.l_o, P, p, lo);
+            st3(B.l_d, P, p, ld);
+            st3(B.l_thr, P, p, thr);
+            B.l_dvcm[p] = dvcm;
+            B.l_dvc[p] = dvc;
+            B.l_len[p] = len;
+            B.l_nspec[p] = nspec;
+          }
+          B.l_ctr[p] = rng.ctr;
+        }
+      }
+    }
+  }
+  const int ei = wave_append(&A.sc->ext[oslot], ext);
+  if (ext) {
+    st3(B.q_o[nxt], P, ei, e_o);
+    st3(B.q_d[nxt], P, ei, e_d);
+    B.q_path[nxt][ei] = p;
+  }
+  const int si = wave_append(&A.sc->sq[kCamSlot], splat);  // traced with the camera primaries
+  if (splat) {
+    const BdptBuf::Sq& Q = B.sq[kCamSlot & 1];
+    st3(Q.o, B.cap_sq, si, s_o);
+    st3(Q.d, B.cap_sq, si, s_d);
+    st3(Q.tgt, B.cap_sq, si, S.cam.pos);
+    st3(Q.val, B.cap_sq, si, s_val);
+    Q.cut[si] = occl_cut(s_o, S.cam.pos, dot(S.cam.pos - s_o, s_d));
+    Q.meta[si] = (SQ_SPLAT << 30) | p;  // (the local path: diagnostics only)
+    Q.pix[si] = s_pix;
+  }
+}
+
 __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGroup G_, int slot) {
   const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
-  const DevScene& S = A.S;
-  const int P = B.P, cur = slot & 1, nxt = cur ^ 1;  // P: buffer stride (local paths)
+  const int P = B.P, cur = slot & 1;
   const int n = A.sc->ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;  // whole waves reach the appends
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
-    bool ext = false, splat = false;
-    V3 e_o, e_d, s_o, s_d, s_val;
-    int s_pix = -1, p = -1;
+    int p = -1, prim = -1;
+    float t = 0.f;
+    V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 0.f);
     if (j < n) {
       p = B.q_path[cur][j];
-      const int prim = B.q_prim[cur][j];
+      prim = B.q_prim[cur][j];
 #ifdef WR_DEBUG_PATH
       if (A.base + p == WR_DEBUG_PATH && A.iter == WR_DEBUG_ITER) {
         const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
@@ -166,112 +283,12 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
       }
 #endif
       if (prim >= 0) {
-        const float t = B.q_t[cur][j];
-        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
-        const Hit h = rebuild_hit(S, prim, t, o, d);
-        Bsdf b;
-        bsdf_init(b, -d, h.n, h.mat, S.mats);
-        if (b.mat != 0) {
-          float dvcm = B.l_dvcm[p], dvc = B.l_dvc[p];
-          int len = B.l_len[p], nspec = B.l_nspec[p];
-          V3 thr = ld3(B.l_thr, P, p);
-          dvcm *= (t * t);  // pathLength > 1 || isFiniteLight: always for area lights (:94-97)
-          dvcm /= fabsf(b.wi.z);
-          dvc /= fabsf(b.wi.z);
-          if (!b.delta) {  // lightStates.push_back (:101-102)
-            const int k = B.v_count[p];
-            const int slot = k * P + p;
-            st3(B.v_pos, kVMax * P, slot, h.p);
-            st3(B.v_n, kVMax * P, slot, h.n);
-            st3(B.v_wi, kVMax * P, slot, b.wi);
-            st3(B.v_thr, kVMax * P, slot, thr);
-            B.v_dvcm[slot] = dvcm;
-            B.v_dvc[slot] = dvc;
-            B.v_cont[slot] = b.cont;
-            B.v_pd[slot] = b.pd;
-            B.v_pg[slot] = b.pg;
-            B.v_len[slot] = len;
-            B.v_nspec[slot] = nspec;
-            B.v_mat[slot] = b.mat;
-            B.v_count[p] = k + 1;
-            if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
-              const DCam& cam = S.cam;
-              const V3 ip = t_point(cam.w2r, h.p);
-              if (check_raster(cam, ip.x, ip.y)) {
-                V3 dtc = cam.pos - h.p;
-                if (dot(-dtc, cam.fwd) > 0) {
-                  const float d2 = sqr_len(dtc);
-                  const float dist = sqrtf(d2);
-                  dtc = div_guarded(dtc, dist);
-                  float cos_to = 0.f, dp, rp;
-                  const V3 f = bsdf_f(b, S.mats, dtc, &cos_to, &dp, &rp);
-                  if (!black(f)) {
-                    rp *= b.cont;
-                    const float cos_at = dot(-dtc, cam.fwd);
-                    const float ipd = cam.plane_dist / cos_at;
-                    const float i2sa = (ipd * ipd) / cos_at;
-                    const float i2s = i2sa * fabsf(cos_to) / d2;
-                    const float pdf_a = i2s;
-                    const float s2i = 1.f / i2s;
-                    const V3 res = div_plain(mul(thr, f), static_cast<float>(A.P) * s2i);
-#ifdef WR_DEBUG_PATH
-                    if (A.base + p == WR_DEBUG_PATH && A.iter == WR_DEBUG_ITER)
-                      printf("[dbg gpu] len %d hit %a %a %a t %a prim %d thr %a %a %a f %a %a %a cos_to %a d2 %a i2s %a res %a %a %a black %d rp %a dvcm %a dvc %a\n",
-                             len, h.p.x, h.p.y, h.p.z, t, prim, thr.x, thr.y, thr.z, f.x, f.y, f.z, cos_to, d2, i2s,
-                             res.x, res.y, res.z, (int)black(res), rp, dvcm, dvc);
-#endif
-                    if (!black(res)) {
-                      const float wl = (pdf_a / static_cast<float>(A.P)) * (dvcm + rp * dvc);
-                      const float w = WR_TEST_SPLAT_W / (wl + 1.f);
-                      splat = true;
-                      s_o = h.p;
-                      s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
-                      s_val = res * w;
-                      s_pix = pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W);
-                    }
-                  }
-                }
-              }
-            }
-          }
-          if (!(len + 2 > A.maxlen)) {  // (:123-127)
-            Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), B.l_ctr[p]};
-            V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
-            if (sample_scatter(S, rng, b, h.p, lo, ld, thr, dvcm, dvc, nspec)) {
-              ext = true;
-              ++len;
-              e_o = lo + ld * WR_EPS;
-              e_d = normalize(ld);
-              st3(B.l_o, P, p, lo);
-              st3(B.l_d, P, p, ld);
-              st3(B.l_thr, P, p, thr);
-              B.l_dvcm[p] = dvcm;
-              B.l_dvc[p] = dvc;
-              B.l_len[p] = len;
-              B.l_nspec[p] = nspec;
-            }
-            B.l_ctr[p] = rng.ctr;
-          }
-        }
+        t = B.q_t[cur][j];
+        o = ld3(B.q_o[cur], P, j);
+        d = ld3(B.q_d[cur], P, j);
       }
     }
-    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
-    if (ext) {
-      st3(B.q_o[nxt], P, ei, e_o);
-      st3(B.q_d[nxt], P, ei, e_d);
-      B.q_path[nxt][ei] = p;
-    }
-    const int si = wave_append(&A.sc->sq[kCamSlot], splat);  // traced with the camera primaries
-    if (splat) {
-      const BdptBuf::Sq& Q = B.sq[kCamSlot & 1];
-      st3(Q.o, B.cap_sq, si, s_o);
-      st3(Q.d, B.cap_sq, si, s_d);
-      st3(Q.tgt, B.cap_sq, si, S.cam.pos);
-      st3(Q.val, B.cap_sq, si, s_val);
-      Q.cut[si] = occl_cut(s_o, S.cam.pos, dot(S.cam.pos - s_o, s_d));
-      Q.meta[si] = (SQ_SPLAT << 30) | p;  // (the local path: diagnostics only)
-      Q.pix[si] = s_pix;
-    }
+    light_vertex(A, p, prim, t, o, d, slot + 1);
   }
 }
 
@@ -326,229 +343,221 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGr
 }
 
 // One camera-subpath vertex (:148-260): emitter hit, DI setup, vertex
-// connections (shadow rays queued), scattering.
-__device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, int bid, int nblk) {
+// connections (shadow rays queued), scattering -- path p's ray (o, d) hit prim
+// at t (prim < 0: a miss, or a pending hard ray: nothing).  Every lane of the
+// wave calls it.  oslot: the step whose queues (shadow / aux, DI records,
+// extension) get this vertex's rays -- slot + 1, or slot + 2 for a deferred
+// vertex (k_late_camera).
+__device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim, float t, V3 o, V3 d, int oslot) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
-  const int P = B.P, cur = slot & 1, nxt = cur ^ 1, cap = B.cap_sq;  // P: buffer stride
-  const int n = A.sc->ext[slot];
-  if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
-  const int gstride = nblk * blockDim.x;
-  const int nround = (n + gstride - 1) / gstride * gstride;
+  const int P = B.P, nxt = oslot & 1, cap = B.cap_sq;  // P: buffer stride
   const float lpp = 1.f / static_cast<float>(S.nlights);
-  const BdptBuf::Sq& Q = B.sq[(slot + 1) & 1];  // rays traced at the next step
-  const BdptBuf::Di& D = B.di[(slot + 1) & 1];
-  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
-    bool live = false, ext = false, conn_phase = false, nee = false, dib = false;
-    int p = -1, pix = -1, nv = 0, len = 0, nspec = 0, cnspec = 0;
-    V3 hp{}, thr{}, cthr{}, e_o{}, e_d{}, nee_tgt{}, nee_d{}, dib_o{}, dib_d{};
-    float dvcm = 0.f, dvc = 0.f, cdvcm = 0.f, cdvc = 0.f;
-    Bsdf b;
-    b.mat = 0;
-    if (j < n) {
-      p = B.q_path[cur][j];
-      const int prim = B.q_prim[cur][j];
-      if (prim >= 0) {
-        const float t = B.q_t[cur][j];
-        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
-        const Hit h = rebuild_hit(S, prim, t, o, d);
-        bsdf_init(b, -d, h.n, h.mat, S.mats);
-        if (b.mat != 0) {
-          hp = h.p;
-          pix = B.c_pix[p];
-          dvcm = B.c_dvcm[p];
-          dvc = B.c_dvc[p];
-          len = B.c_len[p];
-          nspec = B.c_nspec[p];
-          thr = ld3(B.c_thr, P, p);
-          dvcm *= (t * t);  // (:180-182)
-          dvcm /= fabsf(b.wi.z);
-          dvc /= fabsf(b.wi.z);
-          // this vertex's state, used by DI and the connections; the scatter
-          // below updates thr / dvcm / dvc / nspec for the next vertex
-          cthr = thr;
-          cdvcm = dvcm;
-          cdvc = dvc;
-          cnspec = nspec;
-          if (h.mat < 0) {  // hit an emitter (:184-199)
-            if (len_ok(A.ctl, len)) {
-              const DLight L = S.lights[-h.mat - 1];
-              float dpa, ep;
-              V3 r = light_radiance(L, d, &dpa, &ep);
-              if (!black(r)) {
-                if (len != 1) {  // getLightRadiance (:454-482)
-                  dpa *= lpp;
-                  ep *= lpp;
-                  const float wc = dpa * dvcm + ep * dvc;
-                  r = r * (1.f / (1.f + wc));
-                }
-                film_add(A.film, pix, mul(thr, r));
-              }
+  const BdptBuf::Sq& Q = B.sq[oslot & 1];  // rays traced at step oslot
+  const BdptBuf::Di& D = B.di[oslot & 1];
+  bool live = false, ext = false, conn_phase = false, nee = false, dib = false;
+  int pix = -1, nv = 0, len = 0, nspec = 0, cnspec = 0;
+  V3 hp{}, thr{}, cthr{}, e_o{}, e_d{}, nee_tgt{}, nee_d{}, dib_o{}, dib_d{};
+  float dvcm = 0.f, dvc = 0.f, cdvcm = 0.f, cdvc = 0.f;
+  Bsdf b;
+  b.mat = 0;
+  if (prim >= 0) {
+    const Hit h = rebuild_hit(S, prim, t, o, d);
+    bsdf_init(b, -d, h.n, h.mat, S.mats);
+    if (b.mat != 0) {
+      hp = h.p;
+      pix = B.c_pix[p];
+      dvcm = B.c_dvcm[p];
+      dvc = B.c_dvc[p];
+      len = B.c_len[p];
+      nspec = B.c_nspec[p];
+      thr = ld3(B.c_thr, P, p);
+      dvcm *= (t * t);  // (:180-182)
+      dvcm /= fabsf(b.wi.z);
+      dvc /= fabsf(b.wi.z);
+      // this vertex's state, used by DI and the connections; the scatter
+      // below updates thr / dvcm / dvc / nspec for the next vertex
+      cthr = thr;
+      cdvcm = dvcm;
+      cdvc = dvc;
+      cnspec = nspec;
+      if (h.mat < 0) {  // hit an emitter (:184-199)
+        if (len_ok(A.ctl, len)) {
+          const DLight L = S.lights[-h.mat - 1];
+          float dpa, ep;
+          V3 r = light_radiance(L, d, &dpa, &ep);
+          if (!black(r)) {
+            if (len != 1) {  // getLightRadiance (:454-482)
+              dpa *= lpp;
+              ep *= lpp;
+              const float wc = dpa * dvcm + ep * dvc;
+              r = r * (1.f / (1.f + wc));
             }
-          } else if (len < A.maxlen) {
-            live = true;
-            Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(A.base + p)), B.c_ctr[p]};
-            if (!b.delta && len_ok(A.ctl, len + 1)) {  // getDirectIllumination (:205-217, :484-608)
-              const float wlen = 1.f / (static_cast<float>(len) + 1.f - static_cast<float>(nspec));
-              const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
-              const DLight L = S.lights[lid];
-              V3 dtl;
-              float dist = 0.f, dpdf = 0.f, epdf = 0.f, cal = 0.f;
-              const V3 illu = light_illuminance(L, hp, rng.v(), &dtl, &dist, &dpdf, &epdf, &cal);
-              int flags = 0;
-              V3 nee_val = v3(0.f, 0.f, 0.f), bsdf_val = v3(0.f, 0.f, 0.f);
-              float nee_w = 0.f;
-              if (!black(illu) && dpdf > 0) {
-                float cos_to = 0.f, bdp, brp;
-                const V3 bf = bsdf_f(b, S.mats, dtl, &cos_to, &bdp, &brp);
-                if (!black(bf)) {
-                  bdp *= b.cont;
-                  brp *= b.cont;
-                  const V3 tmp = div_plain(mul(illu, bf) * cos_to, dpdf * lpp);
-                  if (!black(tmp)) {
-                    nee = true;
-                    flags |= DI_NEE;
-                    nee_d = normalize(dtl);
-                    nee_tgt = hp + dtl * dist;
-                    const float wl = bdp / (dpdf * lpp);
-                    const float wc = (epdf * cos_to / (dpdf * cal)) * (dvcm + brp * dvc);
-                    nee_w = WR_TEST_DI_W / (wl + 1.f + wc);
-                    nee_val = tmp * (dpdf / (dpdf + bdp));
-                  }
-                }
-              }
-              V3 dtl2 = dtl;
-              float dpdf2 = dpdf, cos_s = 0.f;
-              int type;
-              const V3 bf2 = bsdf_sample(b, S.mats, rng.v(), &dtl2, &dpdf2, &cos_s, &type);
-              if (!black(bf2) && dpdf2 > 0) {
-                float w = 1.f;
-                V3 illu2 = illu;
-                bool early = false;
-                if (!(type & T_SPEC)) {
-                  float lpdf, ep2;
-                  illu2 = light_radiance(L, dtl2, &lpdf, &ep2);
-                  if (cmpf(lpdf) == 0) early = true;  // (:563-564) returns res unweighted
-                  else w = dpdf2 / (dpdf2 + lpdf);
-                }
-                if (early) {
-                  flags |= DI_EARLY;
-                } else {
-                  dib = true;
-                  flags |= DI_BSDF;
-                  dib_o = hp + dtl2 * WR_EPS;
-                  dib_d = normalize(dtl2);
-                  if (!black(illu2)) bsdf_val = div_plain(mul(illu2, bf2) * cos_s, dpdf2) * w;
-                }
-              }
-              // a record only when a ray will be resolved: with neither the NEE
-              // nor the BSDF ray the contribution is exactly zero (:533-607)
-              const int nrays = (nee ? 1 : 0) + (dib ? 1 : 0);
-              if (nrays > 0) {
-                D.flags[p] = flags;
-                st3(D.nee, P, p, nee_val);
-                D.neew[p] = nee_w;
-                st3(D.bsdf, P, p, bsdf_val);
-                st3(D.thr, P, p, thr);
-                D.wlen[p] = wlen;
-                D.light[p] = lid;
-                D.pix[p] = pix;
-                D.state[p] = nrays;
-              }
-            }
-            if (!b.delta) {
-              conn_phase = true;
-              nv = B.v_count[p];
-            }
-            V3 so = ld3(B.c_o, P, p), sd = ld3(B.c_d, P, p);
-            if (sample_scatter(S, rng, b, hp, so, sd, thr, dvcm, dvc, nspec)) {
-              ext = true;
-              e_o = so + sd * WR_EPS;
-              e_d = normalize(sd);
-            }
-            B.c_ctr[p] = rng.ctr;
-            // state for the NEXT vertex; the connections below use the values of
-            // THIS vertex, so keep them (thr/dvcm/dvc/nspec are re-read below)
-            st3(B.c_o, P, p, so);
-            st3(B.c_d, P, p, sd);
+            film_add(A.film, pix, mul(thr, r));
           }
         }
+      } else if (len < A.maxlen) {
+        live = true;
+        Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(A.base + p)), B.c_ctr[p]};
+        if (!b.delta && len_ok(A.ctl, len + 1)) {  // getDirectIllumination (:205-217, :484-608)
+          const float wlen = 1.f / (static_cast<float>(len) + 1.f - static_cast<float>(nspec));
+          const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
+          const DLight L = S.lights[lid];
+          V3 dtl;
+          float dist = 0.f, dpdf = 0.f, epdf = 0.f, cal = 0.f;
+          const V3 illu = light_illuminance(L, hp, rng.v(), &dtl, &dist, &dpdf, &epdf, &cal);
+          int flags = 0;
+          V3 nee_val = v3(0.f, 0.f, 0.f), bsdf_val = v3(0.f, 0.f, 0.f);
+          float nee_w = 0.f;
+          if (!black(illu) && dpdf > 0) {
+            float cos_to = 0.f, bdp, brp;
+            const V3 bf = bsdf_f(b, S.mats, dtl, &cos_to, &bdp, &brp);
+            if (!black(bf)) {
+              bdp *= b.cont;
+              brp *= b.cont;
+              const V3 tmp = div_plain(mul(illu, bf) * cos_to, dpdf * lpp);
+              if (!black(tmp)) {
+                nee = true;
+                flags |= DI_NEE;
+                nee_d = normalize(dtl);
+                nee_tgt = hp + dtl * dist;
+                const float wl = bdp / (dpdf * lpp);
+                const float wc = (epdf * cos_to / (dpdf * cal)) * (dvcm + brp * dvc);
+                nee_w = WR_TEST_DI_W / (wl + 1.f + wc);
+                nee_val = tmp * (dpdf / (dpdf + bdp));
+              }
+            }
+          }
+          V3 dtl2 = dtl;
+          float dpdf2 = dpdf, cos_s = 0.f;
+          int type;
+          const V3 bf2 = bsdf_sample(b, S.mats, rng.v(), &dtl2, &dpdf2, &cos_s, &type);
+          if (!black(bf2) && dpdf2 > 0) {
+            float w = 1.f;
+            V3 illu2 = illu;
+            bool early = false;
+            if (!(type & T_SPEC)) {
+              float lpdf, ep2;
+              illu2 = light_radiance(L, dtl2, &lpdf, &ep2);
+              if (cmpf(lpdf) == 0) early = true;  // (:563-564) returns res unweighted
+              else w = dpdf2 / (dpdf2 + lpdf);
+            }
+            if (early) {
+              flags |= DI_EARLY;
+            } else {
+              dib = true;
+              flags |= DI_BSDF;
+              dib_o = hp + dtl2 * WR_EPS;
+              dib_d = normalize(dtl2);
+              if (!black(illu2)) bsdf_val = div_plain(mul(illu2, bf2) * cos_s, dpdf2) * w;
+            }
+          }
+          // a record only when a ray will be resolved: with neither the NEE
+          // nor the BSDF ray the contribution is exactly zero (:533-607)
+          const int nrays = (nee ? 1 : 0) + (dib ? 1 : 0);
+          if (nrays > 0) {
+            D.flags[p] = flags;
+            st3(D.nee, P, p, nee_val);
+            D.neew[p] = nee_w;
+            st3(D.bsdf, P, p, bsdf_val);
+            st3(D.thr, P, p, thr);
+            D.wlen[p] = wlen;
+            D.light[p] = lid;
+            D.pix[p] = pix;
+            D.state[p] = nrays;
+          }
+        }
+        if (!b.delta) {
+          conn_phase = true;
+          nv = B.v_count[p];
+        }
+        V3 so = ld3(B.c_o, P, p), sd = ld3(B.c_d, P, p);
+        if (sample_scatter(S, rng, b, hp, so, sd, thr, dvcm, dvc, nspec)) {
+          ext = true;
+          e_o = so + sd * WR_EPS;
+          e_d = normalize(sd);
+        }
+        B.c_ctr[p] = rng.ctr;
+        // state for the NEXT vertex; the connections below use the values of
+        // THIS vertex, so keep them (thr/dvcm/dvc/nspec are re-read below)
+        st3(B.c_o, P, p, so);
+        st3(B.c_d, P, p, sd);
       }
     }
-    // DI queue entries
-    {
-      const int ni = wave_append(&A.sc->sq[slot + 1], nee);
-      if (nee) {
-        st3(Q.o, cap, ni, hp);
-        st3(Q.d, cap, ni, nee_d);
-        st3(Q.tgt, cap, ni, nee_tgt);
-        Q.cut[ni] = occl_cut(hp, nee_tgt, dot(nee_tgt - hp, nee_d));
-        Q.meta[ni] = (SQ_NEE << 30) | p;
-        Q.pix[ni] = pix;
-      }
-      const int bi = wave_append(&A.sc->sq[slot + 1], dib);
-      if (dib) {
-        st3(Q.o, cap, bi, dib_o);
-        st3(Q.d, cap, bi, dib_d);
-        Q.cut[bi] = -WR_INF;  // needs the closest hit (same light?)
-        Q.meta[bi] = (SQ_DIB << 30) | p;
-        Q.pix[bi] = pix;
-      }
+  }
+  // DI queue entries
+  {
+    const int ni = wave_append(&A.sc->sq[oslot], nee);
+    if (nee) {
+      st3(Q.o, cap, ni, hp);
+      st3(Q.d, cap, ni, nee_d);
+      st3(Q.tgt, cap, ni, nee_tgt);
+      Q.cut[ni] = occl_cut(hp, nee_tgt, dot(nee_tgt - hp, nee_d));
+      Q.meta[ni] = (SQ_NEE << 30) | p;
+      Q.pix[ni] = pix;
     }
-    // vertex connections to the paired light subpath (:219-257)
-    if (__ballot(conn_phase && nv > 0)) {
-      for (int k = 0; __ballot(conn_phase && k < nv); ++k) {
-        bool shoot = false;
-        V3 sdir{}, stgt{}, sval{};
-        if (conn_phase && k < nv) {
-          const int slot = k * P + p;
-          const int llen = B.v_len[slot];
-          if (llen + 1 + len > A.maxlen) {
-            nv = k;  // break (:237-239)
-          } else {
-            // connectVertices (:610-665)
-            const V3 lpos = ld3(B.v_pos, kVMax * P, slot);
-            V3 dir = lpos - hp;
-            const float d2 = sqr_len(dir);
-            const float dist = sqrtf(d2);
-            dir = div_guarded(dir, dist);
-            float cos_c = 0.f, cdp, crp;
-            const V3 cf = bsdf_f(b, S.mats, dir, &cos_c, &cdp, &crp);
-            if (!black(cf)) {
-              cdp *= b.cont;
-              crp *= b.cont;
-              Bsdf lb;
-              lb.mat = B.v_mat[slot];
-              lb.fr = frame_from_z(ld3(B.v_n, kVMax * P, slot));
-              lb.wi = ld3(B.v_wi, kVMax * P, slot);
-              lb.pd = B.v_pd[slot];
-              lb.pg = B.v_pg[slot];
-              lb.cont = B.v_cont[slot];
-              float cos_l = 0.f, ldp, lrp;
-              const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
-              if (!black(lf)) {
-                ldp *= lb.cont;
-                lrp *= lb.cont;
-                const float G = cos_l * cos_c / d2;
-                if (!(cmpf(G) < 0)) {
-                  const float cdpa = cdp * fabsf(cos_l) / (dist * dist);
-                  const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
-                  const V3 res = mul(cf, lf) * G;
-                  if (!black(res)) {
-                    const float wl = cdpa * (B.v_dvcm[slot] + lrp * B.v_dvc[slot]);
-                    const float wc = ldpa * (cdvcm + crp * cdvc);
-                    const float w = WR_TEST_CONN_W / (wl + 1.f + wc);
-                    const bool counts = len_ok(A.ctl, llen + 1 + len);
-                    if (counts || A.faithful) {
-                      shoot = true;
-                      sdir = normalize(dir);
-                      stgt = hp + dir * dist;
-                      if (counts) {
-                        const float wlen = 1.f / (static_cast<float>(llen) + 1.f + static_cast<float>(len) -
-                                                  static_cast<float>(B.v_nspec[slot]) - static_cast<float>(cnspec));
-                        const V3 lthr = ld3(B.v_thr, kVMax * P, slot);
-                        sval = mul(mul(cthr, lthr), res * w) * wlen;
-                      }
+    const int bi = wave_append(&A.sc->sq[oslot], dib);
+    if (dib) {
+      st3(Q.o, cap, bi, dib_o);
+      st3(Q.d, cap, bi, dib_d);
+      Q.cut[bi] = -WR_INF;  // needs the closest hit (same light?)
+      Q.meta[bi] = (SQ_DIB << 30) | p;
+      Q.pix[bi] = pix;
+    }
+  }
+  // vertex connections to the paired light subpath (:219-257)
+  if (__ballot(conn_phase && nv > 0)) {
+    for (int k = 0; __ballot(conn_phase && k < nv); ++k) {
+      bool shoot = false;
+      V3 sdir{}, stgt{}, sval{};
+      if (conn_phase && k < nv) {
+        const int slot = k * P + p;
+        const int llen = B.v_len[slot];
+        if (llen + 1 + len > A.maxlen) {
+          nv = k;  // break (:237-239)
+        } else {
+          // connectVertices (:610-665)
+          const V3 lpos = ld3(B.v_pos, kVMax * P, slot);
+          V3 dir = lpos - hp;
+          const float d2 = sqr_len(dir);
+          const float dist = sqrtf(d2);
+          dir = div_guarded(dir, dist);
+          float cos_c = 0.f, cdp, crp;
+          const V3 cf = bsdf_f(b, S.mats, dir, &cos_c, &cdp, &crp);
+          if (!black(cf)) {
+            cdp *= b.cont;
+            crp *= b.cont;
+            Bsdf lb;
+            lb.mat = B.v_mat[slot];
+            lb.fr = frame_from_z(ld3(B.v_n, kVMax * P, slot));
+            lb.wi = ld3(B.v_wi, kVMax * P, slot);
+            lb.pd = B.v_pd[slot];
+            lb.pg = B.v_pg[slot];
+            lb.cont = B.v_cont[slot];
+            float cos_l = 0.f, ldp, lrp;
+            const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
+            if (!black(lf)) {
+              ldp *= lb.cont;
+              lrp *= lb.cont;
+              const float G = cos_l * cos_c / d2;
+              if (!(cmpf(G) < 0)) {
+                const float cdpa = cdp * fabsf(cos_l) / (dist * dist);
+                const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
+                const V3 res = mul(cf, lf) * G;
+                if (!black(res)) {
+                  const float wl = cdpa * (B.v_dvcm[slot] + lrp * B.v_dvc[slot]);
+                  const float wc = ldpa * (cdvcm + crp * cdvc);
+                  const float w = WR_TEST_CONN_W / (wl + 1.f + wc);
+                  const bool counts = len_ok(A.ctl, llen + 1 + len);
+                  if (counts || A.faithful) {
+                    shoot = true;
+                    sdir = normalize(dir);
+                    stgt = hp + dir * dist;
+                    if (counts) {
+                      const float wlen = 1.f / (static_cast<float>(llen) + 1.f + static_cast<float>(len) -
+                                                static_cast<float>(B.v_nspec[slot]) - static_cast<float>(cnspec));
+                      const V3 lthr = ld3(B.v_thr, kVMax * P, slot);
+                      sval = mul(mul(cthr, lthr), res * w) * wlen;
                     }
                   }
                 }
@@ -556,33 +565,88 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
             }
           }
         }
-        const int si = wave_append(&A.sc->sq[slot + 1], shoot);
-        if (shoot) {
-          st3(Q.o, cap, si, hp);
-          st3(Q.d, cap, si, sdir);
-          st3(Q.tgt, cap, si, stgt);
-          st3(Q.val, cap, si, sval);
-          Q.cut[si] = occl_cut(hp, stgt, dot(stgt - hp, sdir));
-          Q.meta[si] = (SQ_CONN << 30) | p;
-          Q.pix[si] = pix;
-        }
+      }
+      const int si = wave_append(&A.sc->sq[oslot], shoot);
+      if (shoot) {
+        st3(Q.o, cap, si, hp);
+        st3(Q.d, cap, si, sdir);
+        st3(Q.tgt, cap, si, stgt);
+        st3(Q.val, cap, si, sval);
+        Q.cut[si] = occl_cut(hp, stgt, dot(stgt - hp, sdir));
+        Q.meta[si] = (SQ_CONN << 30) | p;
+        Q.pix[si] = pix;
       }
     }
-    if (live) {  // commit scattered state (:259-260) and the loop increment
-      if (ext) {
-        st3(B.c_thr, P, p, thr);
-        B.c_dvcm[p] = dvcm;
-        B.c_dvc[p] = dvc;
-        B.c_nspec[p] = nspec;
-        B.c_len[p] = len + 1;
-      }
-    }
-    const int ei = wave_append(&A.sc->ext[slot + 1], ext);
+  }
+  if (live) {  // commit scattered state (:259-260) and the loop increment
     if (ext) {
-      st3(B.q_o[nxt], P, ei, e_o);
-      st3(B.q_d[nxt], P, ei, e_d);
-      B.q_path[nxt][ei] = p;
+      st3(B.c_thr, P, p, thr);
+      B.c_dvcm[p] = dvcm;
+      B.c_dvc[p] = dvc;
+      B.c_nspec[p] = nspec;
+      B.c_len[p] = len + 1;
     }
+  }
+  const int ei = wave_append(&A.sc->ext[oslot], ext);
+  if (ext) {
+    st3(B.q_o[nxt], P, ei, e_o);
+    st3(B.q_d[nxt], P, ei, e_d);
+    B.q_path[nxt][ei] = p;
+  }
+}
+
+__device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, int bid, int nblk) {
+  const BdptBuf& B = A.B;
+  const int P = B.P, cur = slot & 1;  // P: buffer stride
+  const int n = A.sc->ext[slot];
+  if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
+  const int gstride = nblk * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;
+  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    int p = -1, prim = -1;
+    float t = 0.f;
+    V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 0.f);
+    if (j < n) {
+      p = B.q_path[cur][j];
+      prim = B.q_prim[cur][j];
+      if (prim >= 0) {
+        t = B.q_t[cur][j];
+        o = ld3(B.q_o[cur], P, j);
+        d = ld3(B.q_d[cur], P, j);
+      }
+    }
+    camera_vertex(A, p, prim, t, o, d, slot + 1);
+  }
+}
+
+// Deferred vertices (WR_TRACE_BVH, "deferred hard rays" in wr_render.hip):
+// the paths whose step-`slot` hit was settled off the critical path
+// (k_late_hard) are shaded one step later, into the queues of step slot + 2.
+// Light vertices feed only their own path's camera connections (:130,
+// :222-229) and every path keeps its own state, counters and random numbers,
+// so the film is the one of the undeferred render.
+template <bool CAMERA>
+__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_late_vertex(BdptGroup G_, LateArgs L, int slot) {
+  const BdptArgs& A = G_.a[blockIdx.y];
+  const LateList& LL = L.l[blockIdx.y];
+  const int half = LL.cap >> 1;
+  const int nt = min(L.n[blockIdx.y][0], half), n = nt + min(L.n[blockIdx.y][1], half);
+  const int gstride = gridDim.x * blockDim.x;
+  const int nround = (n + gstride - 1) / gstride * gstride;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+    int p = -1, prim = -1;
+    float t = 0.f;
+    V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 0.f);
+    if (j < n) {
+      const int i = j < nt ? j : half + (j - nt);
+      p = LL.pth[i];
+      prim = LL.prim[i];
+      t = LL.t[i];
+      o = ld3(LL.o3, LL.cap, i);
+      d = ld3(LL.d3, LL.cap, i);
+    }
+    if (CAMERA) camera_vertex(A, p, prim, t, o, d, slot + 2);
+    else light_vertex(A, p, prim, t, o, d, slot + 2);
   }
 }
 

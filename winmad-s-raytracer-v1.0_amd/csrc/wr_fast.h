@@ -1207,18 +1207,21 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
   for (int base = blockIdx.x * 64; base < QI.n; base += gridDim.x * 64) {
     const int idx = base + lane;
     bool need = false, scan = false, big_tie = false;
+    int q = 0, r = 0, p1 = -1;
+    float t1 = WR_INF;
+    V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 0.f);
     if (idx < QI.n) {
-      int q, r;
       QI.locate(idx, q, r);
       // every load that does not depend on p1 in flight at once
-      const int p1 = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r];
-      const float t1 = qfield(Q, q, [](const RayQueue& x) { return x.out_t; })[r], t2 = t2buf[idx];
+      p1 = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r];
+      t1 = qfield(Q, q, [](const RayQueue& x) { return x.out_t; })[r];
+      const float t2 = t2buf[idx];
       const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
       const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
       const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
       const float* tmx = qfield(Q, q, [](const RayQueue& x) { return x.tmax; });
-      const V3 o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
-      const V3 d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
+      o = v3(o3[r], o3[cap + r], o3[2 * cap + r]);
+      d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
       const float rtmax = tmx ? tmx[r] : WR_INF;
       // p1's membership record: one line with its first four leaves' cells
       const float4* pr = F.prim_rec + 8 * static_cast<size_t>(max(p1, 0));
@@ -1254,6 +1257,38 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
               ctr.mem_sum += dt;
               ctr.scans += (ln > 4 && steps > 64) ? 1u : 0u;
             }
+          }
+        }
+      }
+    }
+    // a deferrable queue (BDPT extension rays): the ray goes to the queue's
+    // late list -- settled off the pipeline's critical path, its path shaded
+    // one step later -- unless its path was deferred before in this pass.
+    // Rare (0.1-0.5 % of rays): one atomic per listed ray.
+    if (need || scan) {
+      const LateList* LL = qfield(Q, q, [](const RayQueue& x) { return x.late; });
+      if (LL) {
+        const int pth = LL->path[r];
+        const int bit = qfield(Q, q, [](const RayQueue& x) { return x.late_bit; });
+        if (!(LL->delayed[pth] & bit)) {
+          const int half = LL->cap >> 1;
+          const int k = atomicAdd(qfield(Q, q, [](const RayQueue& x) { return x.late_n; }) + (scan ? 1 : 0), 1);
+          if (k < half) {
+            const int i = scan ? half + k : k;
+            const int lc = LL->cap;
+            LL->o3[i] = o.x;
+            LL->o3[lc + i] = o.y;
+            LL->o3[2 * lc + i] = o.z;
+            LL->d3[i] = d.x;
+            LL->d3[lc + i] = d.y;
+            LL->d3[2 * lc + i] = d.z;
+            LL->t1[i] = t1;
+            LL->p1[i] = p1;
+            LL->pth[i] = pth;
+            LL->tie[i] = big_tie ? 1 : 0;
+            LL->delayed[pth] = static_cast<uint8_t>(LL->delayed[pth] | bit);
+            qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r] = kPendingPrim;
+            need = scan = false;
           }
         }
       }
@@ -1372,19 +1407,18 @@ __device__ __forceinline__ ListedRay listed_ray(const TraceQueues& Q, const Queu
   return L;
 }
 
-template <bool COUNT, bool WAVE>
-__device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
-                                          const int* hard, const int* hard_n, int bid, int nb, uint32_t* lds,
-                                          FastCounters& ctr) {
+// The tie list of one launch (hard_rays: count, ray getter), WAVE or one ray
+// per lane with the hand-back above.
+template <bool COUNT, bool WAVE, class Get>
+__device__ __forceinline__ void hard_rays(const DevScene& S, const FastScene& F, int nh, Get get, int bid, int nb,
+                                          uint32_t* lds, FastCounters& ctr) {
   const int lane = __lane_id();
   const bool lead = !WAVE || lane == 0;  // writes the answer, counts the uniform work
   int* stk_node = reinterpret_cast<int*>(lds) + lane;
   float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
-  const QueueIndex QI(Q);
-  const int nh = (F.diag & (32 | 128)) ? 0 : hard_n[0];
   if (WAVE) {
     for (int i = bid; i < nh; i += nb) {
-      const ListedRay L = listed_ray(Q, QI, hard[i]);
+      const ListedRay L = get(i);
       settle_ray<COUNT, true>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r, lead,
                               ctr);
     }
@@ -1397,7 +1431,7 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
     ListedRay L{};
     bool back = false;
     if (i < nh) {
-      L = listed_ray(Q, QI, hard[i]);
+      L = get(i);
       back = !settle_ray<COUNT, false>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r,
                                        true, ctr);
     }
@@ -1416,25 +1450,29 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
     }
   }
 }
+template <bool COUNT, bool WAVE>
+__device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
+                                          const int* hard, const int* hard_n, int bid, int nb, uint32_t* lds,
+                                          FastCounters& ctr) {
+  const QueueIndex QI(Q);
+  const int nh = (F.diag & (32 | 128)) ? 0 : hard_n[0];
+  hard_rays<COUNT, WAVE>(S, F, nh, [&](int i) { return listed_ray(Q, QI, hard[i]); }, bid, nb, lds, ctr);
+}
 
 // The scan list (k_fast_resolve's kScan rays and near-ties on many-leaf
 // primitives, at the top of the list array): one ray per wave.  The lanes share out p1's leaves -- the witness for each
 // leaf's cell, else the replay of its path -- and stop once one is reached;
 // p1 then stands.  If none is, t1's triangle is not visited and the ray is
 // settled in general by the same wave (settle_ray, one ray per wave).
-template <bool COUNT>
-__device__ __forceinline__ void scan_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
-                                          const int* hard, const int* hard_n, int hcap, int bid, int nb, uint32_t* lds,
-                                          FastCounters& ctr) {
+template <bool COUNT, class Get>
+__device__ __forceinline__ void scan_rays(const DevScene& S, const FastScene& F, int ns, Get get, int bid, int nb,
+                                          uint32_t* lds, FastCounters& ctr) {
   const int lane = __lane_id();
   int* stk_node = reinterpret_cast<int*>(lds) + lane;
   float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
-  const QueueIndex QI(Q);
-  const int ns = (F.diag & (32 | 64)) ? 0 : hard_n[1];
   for (int i = bid; i < ns; i += nb) {
-    const int e = hard[hcap - 1 - i];
-    const bool tie = e < 0;  // a near-tie on a many-leaf primitive: straight to the general resolution
-    const ListedRay L = listed_ray(Q, QI, tie ? ~e : e);
+    bool tie = false;  // a near-tie on a many-leaf primitive: straight to the general resolution
+    const ListedRay L = get(i, tie);
     bool member = false;
     float tmin, tmax;
     uint32_t steps = 0;
@@ -1460,9 +1498,66 @@ __device__ __forceinline__ void scan_fast(const DevScene& S, const FastScene& F,
       ctr.replay += steps;
       ctr.scans += lane == 0 ? 1u : 0u;
     }
-    if (member) continue;
+    if (member) {  // p1 stands (a queue entry holds it already; a late record gets it)
+      if (lane == 0) {
+        L.outt[L.r] = L.t1;
+        L.outp[L.r] = L.p1;
+      }
+      continue;
+    }
     settle_ray<COUNT, true>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r,
                             lane == 0, ctr);
+  }
+}
+template <bool COUNT>
+__device__ __forceinline__ void scan_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
+                                          const int* hard, const int* hard_n, int hcap, int bid, int nb, uint32_t* lds,
+                                          FastCounters& ctr) {
+  const QueueIndex QI(Q);
+  const int ns = (F.diag & (32 | 64)) ? 0 : hard_n[1];
+  scan_rays<COUNT>(S, F, ns, [&](int i, bool& tie) {
+    const int e = hard[hcap - 1 - i];
+    tie = e < 0;
+    return listed_ray(Q, QI, tie ? ~e : e);
+  }, bid, nb, lds, ctr);
+}
+
+// A record of a late list (extension rays only: [0, inf) windows).
+__device__ __forceinline__ ListedRay late_ray(const LateList& LL, int i) {
+  ListedRay L;
+  const int c = LL.cap;
+  L.o = v3(LL.o3[i], LL.o3[c + i], LL.o3[2 * c + i]);
+  L.d = v3(LL.d3[i], LL.d3[c + i], LL.d3[2 * c + i]);
+  L.rtmin = 0.f;
+  L.rtmax = WR_INF;
+  L.t1 = LL.t1[i];
+  L.p1 = LL.p1[i];
+  L.r = i;
+  L.outt = LL.t;
+  L.outp = LL.prim;
+  return L;
+}
+// k_late_hard: a late list's tie entries (blocks [0, hard_blocks): one per
+// wave up to wave_max entries, else one per lane on lane_blocks) and scan
+// entries (the other blocks, one per wave).  Same resolutions as k_fast_hard.
+template <bool COUNT>
+__device__ __forceinline__ void late_hard(const DevScene& S, const FastScene& F, const LateList& LL, const int* n,
+                                          int hard_blocks, int lane_blocks, int wave_max, uint32_t* lds,
+                                          FastCounters& ctr) {
+  const int half = LL.cap >> 1;
+  const int nt = min(n[0], half), ns = min(n[1], half);
+  const int b = static_cast<int>(blockIdx.x);
+  if (b < hard_blocks) {
+    auto get = [&](int i) { return late_ray(LL, i); };
+    if (nt <= wave_max)
+      hard_rays<COUNT, true>(S, F, nt, get, b, hard_blocks, lds, ctr);
+    else if (b < lane_blocks)
+      hard_rays<COUNT, false>(S, F, nt, get, b, lane_blocks, lds, ctr);
+  } else {
+    scan_rays<COUNT>(S, F, ns, [&](int i, bool& tie) {
+      tie = LL.tie[half + i] != 0;
+      return late_ray(LL, half + i);
+    }, b - hard_blocks, static_cast<int>(gridDim.x) - hard_blocks, lds, ctr);
   }
 }
 
@@ -1490,6 +1585,28 @@ __device__ __forceinline__ void verify_fast(const DevScene& S, const FastScene& 
     kd_walk<false>(S, o, d, tmn ? tmn[r] : 0.f, tmx ? tmx[r] : WR_INF, stk_node, stk_tmin, tb, pb, dummy);
     const int p = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r];
     const float t = qfield(Q, q, [](const RayQueue& x) { return x.out_t; })[r];
+    if (p == kPendingPrim) continue;  // deferred: checked by verify_late
+    ++rays;
+    if (p != pb || (pb >= 0 && __float_as_uint(t) != __float_as_uint(tb))) ++bad;
+  }
+}
+// The same check for a late list's records (after k_late_hard).
+__device__ __forceinline__ void verify_late(const DevScene& S, const FastScene& F, const LateList& LL, const int* n,
+                                            uint32_t* lds, uint32_t& rays, uint32_t& bad) {
+  const int lane = __lane_id();
+  int* stk_node = reinterpret_cast<int*>(lds) + lane;
+  float* stk_tmin = reinterpret_cast<float*>(lds) + F.depth * 64 + lane;
+  FastCounters dummy{};
+  const int half = LL.cap >> 1;
+  const int nt = min(n[0], half), nall = nt + min(n[1], half);
+  for (int j = blockIdx.x * 64 + lane; j < nall; j += gridDim.x * 64) {
+    const int i = j < nt ? j : half + (j - nt);
+    const ListedRay L = late_ray(LL, i);
+    float tb;
+    int pb;
+    kd_walk<false>(S, L.o, L.d, L.rtmin, L.rtmax, stk_node, stk_tmin, tb, pb, dummy);
+    const int p = LL.prim[i];
+    const float t = LL.t[i];
     ++rays;
     if (p != pb || (pb >= 0 && __float_as_uint(t) != __float_as_uint(tb))) ++bad;
   }

@@ -74,6 +74,12 @@ constexpr int kShadeBlock = 256;
 #endif
 constexpr int kGroup = WR_GROUP;
 
+// The late lists of one pipeline step (deferred hard rays, one per group member)
+struct LateArgs {
+  LateList l[kGroup];
+  int* n[kGroup];
+};
+
 enum SqKind { SQ_SPLAT = 0, SQ_CONN = 1, SQ_NEE = 2, SQ_DIB = 3 };
 enum DiFlag { DI_NEE = 1, DI_BSDF = 2, DI_EARLY = 4 };
 // DI record state word: rays still to resolve (low byte) | results
@@ -93,6 +99,7 @@ struct StepCounters {
   int vcm_nverts;     // VCM: light vertices in the merge grid
   int mq[kSlots];     // VCM: merge queries queued at step `slot`
   int hard[kSlots][2];  // WR_TRACE_BVH: rays of step `slot` left to k_fast_hard (tie list, scan list)
+  int late[kSlots][2];  // WR_TRACE_BVH: rays of step `slot` deferred (late list: ties, scans)
 };
 struct DevCounters {
   int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
@@ -102,6 +109,7 @@ struct DevCounters {
   unsigned long long vm_queries, vm_found, vm_merged;  // VCM range queries / vertices in radius / merges
   unsigned long long bvh_nodes, bvh_tests, kd_replay, fallback;  // WR_TRACE_BVH work (count_work)
   unsigned long long verify_rays, verify_bad;                   // WR_BVH_VERIFY
+  unsigned long long deferred;  // BDPT rays settled off the critical path (late lists)
   unsigned long long lat[7];  // WR_TRACE_BVH latency tail (FastCounters mem_max .. scans; max or sum)
 };
 
@@ -273,6 +281,34 @@ k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const int*
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 
+// The deferred hard rays of one pipeline step (blockIdx.y = group member),
+// on the pipeline's side stream; grid as k_fast_hard's.
+template <bool COUNT>
+__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32 WR_HARD_OCC
+k_late_hard(DevScene S, FastScene F, LateArgs L, DevCounters* ctr, int hard_blocks, int lane_blocks, int wave_max) {
+  extern __shared__ uint32_t smem[];
+  FastCounters fc{};
+  late_hard<COUNT>(S, F, L.l[blockIdx.y], L.n[blockIdx.y], hard_blocks, lane_blocks, wave_max, smem, fc);
+  if (COUNT) fast_counts<COUNT>(ctr, fc);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int half = L.l[blockIdx.y].cap >> 1;
+    atomicAdd(&ctr->deferred, static_cast<unsigned long long>(min(L.n[blockIdx.y][0], half) +
+                                                              min(L.n[blockIdx.y][1], half)));
+  }
+}
+// WR_BVH_VERIFY: the late lists' answers against the KD walk
+__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
+k_late_verify(DevScene S, FastScene F, LateArgs L, DevCounters* ctr) {
+  extern __shared__ uint32_t smem[];
+  uint32_t rays = 0, bad = 0;
+  verify_late(S, F, L.l[blockIdx.y], L.n[blockIdx.y], smem, rays, bad);
+  const unsigned long long a = wave_sum(rays), b = wave_sum(bad);
+  if (lane_id() == 0) {
+    atomicAdd(&ctr->verify_rays, a);
+    atomicAdd(&ctr->verify_bad, b);
+  }
+}
+
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
 k_fast_verify(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr) {
   extern __shared__ uint32_t smem[];
@@ -416,6 +452,15 @@ struct Pipe {
   std::vector<int> ev_cat;
   size_t ev_used = 0;
   hipEvent_t done = nullptr;
+  // deferred hard rays (BDPT, WR_TRACE_BVH): a side stream settles a step's
+  // late lists and shades their paths while the pipeline goes on
+  hipStream_t side = nullptr;
+  hipEvent_t ev_res[2]{}, ev_vtx[2]{}, ev_late[2]{};  // per step parity
+  Arena late_mem;
+  size_t late_recs = 0, late_paths = 0;  // records per list, paths per member laid out
+  LateList late_h[kGroup][2]{};          // host copies: [member][step parity]
+  LateList* late_d = nullptr;            // device copies, same order
+  uint8_t* delayed = nullptr;            // [kGroup][late_paths]
 };
 
 struct wr_context {
@@ -465,6 +510,8 @@ struct wr_context {
   bool fast_on = false;   // WR_TRACE_BVH mode selected
   int fast_blocks = 4096; // resident one-wave workgroups of k_trace_fast
   bool verify = false;      // WR_BVH_VERIFY=1: every BVH answer checked against the KD walk
+  // BDPT hard rays off the critical path (env WR_DEFER=1; off by default)
+  int defer = -1;
   float* api_t2 = nullptr;  // t2 scratch of the API path
   size_t api_t2_cap = 0;
   int2* api_spill = nullptr;  // the API path's search stack spill area
@@ -733,6 +780,18 @@ int pipelines_that_fit(wr_context* c, int kind, int P, int sets, int want) {
 }
 
 // ---- launch helpers with optional per-launch HIP events (on the pipeline's stream)
+// Flags of the library's events.  By default HIP records an event with a
+// system-scope release (cache writeback for host visibility); the render's
+// events only order and time work on this device, so they skip it
+// (hipEventDisableSystemFence).  Env WR_EVENT_SYSTEM_FENCE=1 restores it.
+unsigned ev_flags(unsigned base) {
+  static const bool sys = [] {
+    const char* e = std::getenv("WR_EVENT_SYSTEM_FENCE");
+    return e && std::atoi(e) != 0;
+  }();
+  return sys ? base : (base | hipEventDisableSystemFence);
+}
+
 struct Timer {
   wr_context* c;
   Pipe* p;
@@ -741,7 +800,7 @@ struct Timer {
     if (!c->timing || !p) return;
     if (p->ev_used >= p->events.size()) {
       hipEvent_t e;
-      (void)hipEventCreate(&e);
+      (void)hipEventCreateWithFlags(&e, ev_flags(hipEventDefault));
       p->events.push_back(e);
       p->ev_cat.push_back(0);
     }
@@ -751,8 +810,9 @@ struct Timer {
 };
 
 RayQueue rq(const float* o3, const float* d3, int cap, const int* cnt, float* t, int* prim,
-            const float* tmin = nullptr, const float* tmax = nullptr, const float* cut = nullptr) {
-  return RayQueue{o3, d3, cap, cnt, tmin, tmax, t, prim, cut};
+            const float* tmin = nullptr, const float* tmax = nullptr, const float* cut = nullptr,
+            const LateList* late = nullptr, int* late_n = nullptr, int late_bit = 0) {
+  return RayQueue{o3, d3, cap, cnt, tmin, tmax, t, prim, cut, late, late_n, late_bit};
 }
 // queues of one launch (empty `count` pointers are skipped)
 struct QueueList {
@@ -835,10 +895,63 @@ int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
   return WR_OK;
 }
 
+// Late lists of a pipeline (deferred hard rays), `recs` records each, for
+// buffer sets of `paths` paths; the side stream and its events on first use.
+// The lists' queue path arrays are the pipeline's current BDPT buffers.
+int ensure_late(Pipe& p, int paths, int recs) {
+  if (!p.side) {
+    HIPCHK(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+      HIPCHK(hipEventCreateWithFlags(&p.ev_res[k], ev_flags(hipEventDisableTiming)));
+      HIPCHK(hipEventCreateWithFlags(&p.ev_vtx[k], ev_flags(hipEventDisableTiming)));
+      HIPCHK(hipEventCreateWithFlags(&p.ev_late[k], ev_flags(hipEventDisableTiming)));
+    }
+  }
+  if (p.late_recs < static_cast<size_t>(recs) || p.late_paths < static_cast<size_t>(paths)) {
+    recs = std::max<int>(recs, static_cast<int>(p.late_recs));
+    paths = std::max<int>(paths, static_cast<int>(p.late_paths));
+    auto lay = [&](Arena& a, bool set) {
+      for (int m = 0; m < kGroup; ++m)
+        for (int k = 0; k < 2; ++k) {
+          LateList L{};
+          L.cap = recs;
+          L.o3 = a.take<float>(3 * size_t(recs));
+          L.d3 = a.take<float>(3 * size_t(recs));
+          L.t1 = a.take<float>(recs);
+          L.p1 = a.take<int>(recs);
+          L.pth = a.take<int>(recs);
+          L.tie = a.take<int>(recs);
+          L.t = a.take<float>(recs);
+          L.prim = a.take<int>(recs);
+          if (set) p.late_h[m][k] = L;
+        }
+      uint8_t* dl = a.take<uint8_t>(size_t(kGroup) * paths);
+      LateList* ld = a.take<LateList>(size_t(kGroup) * 2);
+      if (set) {
+        p.delayed = dl;
+        p.late_d = ld;
+      }
+    };
+    if (int rc = p.late_mem.reserve(measure([&](Arena& a) { lay(a, false); }))) return rc;
+    lay(p.late_mem, true);
+    p.late_recs = recs;
+    p.late_paths = paths;
+  }
+  for (int m = 0; m < kGroup; ++m)
+    for (int k = 0; k < 2; ++k) {
+      LateList& L = p.late_h[m][k];
+      L.path = p.bb[m].q_path[k];
+      L.delayed = p.delayed + size_t(m) * p.late_paths;
+    }
+  HIPCHK(hipMemcpyAsync(p.late_d, p.late_h, sizeof(p.late_h), hipMemcpyHostToDevice, p.stream));
+  return WR_OK;
+}
+
 // One persistent traversal launch over the queues of Q (max_rays bounds the
 // grid).  WR_TRACE_BVH: the verified-BVH search + its resolve launch instead.
 int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const TraceSlot& ts, Timer& tm, bool count,
-                 const TraceQueues& Q_, int max_rays, int mode = TRACE_PLAIN, bool hard_wave = false) {
+                 const TraceQueues& Q_, int max_rays, int mode = TRACE_PLAIN, bool hard_wave = false,
+                 hipEvent_t after_resolve = nullptr) {
   int* fetch = ts.fetch;
   TraceQueues Q = Q_;
   if (c->no_cut)  // measurement knob: the same launches without the dead-work elision
@@ -862,6 +975,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
                        dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), 0, stream, c->ds, c->fs,
                        Q, ctr, ts.t2, hard, ts.hard_n, static_cast<int>(ts.t2_cap));
+    if (after_resolve) (void)hipEventRecord(after_resolve, stream);  // the late lists are complete
     if (c->trace_log) (void)hipEventRecord(fb, stream);
     // the hard rays are a few in 10^4: a small grid drains any count (one
     // ray per wave for the API calls: up to 2048 at once, 8 waves per CU)
@@ -1081,6 +1195,7 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
     sum.fallback += h.fallback;
     sum.verify_rays += h.verify_rays;
     sum.verify_bad += h.verify_bad;
+    sum.deferred += h.deferred;
     for (int k = 0; k < 8; ++k) sum.stamps[k] += h.stamps[k];
   }
   st->closest_rays += static_cast<int64_t>(sum.closest);
@@ -1099,6 +1214,7 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
   st->verify_rays += static_cast<int64_t>(sum.verify_rays);
   st->verify_mismatches += static_cast<int64_t>(sum.verify_bad);
   st->pipelines = std::max<int64_t>(st->pipelines, n);
+  st->deferred_rays += static_cast<int64_t>(sum.deferred);
   if (c->trace_log && c->fast_on) {
     unsigned long long mx[3] = {0, 0, 0};
     for (int i = 0; i < n; ++i) {
@@ -1269,8 +1385,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   auto* c = new wr_context();
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->t_ref, hipEventDefault) != hipSuccess ||
-      hipEventCreateWithFlags(&c->t_null, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->t_ref, ev_flags(hipEventDefault)) != hipSuccess ||
+      hipEventCreateWithFlags(&c->t_null, ev_flags(hipEventDisableTiming)) != hipSuccess) {
     wr_destroy(c);
     return fail(WR_E_HIP, "hipStreamCreate failed");
   }
@@ -1280,7 +1396,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   for (Pipe& pp : c->pipes) {
     if (&pp == &c->pipes[0]) {
       pp.stream = c->stream;
-      if (hipEventCreateWithFlags(&pp.done, hipEventDisableTiming) != hipSuccess ||
+      if (hipEventCreateWithFlags(&pp.done, ev_flags(hipEventDisableTiming)) != hipSuccess ||
           hipMalloc(&pp.ctr, sizeof(DevCounters)) != hipSuccess ||
           hipMalloc(&pp.sc, kGroup * sizeof(StepCounters)) != hipSuccess) {
         wr_destroy(c);
@@ -1289,7 +1405,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       continue;
     }
     if (hipStreamCreateWithFlags(&pp.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&pp.done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&pp.done, ev_flags(hipEventDisableTiming)) != hipSuccess ||
         hipMalloc(&pp.ctr, sizeof(DevCounters)) != hipSuccess ||
         hipMalloc(&pp.sc, kGroup * sizeof(StepCounters)) != hipSuccess) {
       wr_destroy(c);
@@ -1309,6 +1425,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   if (const char* e = std::getenv("WR_PIECE_MIN")) c->piece_min = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("WR_TIE_WAVE_MAX")) c->tie_wave_max = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("WR_ISSUE_THREADS")) c->issue_threads = std::max(1, std::min(kMaxPipes, std::atoi(e)));
+  if (const char* e = std::getenv("WR_DEFER")) c->defer = std::atoi(e) != 0 ? 1 : 0;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
     // grid-stride vertex / resolve kernels: blocks per CU (knob WR_SHADE_GRID).
@@ -1636,6 +1753,12 @@ void wr_destroy(wr_context* c) {
     if (p.stream) (void)hipStreamSynchronize(p.stream);
     for (hipEvent_t e : p.events) (void)hipEventDestroy(e);
     if (p.done) (void)hipEventDestroy(p.done);
+    if (p.side) (void)hipStreamSynchronize(p.side);
+    for (int k = 0; k < 2; ++k)
+      for (hipEvent_t e : {p.ev_res[k], p.ev_vtx[k], p.ev_late[k]})
+        if (e) (void)hipEventDestroy(e);
+    if (p.side) (void)hipStreamDestroy(p.side);
+    p.late_mem.release();
     if (p.ctr) (void)hipFree(p.ctr);
     if (p.sc) (void)hipFree(p.sc);
     p.work.release();
@@ -1837,6 +1960,15 @@ static int issue_round(wr_context* c, int live, int nsteps, Fn&& fn, int np) {
 }
 }  // extern "C++"
 
+// Deferred hard rays on np pipelines: env WR_DEFER=1 only.
+static bool defer_enabled(const wr_context* c, int np) {
+  (void)np;
+  return c->defer > 0;  // off by default: measured slower (deferred hard rays)
+}
+
+// late-list records per group member and step parity (ties + scans) for pieces of `cap` paths
+static int late_records(int cap) { return 2 * std::max(4096, cap / 32); }
+
 static int check_bdpt(const wr_context* c, const wr_bdpt_params* prm, const float* film) {
   if (!c || !prm || !film) return fail(WR_E_ARG, "null argument");
   if (prm->width <= 0 || prm->height <= 0 || prm->iterations < 0) return fail(WR_E_ARG, "bad film size");
@@ -1872,6 +2004,19 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
     for (int i = 0; i < np; ++i)
       if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
   }
+  // Deferred hard rays: in BVH mode the extension rays a step's resolve cannot
+  // settle (near-ties, membership scans: 0.1-0.5 % of them) go to a late list
+  // instead of the step's k_fast_hard; the pipeline's side stream settles them
+  // (k_late_hard) and shades their paths one step later (k_late_vertex), while
+  // the pipeline shades every other path and traces on.  Step s's late work
+  // writes step s + 2's queues, so the pipeline waits for it only before that
+  // step's traversal.  A path is deferred once per pass, and each pass gets
+  // one step more (the light pass a bounce step, the camera pass extension
+  // rays at its last step): a deferred path's vertices come one step late.
+  const bool defer = c->fast_on && !c->stamps && defer_enabled(c, np);
+  if (defer)
+    for (int i = 0; i < np; ++i)
+      if (int rc = ensure_late(c->pipes[i], cap, late_records(cap))) return rc;
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
@@ -1896,8 +2041,11 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
     Pipe* pp = nullptr;
     BdptGroup GA;
     int gn = 0, nmax = 0;
+    bool late[kSlots] = {};  // late work issued at step slot
   };
-  const int nsteps = 2 * maxlen + 2;
+  // steps: light gen, light bounces b = 0 .. lb_n - 1, camera gen, camera bounces b = 0 .. maxlen
+  const int lb_n = maxlen - 1 + (defer ? 1 : 0);
+  const int nsteps = lb_n + maxlen + 3;
   auto issue = [&](GroupIssue& G, int step) -> int {
     Pipe& pp = *G.pp;
     const hipStream_t sm = pp.stream;
@@ -1908,45 +2056,106 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
       const BdptBuf::Sq& Q = pp.bb[m].sq[slot & 1];
       return rq(Q.o, Q.d, pp.bb[m].cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut);
     };
-    auto ext = [&](int m, int slot) {
+    // extension rays of step `slot`; bit: the pass's deferral bit (0: not deferrable)
+    auto ext = [&](int m, int slot, int bit) {
       const BdptBuf& B = pp.bb[m];
       const int q = slot & 1;
-      return rq(B.q_o[q], B.q_d[q], B.P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
+      if (!bit) return rq(B.q_o[q], B.q_d[q], B.P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
+      return rq(B.q_o[q], B.q_d[q], B.P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q], nullptr, nullptr, nullptr,
+                pp.late_d + 2 * m + q, pp.sc[m].late[slot], bit);
+    };
+    // before step `slot`'s traversal: the late work of step slot - 2 wrote its queues
+    auto wait_late = [&](int slot) -> int {
+      if (slot >= 2 && G.late[slot - 2]) HIPCHK(hipStreamWaitEvent(sm, pp.ev_late[slot & 1], 0));
+      return WR_OK;
+    };
+    // after step `slot`'s vertex launch: its late lists, on the side stream
+    auto issue_late = [&](int slot, bool camera, int g) -> int {
+      const int k = slot & 1;
+      LateArgs L;
+      for (int m = 0; m < kGroup; ++m) {
+        L.l[m] = pp.late_h[m][k];
+        L.n[m] = pp.sc[m].late[slot];
+      }
+      HIPCHK(hipEventRecord(pp.ev_vtx[k], sm));
+      HIPCHK(hipStreamWaitEvent(pp.side, pp.ev_res[k], 0));
+      const int hblocks = std::max(64, c->tie_wave_max);
+      hipLaunchKernelGGL(count ? k_late_hard<true> : k_late_hard<false>, dim3(hblocks + WR_SCAN_WAVES, gn),
+                         dim3(kTraceBlock), fast_lds_bytes(c->fs.depth), pp.side, c->ds, c->fs, L, pp.ctr, hblocks, 64,
+                         c->tie_wave_max);
+      if (c->verify)
+        hipLaunchKernelGGL(k_late_verify, dim3(64, gn), dim3(kTraceBlock), fast_lds_bytes(c->fs.depth), pp.side, c->ds,
+                           c->fs, L, pp.ctr);
+      HIPCHK(hipStreamWaitEvent(pp.side, pp.ev_vtx[k], 0));
+      const int lg = std::max(1, std::min(g, 64));
+      if (camera)
+        hipLaunchKernelGGL(k_late_vertex<true>, dim3(lg, gn), dim3(kShadeBlock), 0, pp.side, G.GA, L, slot);
+      else
+        hipLaunchKernelGGL(k_late_vertex<false>, dim3(lg, gn), dim3(kShadeBlock), 0, pp.side, G.GA, L, slot);
+      HIPCHK(hipEventRecord(pp.ev_late[k], pp.side));
+      G.late[slot] = true;
+      return WR_OK;
     };
     const int sq_max = G.nmax * (kVMax + 2);  // <= cap_sq
     const int g = shade_grid(c, G.nmax);
     if (step == 0) {
       HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
+      if (defer) HIPCHK(hipMemsetAsync(pp.delayed, 0, kGroup * pp.late_paths, sm));
+      for (bool& x : G.late) x = false;
       // ---------------- light pass (:67-131)
       hipLaunchKernelGGL(k_light_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA);
       tm.mark(WR_K_GEN);
-    } else if (step < maxlen) {
+    } else if (step <= lb_n) {
       const int b = step - 1;
+      // deferrable up to the last regular bounce (a deferred path's next ray,
+      // queue b + 2, is traced by the extra step b = maxlen - 1)
+      const int bit = (defer && b <= maxlen - 2) ? 1 : 0;
+      if (int rc = wait_late(b)) return rc;
       QueueList ql;
-      for (int m = 0; m < gn; ++m) ql.add(ext(m, b), A[m].n);
-      trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
+      for (int m = 0; m < gn; ++m) ql.add(ext(m, b, bit), A[m].n);
+      trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE, false,
+                   bit ? pp.ev_res[b & 1] : nullptr);
       hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA, b);
       tm.mark(WR_K_SHADE);
-    } else if (step == maxlen) {
+      if (bit)
+        if (int rc = issue_late(b, false, g)) return rc;
+    } else if (step == lb_n + 1) {
       // ---------------- camera pass (:133-264).  The light pass's splat rays
       // (connectToCamera) ride along with the primary rays; afterwards each
-      // bounce's shadow / aux rays ride along with the next bounce's extension rays.
+      // bounce's shadow / aux rays ride along with the next bounce's extension
+      // rays.  Every light vertex and splat, deferred ones too, comes first.
+      for (int b = lb_n - 1; b >= 0; --b)
+        if (G.late[b]) {
+          HIPCHK(hipStreamWaitEvent(sm, pp.ev_late[b & 1], 0));
+          break;
+        }
       hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA);
       tm.mark(WR_K_GEN);
     } else {
-      const int b = step - maxlen - 1;
+      const int b = step - lb_n - 2;
       const int slot = kCamSlot + b;
-      const bool more = b < maxlen;  // extension rays of bounce b exist
+      const bool more = b < maxlen + (defer ? 1 : 0);  // extension rays of bounce b exist
+      const int bit = (defer && b <= maxlen - 1) ? 2 : 0;
+      if (int rc = wait_late(slot)) return rc;
       QueueList ql;
       for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), A[m].n * (kVMax + 2));
       if (more)
-        for (int m = 0; m < gn; ++m) ql.add(ext(m, slot), A[m].n);
-      trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE);
+        for (int m = 0; m < gn; ++m) ql.add(ext(m, slot, bit), A[m].n);
+      trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE, false,
+                   bit ? pp.ev_res[slot & 1] : nullptr);
       // resolve this step's shadow / aux rays and shade its vertices in one launch
       const int nres = shade_grid(c, sq_max);
       hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, G.GA, slot, nres,
                          more ? 1 : 0);
       tm.mark(WR_K_SHADE);
+      if (bit)
+        if (int rc = issue_late(slot, true, g)) return rc;
+      if (b == maxlen)  // the group's last step: join the side stream's remaining work
+        for (int s2 = slot; s2 >= kCamSlot; --s2)
+          if (G.late[s2]) {
+            HIPCHK(hipStreamWaitEvent(sm, pp.ev_late[s2 & 1], 0));
+            break;
+          }
     }
     return WR_OK;
   };
@@ -2317,6 +2526,7 @@ static void add_stats(wr_stats* d, const wr_stats& s) {
   d->verify_rays += s.verify_rays;
   d->verify_mismatches += s.verify_mismatches;
   d->pipelines = std::max(d->pipelines, s.pipelines);
+  d->deferred_rays += s.deferred_rays;
 }
 
 static int ensure_dev_film(wr_context* d, float** buf, size_t* have, size_t nf) {
@@ -2410,6 +2620,46 @@ static int multi_render(wr_context* c, size_t nf, float* film, int film_on_devic
 }
 
 }  // extern "C++"
+
+// The work buffers every pipeline of one device needs for renders of this
+// kind and film size: what the first render would allocate (SurfaceIntegrator::
+// init's share of the set-up, surfaceIntegrator.h:14-34), so that render()
+// itself only renders.
+static int reserve_one(wr_context* c, int kind, int W, int H) {
+  HIPCHK(hipSetDevice(c->device));
+  const int P = W * H;
+  int fit = 0, cap = P;
+  if (kind == WR_INTEGRATOR_BDPT) {
+    wr_bdpt_params prm{};
+    prm.width = W;
+    prm.height = H;
+    cap = piece_capacity(c, P, bdpt_unit(&prm));
+    fit = pipelines_that_fit(c, 1, cap, kGroup, c->npipes);
+  } else {
+    fit = pipelines_that_fit(c, kind == WR_INTEGRATOR_VCM ? 3 : 2, P, kGroup, c->npipes);
+  }
+  if (fit < 1) return WR_E_HIP;  // message set by the allocation
+  const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
+  const size_t per = kGroup * (std::max(cap_sq, size_t(cap)) + size_t(cap));
+  for (int i = 0; i < fit; ++i)
+    if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
+  if (kind == WR_INTEGRATOR_BDPT && c->fast_on && !c->stamps && defer_enabled(c, fit))
+    for (int i = 0; i < fit; ++i)
+      if (int rc = ensure_late(c->pipes[i], cap, late_records(cap))) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  return WR_OK;
+}
+
+int wr_reserve(wr_context* c, int integrator, int32_t width, int32_t height) {
+  if (!c) return fail(WR_E_ARG, "null argument");
+  if (integrator < WR_INTEGRATOR_BDPT || integrator > WR_INTEGRATOR_PATH) return fail(WR_E_ARG, "bad integrator");
+  if (width <= 0 || height <= 0) return fail(WR_E_ARG, "bad film size");
+  if (static_cast<int64_t>(width) * height >= (1 << 30) / (kVMax + 2)) return fail(WR_E_ARG, "film too large for one context");
+  if (int rc = reserve_one(c, integrator, width, height)) return rc;
+  for (wr_context* d : c->subs)
+    if (int rc = reserve_one(d, integrator, width, height)) return rc;
+  return WR_OK;
+}
 
 int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int film_on_device, wr_stats* st) {
   if (int rc = check_bdpt(c, prm, film)) return rc;

@@ -162,6 +162,28 @@ __device__ __forceinline__ bool sph_hit(const DevScene& S, int prim, V3 o, V3 d,
   return true;
 }
 
+// Hard rays taken off a render pipeline's critical path (WR_TRACE_BVH, BDPT
+// extension rays; wr_render.hip, "deferred hard rays").  k_fast_resolve copies
+// a deferrable ray it cannot settle into this list and marks its queue entry
+// pending (out_prim = kPendingPrim: the vertex kernel skips it).  A side stream
+// settles the list (k_late_hard) and shades the paths one step later.  A path
+// is deferred at most once per pass (the queue's late_bit of delayed[path]).
+// Records: tie entries at [0, n[0]), scan entries at [cap / 2, cap / 2 +
+// n[1]), n = the queue's late_n (the step's counters).
+struct LateList {
+  int cap;
+  const int* path;    // the queue's path index per entry
+  uint8_t* delayed;   // per path (local index)
+  float *o3, *d3;     // [3][cap]
+  float* t1;          // the search's smallest hit (input of the resolution)
+  int* p1;
+  int* pth;           // path of the record
+  int* tie;           // scan entries: a near-tie on a many-leaf primitive
+  float* t;           // the settled answer (k_late_hard)
+  int* prim;
+};
+constexpr int kPendingPrim = -2;
+
 // A ray queue: SoA origins / directions [3][cap], count on device, optional
 // per-ray [tmin, tmax], and the (t, prim) outputs.
 struct RayQueue {
@@ -176,6 +198,10 @@ struct RayQueue {
   // shadow rays (Scene::occluded, scene.cpp:55-69): a ray may stop as soon as
   // its best hit is below cut[k] -- see occl_cut.  nullptr / -INF: closest hit
   const float* cut;
+  // deferrable hard rays (device pointer; nullptr: settled in the launch)
+  const LateList* late;
+  int* late_n;   // [2] this step's late-list counts
+  int late_bit;  // the pass's bit of LateList::delayed
 };
 
 // Scene::occluded(p1, dir, p2) answers "unoccluded" iff the closest hit is

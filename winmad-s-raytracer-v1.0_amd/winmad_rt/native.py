@@ -16,13 +16,15 @@ LIB_PATH = os.environ.get("WR_LIB") or os.path.join(PKG_DIR, "libwinmad_rt.so")
 WR_OK, WR_E_ARG, WR_E_IO, WR_E_HIP, WR_E_SCENE, WR_E_NODEVICE = 0, -1, -2, -3, -4, -5
 K_TRACE, K_SHADE, K_RESOLVE, K_GEN, K_OTHER = 0, 1, 2, 3, 4
 TRACE_REFERENCE, TRACE_BVH = 0, 1
+INTEGRATOR_BDPT, INTEGRATOR_VCM, INTEGRATOR_PATH = 0, 1, 2
 
 # every entry point declared in include/winmad_rt.h
 EXPORTS = ["wr_scene_load", "wr_scene_from_desc", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free",
            "wr_device_count", "wr_create", "wr_create_multi", "wr_context_devices", "wr_destroy", "wr_comm_unique_id",
            "wr_comm_init", "wr_film_reduce", "wr_set_pipelines", "wr_set_trace_mode", "wr_trace_closest", "wr_occluded",
            "wr_render_bdpt", "wr_render_path", "wr_render_vcm", "wr_path_radiance", "wr_film_write_ppm",
-           "wr_film_write_image", "wr_checkpoint_save", "wr_checkpoint_load", "wr_last_error", "wr_api_version"]
+           "wr_film_write_image", "wr_checkpoint_save", "wr_checkpoint_load", "wr_last_error", "wr_api_version",
+           "wr_reserve"]
 CKPT_BDPT, CKPT_VCM, CKPT_PT = 1, 2, 3
 
 
@@ -83,7 +85,8 @@ class WrStats(C.Structure):
                 ("vm_queries", C.c_int64), ("vm_found", C.c_int64), ("vm_merged", C.c_int64),
                 ("prim_tests", C.c_int64), ("bvh_nodes", C.c_int64), ("bvh_tests", C.c_int64),
                 ("kd_replay_steps", C.c_int64), ("fallback_rays", C.c_int64), ("verify_rays", C.c_int64),
-                ("verify_mismatches", C.c_int64), ("pipelines", C.c_int64)]
+                ("verify_mismatches", C.c_int64), ("pipelines", C.c_int64),
+                ("deferred_rays", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
@@ -142,6 +145,7 @@ def lib():
         L.wr_destroy.restype = None
         L.wr_set_pipelines.argtypes = [P, I]
         L.wr_set_trace_mode.argtypes = [P, I]
+        L.wr_reserve.argtypes = [P, I, I, I]
         L.wr_trace_closest.argtypes = [P, C.POINTER(WrRay), I64, C.POINTER(WrHit)]
         L.wr_occluded.argtypes = [P, C.POINTER(WrRay), C.POINTER(C.c_float), I64, C.POINTER(C.c_uint8)]
         L.wr_render_bdpt.argtypes = [P, C.POINTER(WrBdptParams), P, I, C.POINTER(WrStats)]
@@ -293,6 +297,11 @@ class Context:
     def set_pipelines(self, n):
         """Concurrent render pipelines (streams) for render_bdpt / render_path."""
         check(lib().wr_set_pipelines(self.h, n))
+
+    def reserve(self, integrator, width, height):
+        """wr_reserve: allocate the work buffers of renders of this kind
+        (INTEGRATOR_BDPT / _VCM / _PATH) and film size now."""
+        check(lib().wr_reserve(self.h, integrator, width, height))
 
     def set_trace_mode(self, mode):
         """TRACE_REFERENCE (the reference's KD walk) or TRACE_BVH (verified BVH
