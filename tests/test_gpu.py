@@ -368,9 +368,11 @@ def test_trace_large_batch_matches_oracle_and_small_batches():
 
 
 @pytest.mark.parametrize("pipes", [1, 3, 8])
-def test_pipeline_count_does_not_change_the_render(pipes):
+def test_pipeline_count_does_not_change_the_render(pipes, monkeypatch):
     """Iterations / samples dealt to 1..16 concurrent streams: same rays, same film
-    up to the order of float atomics."""
+    up to the order of float atomics.  (WR_PIECE_MIN: shares of this small
+    render go to every pipeline.)"""
+    monkeypatch.setenv("WR_PIECE_MIN", "1024")
     path = _scenes.torus(96, 64)
     s = native.Scene(path)
     c = native.Context(s, 0)
@@ -378,6 +380,7 @@ def test_pipeline_count_does_not_change_the_render(pipes):
     ref, rs = c.render_bdpt(96, 64, iterations=5, seed=21)
     c.set_pipelines(pipes)
     got, gs = c.render_bdpt(96, 64, iterations=5, seed=21)
+    assert rs.pipelines == 2 and gs.pipelines == pipes, (rs.pipelines, gs.pipelines)
     assert gs.closest_rays == rs.closest_rays and gs.shadow_rays == rs.shadow_rays
     assert np.allclose(got, ref, rtol=1e-4, atol=1e-6)
     cb = native.Context(native.Scene(_scenes.cbox(64, 48)), 0)

@@ -201,6 +201,7 @@ def test_deferred_hard_rays_render_the_same_film(name, maker, W, H, its, monkeyp
     path = maker()
     s = native.Scene(path)
     films = {}
+    monkeypatch.setenv("WR_PIECE_MIN", "4096")  # every pipeline gets a share of these small renders
     for defer in ("1", "0"):
         monkeypatch.setenv("WR_DEFER", defer)
         c = native.Context(s, 0)
@@ -209,6 +210,7 @@ def test_deferred_hard_rays_render_the_same_film(name, maker, W, H, its, monkeyp
         films[defer] = c.render_bdpt(W, H, iterations=its, seed=5489)
         c.close()
     (fa, sa), (fb, sb) = films["1"], films["0"]
+    assert sa.pipelines == 4
     assert sa.deferred_rays > 0 and sb.deferred_rays == 0, (sa.deferred_rays, sb.deferred_rays)
     assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
     assert _film_close(fa, fb)

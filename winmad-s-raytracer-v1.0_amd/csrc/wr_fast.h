@@ -1180,6 +1180,28 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   }
 }
 
+// Is Triangle::hit's denominator (triangle.cpp:43-44) for this direction
+// within 1e-5 of the magnitude of its products, i.e. does the ray run nearly in
+// the triangle's plane?  There the computed (beta, gamma, t) approach their
+// rounding noise, and a coplanar neighbour outside the search window could be
+// accepted by the reference at a noise t; such rays take the KD walk.  The
+// noise level is ~4 ulp (2.4e-7), so 1e-5 leaves a factor 40.
+constexpr float kGrazeRel = 1e-5f;
+// tie-list entries: launch index, | kWalkEntry for a ray the KD walk settles
+constexpr int kWalkEntry = 1 << 30;
+__device__ __forceinline__ bool grazing_test(const DevScene& S, int prim, V3 dir) {
+  if (S.prim_type[prim] != 0) return false;
+  const float4 g = S.prim_tri[prim];
+  const float2 g2 = S.prim_tri2[prim];
+  const float A = g.x, B = g.y, C = g.z, D = g.w, E = g2.x, F = g2.y;
+  const float G = dir.x, H = dir.y, I = dir.z;
+  const float EIHF = E * I - H * F, GFDI = G * F - D * I, DHEG = D * H - E * G;
+  const float den = A * EIHF + B * GFDI + C * DHEG;
+  const float mag = fabsf(A) * (fabsf(E * I) + fabsf(H * F)) + fabsf(B) * (fabsf(G * F) + fabsf(D * I)) +
+                    fabsf(C) * (fabsf(D * H) + fabsf(E * G));
+  return fabsf(den) <= kGrazeRel * mag;
+}
+
 // one atomic per wave: this lane's slot in a list (or -1 if !want)
 __device__ __forceinline__ int fast_append(int* counter, bool want) {
   const unsigned long long m = __ballot(want);
@@ -1206,7 +1228,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
   // every lane of the wave takes part in each list append (whole iterations)
   for (int base = blockIdx.x * 64; base < QI.n; base += gridDim.x * 64) {
     const int idx = base + lane;
-    bool need = false, scan = false, big_tie = false;
+    bool need = false, scan = false, big_tie = false, walk = false;
     int q = 0, r = 0, p1 = -1;
     float t1 = WR_INF;
     V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 0.f);
@@ -1226,7 +1248,13 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
       // p1's membership record: one line with its first four leaves' cells
       const float4* pr = F.prim_rec + 8 * static_cast<size_t>(max(p1, 0));
       const float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3], c4 = pr[4], c5 = pr[5];
-      if (p1 >= 0) {  // (no hit anywhere: a miss for the reference too)
+      if (p1 >= 0 && grazing_test(S, p1, d)) {
+        // the ray runs within ~1e-5 (relative) of the winner's plane: Cramer's
+        // rule is near its rounding noise there, beyond the search margins'
+        // reach (margins) -- the KD walk settles it
+        need = true;
+        walk = true;
+      } else if (p1 >= 0) {  // (no hit anywhere: a miss for the reference too)
         const bool tie = !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0);
         if (tie) {
           // a tie on a many-leaf primitive (walls, floors: up to thousands of
@@ -1265,7 +1293,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
     // late list -- settled off the pipeline's critical path, its path shaded
     // one step later -- unless its path was deferred before in this pass.
     // Rare (0.1-0.5 % of rays): one atomic per listed ray.
-    if (need || scan) {
+    if ((need || scan) && !walk) {
       const LateList* LL = qfield(Q, q, [](const RayQueue& x) { return x.late; });
       if (LL) {
         const int pth = LL->path[r];
@@ -1294,7 +1322,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
       }
     }
     const int slot = fast_append(hard_n, need);
-    if (need) hard[slot] = idx;
+    if (need) hard[slot] = walk ? (idx | kWalkEntry) : idx;
     // the scan list fills the same array from the top (a ray is in one list)
     const int sslot = fast_append(hard_n + 1, scan);
     if (scan) hard[hcap - 1 - sslot] = big_tie ? ~idx : idx;
@@ -1319,10 +1347,10 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
 template <bool COUNT, bool WAVE>
 __device__ __forceinline__ bool settle_ray(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin, float rtmax,
                                            float t1, int* stk_node, float* stk_tmin, float* outt, int* outp, int r,
-                                           bool lead, FastCounters& ctr) {
+                                           bool lead, FastCounters& ctr, bool walk = false) {
   float tb;
   int pb;
-  if (!(F.diag & 2)) {
+  if (!(F.diag & 2) && !walk) {
     uint32_t steps = 0, psteps = 0;
     int dbg = 0;
     const uint64_t c0 = COUNT ? wall_clock64() : 0;
@@ -1385,7 +1413,9 @@ struct ListedRay {
   int p1, r;
   float* outt;
   int* outp;
+  bool walk;  // straight to the KD walk (k_fast_resolve's grazing winners)
 };
+
 __device__ __forceinline__ ListedRay listed_ray(const TraceQueues& Q, const QueueIndex& QI, int idx) {
   ListedRay L;
   int q;
@@ -1404,6 +1434,7 @@ __device__ __forceinline__ ListedRay listed_ray(const TraceQueues& Q, const Queu
   L.d = v3(d3[r], d3[cap + r], d3[2 * cap + r]);
   L.rtmin = tmn ? tmn[r] : 0.f;
   L.rtmax = tmx ? tmx[r] : WR_INF;
+  L.walk = false;
   return L;
 }
 
@@ -1420,7 +1451,7 @@ __device__ __forceinline__ void hard_rays(const DevScene& S, const FastScene& F,
     for (int i = bid; i < nh; i += nb) {
       const ListedRay L = get(i);
       settle_ray<COUNT, true>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r, lead,
-                              ctr);
+                              ctr, L.walk);
     }
     return;
   }
@@ -1433,7 +1464,7 @@ __device__ __forceinline__ void hard_rays(const DevScene& S, const FastScene& F,
     if (i < nh) {
       L = get(i);
       back = !settle_ray<COUNT, false>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r,
-                                       true, ctr);
+                                       true, ctr, L.walk);
     }
     for (unsigned long long m = __ballot(back); m != 0ull; m &= m - 1ull) {
       const int src = __ffsll(static_cast<unsigned long long>(m)) - 1;
@@ -1456,7 +1487,12 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
                                           FastCounters& ctr) {
   const QueueIndex QI(Q);
   const int nh = (F.diag & (32 | 128)) ? 0 : hard_n[0];
-  hard_rays<COUNT, WAVE>(S, F, nh, [&](int i) { return listed_ray(Q, QI, hard[i]); }, bid, nb, lds, ctr);
+  hard_rays<COUNT, WAVE>(S, F, nh, [&](int i) {
+    const int e = hard[i];
+    ListedRay L = listed_ray(Q, QI, e & ~kWalkEntry);
+    L.walk = (e & kWalkEntry) != 0;
+    return L;
+  }, bid, nb, lds, ctr);
 }
 
 // The scan list (k_fast_resolve's kScan rays and near-ties on many-leaf
@@ -1535,6 +1571,7 @@ __device__ __forceinline__ ListedRay late_ray(const LateList& LL, int i) {
   L.r = i;
   L.outt = LL.t;
   L.outp = LL.prim;
+  L.walk = false;
   return L;
 }
 // k_late_hard: a late list's tie entries (blocks [0, hard_blocks): one per

@@ -494,9 +494,14 @@ struct wr_context {
   bool no_cut = false;            // WR_TRACE_NO_CUT=1: shadow rays run to the end (no occl_cut)
   bool timing = false;
   // BDPT pieces (plan_pieces): at most piece_cap paths per buffer set, shares of
-  // at least piece_min paths per pipeline (env WR_PIECE_CAP / WR_PIECE_MIN)
+  // at least piece_min paths per pipeline (env WR_PIECE_CAP / WR_PIECE_MIN).
+  // A short render runs on fewer, fuller pipelines: measured C2 Mrays/s for
+  // piece_min 16 K / 384 K / 512 K / 640 K / 768 K / 1 M paths at 1 iteration
+  // 656 / 771 / 951 / 1,002 / 868 / 841, at 4 iterations 1,559 / 1,585 /
+  // 1,334 / 1,659 / 1,669 / 1,717; 20 and 256 iterations within noise
+  // (profiles/r3/piece_min)
   int piece_cap = 1 << 21;
-  int piece_min = 16384;
+  int piece_min = 655360;
   // pipelines' k_fast_hard: launches with at most this many ties resolve them
   // one per wave (env WR_TIE_WAVE_MAX; 0: always one per lane)
   int tie_wave_max = 512;
