@@ -346,6 +346,10 @@ def main():
                     "tests_per_ray": round(cst.prim_tests / rays, 2),
                     "nodes_per_ray": round((cst.inner_visits + cst.leaf_visits) / rays, 2),
                     "trace_share_of_wall": round(st.trace_wall_ms / 1e3 / max(1e-9, elapsed), 3)}
+        if traffic:
+            # measured HBM bytes per traversal step against the minimum ray I/O
+            # (48 B per ray: origin, direction, hit t and primitive)
+            roofline["traffic_over_ray_io"] = round(traffic / (48.0 * rays / max(1, trace_launches)), 3)
         if bvh:
             roofline["kernel"] = "k_trace_fast (verified BVH closest hit) + k_trace over its fallback rays"
             roofline["algorithmic_bytes"] = ("BVH: 48 B per ray + 64 B per node + 48 B per triangle test + 8 B per "

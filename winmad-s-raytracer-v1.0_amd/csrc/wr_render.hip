@@ -2003,10 +2003,12 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   if (fit < 1) return WR_E_HIP;  // message set by the allocation
   const PiecePlan plan = plan_pieces(f_lo, f_hi, P, unit, cap, fit, c->piece_min);
   const int np = plan.pipes();
-  {  // WR_TRACE_BVH t2 scratch: a launch takes <= kGroup x (shadow / aux + extension) queues
+  {  // WR_TRACE_BVH t2 scratch: a launch takes <= kGroup x (shadow / aux + extension) queues.
+     // Laid out on every pipeline that fits, as the work buffers are: a short
+     // render (a warm-up) on few of them leaves nothing to allocate to a long one
     const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
     const size_t per = kGroup * (std::max(cap_sq, size_t(cap)) + size_t(cap));
-    for (int i = 0; i < np; ++i)
+    for (int i = 0; i < fit; ++i)
       if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
   }
   // Deferred hard rays: in BVH mode the extension rays a step's resolve cannot
@@ -2020,7 +2022,7 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   // rays at its last step): a deferred path's vertices come one step late.
   const bool defer = c->fast_on && !c->stamps && defer_enabled(c, np);
   if (defer)
-    for (int i = 0; i < np; ++i)
+    for (int i = 0; i < fit; ++i)
       if (int rc = ensure_late(c->pipes[i], cap, late_records(cap))) return rc;
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
@@ -2230,7 +2232,7 @@ static int render_vcm_one(wr_context* c, const wr_vcm_params* prm, float* film, 
   {  // WR_TRACE_BVH t2 scratch: a launch takes <= kGroup x (shadow / aux + extension) queues
     const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
     const size_t per = kGroup * (std::max(cap_sq, size_t(P)) + size_t(P));
-    for (int i = 0; i < np; ++i)
+    for (int i = 0; i < fit; ++i)
       if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
   }
   float* dfilm = nullptr;
@@ -2442,7 +2444,7 @@ static int render_path_one(wr_context* c, const wr_path_params* prm, float* film
   {  // WR_TRACE_BVH t2 scratch: a launch takes <= kGroup x (shadow / aux + extension) queues
     const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
     const size_t per = kGroup * (std::max(cap_sq, size_t(P)) + size_t(P));
-    for (int i = 0; i < np; ++i)
+    for (int i = 0; i < fit; ++i)
       if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
   }
   float* dfilm = nullptr;
