@@ -260,13 +260,24 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
   }
 }
 
-__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGroup G_, int slot) {
+template <bool CAMERA>
+__device__ __forceinline__ void late_vertex_body(const BdptArgs& A, const LateList& LL, const int* cnt, int slot,
+                                                 int bid, int nblk);
+// Blocks [0, gridDim.x - nlate) shade this step's vertices, the last nlate
+// blocks the previous step's deferred ones (late_vertex_body).
+__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGroup G_, int slot, LateArgs L,
+                                                                         int nlate) {
   const BdptArgs& A = G_.a[blockIdx.y];
+  const int nmain = static_cast<int>(gridDim.x) - nlate;
+  if (static_cast<int>(blockIdx.x) >= nmain) {
+    late_vertex_body<false>(A, L.l[blockIdx.y], L.n[blockIdx.y], slot, blockIdx.x - nmain, nlate);
+    return;
+  }
   const BdptBuf& B = A.B;
   const int P = B.P, cur = slot & 1;
   const int n = A.sc->ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
-  const int gstride = gridDim.x * blockDim.x;
+  const int gstride = nmain * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;  // whole waves reach the appends
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
     int p = -1, prim = -1;
@@ -620,20 +631,20 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
 }
 
 // Deferred vertices (WR_TRACE_BVH, "deferred hard rays" in wr_render.hip):
-// the paths whose step-`slot` hit was settled off the critical path
-// (k_late_hard) are shaded one step later, into the queues of step slot + 2.
-// Light vertices feed only their own path's camera connections (:130,
-// :222-229) and every path keeps its own state, counters and random numbers,
-// so the film is the one of the undeferred render.
+// the paths whose step-(slot - 1) hit was settled off the critical path (by
+// the blocks of step slot's search launch) are shaded one step late, by extra
+// blocks of step slot's vertex launch, into the same queues as this step's
+// vertices (step slot + 1).  Light vertices feed only their own path's camera
+// connections (:130, :222-229) and every path keeps its own state, counters
+// and random numbers, so the film is the one of the undeferred render.
 template <bool CAMERA>
-__global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_late_vertex(BdptGroup G_, LateArgs L, int slot) {
-  const BdptArgs& A = G_.a[blockIdx.y];
-  const LateList& LL = L.l[blockIdx.y];
+__device__ __forceinline__ void late_vertex_body(const BdptArgs& A, const LateList& LL, const int* cnt, int slot,
+                                                 int bid, int nblk) {
   const int half = LL.cap >> 1;
-  const int nt = min(L.n[blockIdx.y][0], half), n = nt + min(L.n[blockIdx.y][1], half);
-  const int gstride = gridDim.x * blockDim.x;
+  const int nt = min(cnt[0], half), n = nt + min(cnt[1], half);
+  const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nround; j += gstride) {
+  for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
     int p = -1, prim = -1;
     float t = 0.f;
     V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 0.f);
@@ -645,8 +656,8 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_late_vertex(BdptGr
       o = ld3(LL.o3, LL.cap, i);
       d = ld3(LL.d3, LL.cap, i);
     }
-    if (CAMERA) camera_vertex(A, p, prim, t, o, d, slot + 2);
-    else light_vertex(A, p, prim, t, o, d, slot + 2);
+    if (CAMERA) camera_vertex(A, p, prim, t, o, d, slot + 1);
+    else light_vertex(A, p, prim, t, o, d, slot + 1);
   }
 }
 
@@ -728,9 +739,13 @@ __device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int
 // One camera-pass step after its traversal: resolve the step's shadow / aux
 // rays (blocks [0, nres)) and shade its camera vertices (the rest) -- they touch
 // different queue / DI buffers.  The last step has no vertices (shade = 0).
+// ... blocks [0, nres) resolve, then this step's vertices, then (the last
+// nlate blocks) the previous step's deferred vertices.
 __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_camera_step(BdptGroup G_, int slot, int nres,
-                                                                         int shade) {
+                                                                         int shade, LateArgs L, int nlate) {
   const BdptArgs& A = G_.a[blockIdx.y];
-  if (static_cast<int>(blockIdx.x) < nres) sq_resolve_body(A, slot, blockIdx.x, nres);
-  else if (shade) camera_shade_body(A, slot, blockIdx.x - nres, gridDim.x - nres);
+  const int b = static_cast<int>(blockIdx.x), nmain = static_cast<int>(gridDim.x) - nlate;
+  if (b < nres) sq_resolve_body(A, slot, b, nres);
+  else if (b >= nmain) late_vertex_body<true>(A, L.l[blockIdx.y], L.n[blockIdx.y], slot, b - nmain, nlate);
+  else if (shade) camera_shade_body(A, slot, b - nres, nmain - nres);
 }

@@ -893,11 +893,12 @@ __device__ __forceinline__ auto qfield(const TraceQueues& Q, int q, Fn field) {
 
 template <bool COUNT>
 __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, int* fetch,
-                                           float* t2buf, int2* spill, uint32_t* lds, FastCounters& ctr) {
+                                           float* t2buf, int2* spill, uint32_t* lds, FastCounters& ctr,
+                                           int bid, int nblk) {  // this block's index among the launch's nblk search blocks
   const int lane = __lane_id();
   int* stk_link = reinterpret_cast<int*>(lds) + lane;
   uint16_t* stk_t = reinterpret_cast<uint16_t*>(reinterpret_cast<int*>(lds) + min(F.sdepth, kLdsStack) * 64) + lane;
-  const size_t gl = static_cast<size_t>(gridDim.x) * 64, gidx = static_cast<size_t>(blockIdx.x) * 64 + lane;
+  const size_t gl = static_cast<size_t>(nblk) * 64, gidx = static_cast<size_t>(bid) * 64 + lane;
   const QueueIndex QI(Q);
   const int n = QI.n;
   // Waves past the ones the rays need leave before touching the shared cursor:
@@ -909,8 +910,8 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
 #ifndef WR_GRAB_ADAPT
 #define WR_GRAB_ADAPT 1
 #endif
-  const int grab = WR_GRAB_ADAPT && n <= 64 * static_cast<int>(gridDim.x) ? 64 : kRayGrab;
-  if (static_cast<int>(blockIdx.x) * grab >= n) return;
+  const int grab = WR_GRAB_ADAPT && n <= 64 * nblk ? 64 : kRayGrab;
+  if (bid * grab >= n) return;
   int r = -1, qi = 0, lidx = 0;
   bool pool = true;
   int pb = 0, pe = 0;
@@ -1579,11 +1580,10 @@ __device__ __forceinline__ ListedRay late_ray(const LateList& LL, int i) {
 // entries (the other blocks, one per wave).  Same resolutions as k_fast_hard.
 template <bool COUNT>
 __device__ __forceinline__ void late_hard(const DevScene& S, const FastScene& F, const LateList& LL, const int* n,
-                                          int hard_blocks, int lane_blocks, int wave_max, uint32_t* lds,
-                                          FastCounters& ctr) {
+                                          int b, int nb, int hard_blocks, int lane_blocks, int wave_max,
+                                          uint32_t* lds, FastCounters& ctr) {
   const int half = LL.cap >> 1;
   const int nt = min(n[0], half), ns = min(n[1], half);
-  const int b = static_cast<int>(blockIdx.x);
   if (b < hard_blocks) {
     auto get = [&](int i) { return late_ray(LL, i); };
     if (nt <= wave_max)
@@ -1594,7 +1594,7 @@ __device__ __forceinline__ void late_hard(const DevScene& S, const FastScene& F,
     scan_rays<COUNT>(S, F, ns, [&](int i, bool& tie) {
       tie = LL.tie[half + i] != 0;
       return late_ray(LL, half + i);
-    }, b - hard_blocks, static_cast<int>(gridDim.x) - hard_blocks, lds, ctr);
+    }, b - hard_blocks, nb - hard_blocks, lds, ctr);
   }
 }
 

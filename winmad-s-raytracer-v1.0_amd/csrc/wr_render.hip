@@ -225,15 +225,30 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
     else atomicAdd(&ctr->lat[k], static_cast<unsigned long long>(lat[k]));
   }
 }
-template <bool COUNT>
 #ifndef WR_FAST_WAVES
 #define WR_FAST_WAVES 4  // minimum waves per SIMD the search's registers must allow
 #endif
+// LATE: blocks [0, lblocks) settle the previous step's deferred hard rays
+// (its late lists, late_hard) beside this step's search; they come first so
+// that they are dispatched with the search's persistent blocks, not after them
+template <bool COUNT, bool LATE>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WR_FAST_WAVES, 8))) WR_NO_PK_FP32
-k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* spill) {
+k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* spill,
+             LateArgs L, int lblocks, int gn, int hblocks, int lane_blocks, int wave_max) {
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
-  trace_fast<COUNT>(S, F, Q, fetch, t2buf, spill, smem, fc);
+  const int b = static_cast<int>(blockIdx.x);
+  if (LATE && b < lblocks) {
+    const int per = lblocks / gn, m = b / per, bb = b % per;
+    late_hard<COUNT>(S, F, L.l[m], L.n[m], bb, per, hblocks, lane_blocks, wave_max, smem, fc);
+    if (bb == 0 && threadIdx.x == 0) {
+      const int half = L.l[m].cap >> 1;
+      atomicAdd(&ctr->deferred, static_cast<unsigned long long>(min(L.n[m][0], half) + min(L.n[m][1], half)));
+    }
+  } else {
+    trace_fast<COUNT>(S, F, Q, fetch, t2buf, spill, smem, fc, b - (LATE ? lblocks : 0),
+                      static_cast<int>(gridDim.x) - (LATE ? lblocks : 0));
+  }
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 template <bool COUNT>
@@ -281,21 +296,6 @@ k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const int*
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 
-// The deferred hard rays of one pipeline step (blockIdx.y = group member),
-// on the pipeline's side stream; grid as k_fast_hard's.
-template <bool COUNT>
-__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32 WR_HARD_OCC
-k_late_hard(DevScene S, FastScene F, LateArgs L, DevCounters* ctr, int hard_blocks, int lane_blocks, int wave_max) {
-  extern __shared__ uint32_t smem[];
-  FastCounters fc{};
-  late_hard<COUNT>(S, F, L.l[blockIdx.y], L.n[blockIdx.y], hard_blocks, lane_blocks, wave_max, smem, fc);
-  if (COUNT) fast_counts<COUNT>(ctr, fc);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const int half = L.l[blockIdx.y].cap >> 1;
-    atomicAdd(&ctr->deferred, static_cast<unsigned long long>(min(L.n[blockIdx.y][0], half) +
-                                                              min(L.n[blockIdx.y][1], half)));
-  }
-}
 // WR_BVH_VERIFY: the late lists' answers against the KD walk
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
 k_late_verify(DevScene S, FastScene F, LateArgs L, DevCounters* ctr) {
@@ -452,10 +452,8 @@ struct Pipe {
   std::vector<int> ev_cat;
   size_t ev_used = 0;
   hipEvent_t done = nullptr;
-  // deferred hard rays (BDPT, WR_TRACE_BVH): a side stream settles a step's
-  // late lists and shades their paths while the pipeline goes on
-  hipStream_t side = nullptr;
-  hipEvent_t ev_res[2]{}, ev_vtx[2]{}, ev_late[2]{};  // per step parity
+  // deferred hard rays (BDPT, WR_TRACE_BVH): a step's late lists, settled and
+  // shaded by extra blocks of the next step's launches
   Arena late_mem;
   size_t late_recs = 0, late_paths = 0;  // records per list, paths per member laid out
   LateList late_h[kGroup][2]{};          // host copies: [member][step parity]
@@ -901,17 +899,9 @@ int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
 }
 
 // Late lists of a pipeline (deferred hard rays), `recs` records each, for
-// buffer sets of `paths` paths; the side stream and its events on first use.
-// The lists' queue path arrays are the pipeline's current BDPT buffers.
+// buffer sets of `paths` paths.  The lists' queue path arrays are the
+// pipeline's current BDPT buffers.
 int ensure_late(Pipe& p, int paths, int recs) {
-  if (!p.side) {
-    HIPCHK(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
-    for (int k = 0; k < 2; ++k) {
-      HIPCHK(hipEventCreateWithFlags(&p.ev_res[k], ev_flags(hipEventDisableTiming)));
-      HIPCHK(hipEventCreateWithFlags(&p.ev_vtx[k], ev_flags(hipEventDisableTiming)));
-      HIPCHK(hipEventCreateWithFlags(&p.ev_late[k], ev_flags(hipEventDisableTiming)));
-    }
-  }
   if (p.late_recs < static_cast<size_t>(recs) || p.late_paths < static_cast<size_t>(paths)) {
     recs = std::max<int>(recs, static_cast<int>(p.late_recs));
     paths = std::max<int>(paths, static_cast<int>(p.late_paths));
@@ -954,9 +944,13 @@ int ensure_late(Pipe& p, int paths, int recs) {
 
 // One persistent traversal launch over the queues of Q (max_rays bounds the
 // grid).  WR_TRACE_BVH: the verified-BVH search + its resolve launch instead.
+// Blocks of a fused search launch that settle the previous step's late lists:
+// per group member kLateTieBlocks tie waves (one tie per wave up to that many,
+// else one per lane on kLateLaneBlocks) and kLateScanBlocks scan waves
+constexpr int kLateTieBlocks = 256, kLateLaneBlocks = 64, kLateScanBlocks = 64;
 int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const TraceSlot& ts, Timer& tm, bool count,
                  const TraceQueues& Q_, int max_rays, int mode = TRACE_PLAIN, bool hard_wave = false,
-                 hipEvent_t after_resolve = nullptr) {
+                 const LateArgs* late_prev = nullptr, int late_gn = 0) {
   int* fetch = ts.fetch;
   TraceQueues Q = Q_;
   if (c->no_cut)  // measurement knob: the same launches without the dead-work elision
@@ -973,14 +967,26 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
       (void)hipEventCreate(&fb);
       (void)hipEventRecord(f0, stream);
     }
-    hipLaunchKernelGGL(count ? k_trace_fast<true> : k_trace_fast<false>, dim3(fgrid), dim3(kTraceBlock), slds, stream,
-                       c->ds, c->fs, Q, ctr, fetch, ts.t2, ts.spill);
+    if (late_prev) {  // + the previous step's deferred hard rays, beside the search
+      const int lblocks = late_gn * (kLateTieBlocks + kLateScanBlocks);
+      auto kf = count ? k_trace_fast<true, true> : k_trace_fast<false, true>;
+      hipLaunchKernelGGL(kf, dim3(lblocks + fgrid),
+                         dim3(kTraceBlock), std::max(slds, lds), stream, c->ds, c->fs, Q, ctr, fetch, ts.t2, ts.spill,
+                         *late_prev, lblocks, late_gn, kLateTieBlocks, kLateLaneBlocks, kLateTieBlocks);
+      if (c->verify)
+        hipLaunchKernelGGL(k_late_verify, dim3(64, late_gn), dim3(kTraceBlock), lds, stream, c->ds, c->fs, *late_prev,
+                           ctr);
+    } else {
+      auto kf = count ? k_trace_fast<true, false> : k_trace_fast<false, false>;
+      hipLaunchKernelGGL(kf, dim3(fgrid),
+                         dim3(kTraceBlock), slds, stream, c->ds, c->fs, Q, ctr, fetch, ts.t2, ts.spill, LateArgs{}, 0,
+                         1, 0, 0, 0);
+    }
     if (c->trace_log) (void)hipEventRecord(fa, stream);
     int* hard = reinterpret_cast<int*>(ts.t2 + ts.t2_cap);
     hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
                        dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), 0, stream, c->ds, c->fs,
                        Q, ctr, ts.t2, hard, ts.hard_n, static_cast<int>(ts.t2_cap));
-    if (after_resolve) (void)hipEventRecord(after_resolve, stream);  // the late lists are complete
     if (c->trace_log) (void)hipEventRecord(fb, stream);
     // the hard rays are a few in 10^4: a small grid drains any count (one
     // ray per wave for the API calls: up to 2048 at once, 8 waves per CU)
@@ -1710,7 +1716,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       fs.depth = std::max(fh.depth + 1, d.max_stack + 1);
       c->fast_ok = true;
       int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_fast<false>, kTraceBlock,
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_fast<false, false>, kTraceBlock,
                                                        search_lds_bytes(fs.sdepth)) != hipSuccess ||
           per_cu <= 0)
         per_cu = 8;
@@ -1758,11 +1764,6 @@ void wr_destroy(wr_context* c) {
     if (p.stream) (void)hipStreamSynchronize(p.stream);
     for (hipEvent_t e : p.events) (void)hipEventDestroy(e);
     if (p.done) (void)hipEventDestroy(p.done);
-    if (p.side) (void)hipStreamSynchronize(p.side);
-    for (int k = 0; k < 2; ++k)
-      for (hipEvent_t e : {p.ev_res[k], p.ev_vtx[k], p.ev_late[k]})
-        if (e) (void)hipEventDestroy(e);
-    if (p.side) (void)hipStreamDestroy(p.side);
     p.late_mem.release();
     if (p.ctr) (void)hipFree(p.ctr);
     if (p.sc) (void)hipFree(p.sc);
@@ -2013,13 +2014,14 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   }
   // Deferred hard rays: in BVH mode the extension rays a step's resolve cannot
   // settle (near-ties, membership scans: 0.1-0.5 % of them) go to a late list
-  // instead of the step's k_fast_hard; the pipeline's side stream settles them
-  // (k_late_hard) and shades their paths one step later (k_late_vertex), while
-  // the pipeline shades every other path and traces on.  Step s's late work
-  // writes step s + 2's queues, so the pipeline waits for it only before that
-  // step's traversal.  A path is deferred once per pass, and each pass gets
-  // one step more (the light pass a bounce step, the camera pass extension
-  // rays at its last step): a deferred path's vertices come one step late.
+  // instead of the step's k_fast_hard, so the step's vertex launch follows its
+  // resolve without waiting for them.  The next step's search launch settles
+  // them in extra blocks beside its search (late_hard), and its vertex launch
+  // shades their paths in extra blocks, into the same queues as its own
+  // vertices: a deferred path is one step behind, and the hard rays' latency
+  // hides under the next search instead of lengthening the chain.  A path is
+  // deferred once per pass, and each pass gets one step more (the light pass a
+  // bounce step, the camera pass extension rays at its last step).
   const bool defer = c->fast_on && !c->stamps && defer_enabled(c, np);
   if (defer)
     for (int i = 0; i < fit; ++i)
@@ -2071,38 +2073,19 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
       return rq(B.q_o[q], B.q_d[q], B.P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q], nullptr, nullptr, nullptr,
                 pp.late_d + 2 * m + q, pp.sc[m].late[slot], bit);
     };
-    // before step `slot`'s traversal: the late work of step slot - 2 wrote its queues
-    auto wait_late = [&](int slot) -> int {
-      if (slot >= 2 && G.late[slot - 2]) HIPCHK(hipStreamWaitEvent(sm, pp.ev_late[slot & 1], 0));
-      return WR_OK;
-    };
-    // after step `slot`'s vertex launch: its late lists, on the side stream
-    auto issue_late = [&](int slot, bool camera, int g) -> int {
-      const int k = slot & 1;
-      LateArgs L;
+    // the late lists of step slot - 1 (when it deferred): settled by extra
+    // blocks of step slot's search launch, shaded by extra blocks of its vertex
+    // launch, into the queues of step slot + 1
+    auto late_of = [&](int slot, LateArgs& L) -> bool {
+      if (slot < 1 || !G.late[slot - 1]) return false;
+      const int k = (slot - 1) & 1;
       for (int m = 0; m < kGroup; ++m) {
         L.l[m] = pp.late_h[m][k];
-        L.n[m] = pp.sc[m].late[slot];
+        L.n[m] = pp.sc[m].late[slot - 1];
       }
-      HIPCHK(hipEventRecord(pp.ev_vtx[k], sm));
-      HIPCHK(hipStreamWaitEvent(pp.side, pp.ev_res[k], 0));
-      const int hblocks = std::max(64, c->tie_wave_max);
-      hipLaunchKernelGGL(count ? k_late_hard<true> : k_late_hard<false>, dim3(hblocks + WR_SCAN_WAVES, gn),
-                         dim3(kTraceBlock), fast_lds_bytes(c->fs.depth), pp.side, c->ds, c->fs, L, pp.ctr, hblocks, 64,
-                         c->tie_wave_max);
-      if (c->verify)
-        hipLaunchKernelGGL(k_late_verify, dim3(64, gn), dim3(kTraceBlock), fast_lds_bytes(c->fs.depth), pp.side, c->ds,
-                           c->fs, L, pp.ctr);
-      HIPCHK(hipStreamWaitEvent(pp.side, pp.ev_vtx[k], 0));
-      const int lg = std::max(1, std::min(g, 64));
-      if (camera)
-        hipLaunchKernelGGL(k_late_vertex<true>, dim3(lg, gn), dim3(kShadeBlock), 0, pp.side, G.GA, L, slot);
-      else
-        hipLaunchKernelGGL(k_late_vertex<false>, dim3(lg, gn), dim3(kShadeBlock), 0, pp.side, G.GA, L, slot);
-      HIPCHK(hipEventRecord(pp.ev_late[k], pp.side));
-      G.late[slot] = true;
-      return WR_OK;
+      return true;
     };
+    const int lg = std::max(1, std::min(shade_grid(c, G.nmax), 32));  // late-vertex blocks per member
     const int sq_max = G.nmax * (kVMax + 2);  // <= cap_sq
     const int g = shade_grid(c, G.nmax);
     if (step == 0) {
@@ -2114,28 +2097,23 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
       tm.mark(WR_K_GEN);
     } else if (step <= lb_n) {
       const int b = step - 1;
-      // deferrable up to the last regular bounce (a deferred path's next ray,
-      // queue b + 2, is traced by the extra step b = maxlen - 1)
+      // deferrable up to the last regular bounce (a deferred path's next ray is
+      // traced one step late: the extra step b = maxlen - 1 traces the last ones)
       const int bit = (defer && b <= maxlen - 2) ? 1 : 0;
-      if (int rc = wait_late(b)) return rc;
+      LateArgs L{};
+      const bool lp = late_of(b, L);
       QueueList ql;
       for (int m = 0; m < gn; ++m) ql.add(ext(m, b, bit), A[m].n);
       trace_launch(c, sm, pp.ctr, tslot(pp, b), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE, false,
-                   bit ? pp.ev_res[b & 1] : nullptr);
-      hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA, b);
+                   lp ? &L : nullptr, gn);
+      hipLaunchKernelGGL(k_light_shade, dim3(g + (lp ? lg : 0), gn), dim3(kShadeBlock), 0, sm, G.GA, b, L,
+                         lp ? lg : 0);
       tm.mark(WR_K_SHADE);
-      if (bit)
-        if (int rc = issue_late(b, false, g)) return rc;
+      G.late[b] = bit != 0;
     } else if (step == lb_n + 1) {
       // ---------------- camera pass (:133-264).  The light pass's splat rays
       // (connectToCamera) ride along with the primary rays; afterwards each
-      // bounce's shadow / aux rays ride along with the next bounce's extension
-      // rays.  Every light vertex and splat, deferred ones too, comes first.
-      for (int b = lb_n - 1; b >= 0; --b)
-        if (G.late[b]) {
-          HIPCHK(hipStreamWaitEvent(sm, pp.ev_late[b & 1], 0));
-          break;
-        }
+      // bounce's shadow / aux rays ride along with the next bounce's extension rays.
       hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA);
       tm.mark(WR_K_GEN);
     } else {
@@ -2143,26 +2121,21 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
       const int slot = kCamSlot + b;
       const bool more = b < maxlen + (defer ? 1 : 0);  // extension rays of bounce b exist
       const int bit = (defer && b <= maxlen - 1) ? 2 : 0;
-      if (int rc = wait_late(slot)) return rc;
+      LateArgs L{};
+      const bool lp = late_of(slot, L);
       QueueList ql;
       for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), A[m].n * (kVMax + 2));
       if (more)
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot, bit), A[m].n);
       trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE, false,
-                   bit ? pp.ev_res[slot & 1] : nullptr);
-      // resolve this step's shadow / aux rays and shade its vertices in one launch
+                   lp ? &L : nullptr, gn);
+      // resolve this step's shadow / aux rays and shade its vertices (and the
+      // previous step's deferred ones) in one launch
       const int nres = shade_grid(c, sq_max);
-      hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, G.GA, slot, nres,
-                         more ? 1 : 0);
+      hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0) + (lp ? lg : 0), gn), dim3(kShadeBlock), 0, sm,
+                         G.GA, slot, nres, more ? 1 : 0, L, lp ? lg : 0);
       tm.mark(WR_K_SHADE);
-      if (bit)
-        if (int rc = issue_late(slot, true, g)) return rc;
-      if (b == maxlen)  // the group's last step: join the side stream's remaining work
-        for (int s2 = slot; s2 >= kCamSlot; --s2)
-          if (G.late[s2]) {
-            HIPCHK(hipStreamWaitEvent(sm, pp.ev_late[s2 & 1], 0));
-            break;
-          }
+      G.late[slot] = bit != 0;
     }
     return WR_OK;
   };
