@@ -153,91 +153,89 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
   V3 e_o, e_d, s_o, s_d, s_val;
   int s_pix = -1;
   if (prim >= 0) {
-    {
-      const Hit h = rebuild_hit(S, prim, t, o, d);
-      Bsdf b;
-      bsdf_init(b, -d, h.n, h.mat, S.mats);
-      if (b.mat != 0) {
-        float dvcm = B.l_dvcm[p], dvc = B.l_dvc[p];
-        int len = B.l_len[p], nspec = B.l_nspec[p];
-        V3 thr = ld3(B.l_thr, P, p);
-        dvcm *= (t * t);  // pathLength > 1 || isFiniteLight: always for area lights (:94-97)
-        dvcm /= fabsf(b.wi.z);
-        dvc /= fabsf(b.wi.z);
-        if (!b.delta) {  // lightStates.push_back (:101-102)
-          const int k = B.v_count[p];
-          const int slot = k * P + p;
-          st3(B.v_pos, kVMax * P, slot, h.p);
-          st3(B.v_n, kVMax * P, slot, h.n);
-          st3(B.v_wi, kVMax * P, slot, b.wi);
-          st3(B.v_thr, kVMax * P, slot, thr);
-          B.v_dvcm[slot] = dvcm;
-          B.v_dvc[slot] = dvc;
-          B.v_cont[slot] = b.cont;
-          B.v_pd[slot] = b.pd;
-          B.v_pg[slot] = b.pg;
-          B.v_len[slot] = len;
-          B.v_nspec[slot] = nspec;
-          B.v_mat[slot] = b.mat;
-          B.v_count[p] = k + 1;
-          if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
-            const DCam& cam = S.cam;
-            const V3 ip = t_point(cam.w2r, h.p);
-            if (check_raster(cam, ip.x, ip.y)) {
-              V3 dtc = cam.pos - h.p;
-              if (dot(-dtc, cam.fwd) > 0) {
-                const float d2 = sqr_len(dtc);
-                const float dist = sqrtf(d2);
-                dtc = div_guarded(dtc, dist);
-                float cos_to = 0.f, dp, rp;
-                const V3 f = bsdf_f(b, S.mats, dtc, &cos_to, &dp, &rp);
-                if (!black(f)) {
-                  rp *= b.cont;
-                  const float cos_at = dot(-dtc, cam.fwd);
-                  const float ipd = cam.plane_dist / cos_at;
-                  const float i2sa = (ipd * ipd) / cos_at;
-                  const float i2s = i2sa * fabsf(cos_to) / d2;
-                  const float pdf_a = i2s;
-                  const float s2i = 1.f / i2s;
-                  const V3 res = div_plain(mul(thr, f), static_cast<float>(A.P) * s2i);
+    const Hit h = rebuild_hit(S, prim, t, o, d);
+    Bsdf b;
+    bsdf_init(b, -d, h.n, h.mat, S.mats);
+    if (b.mat != 0) {
+      float dvcm = B.l_dvcm[p], dvc = B.l_dvc[p];
+      int len = B.l_len[p], nspec = B.l_nspec[p];
+      V3 thr = ld3(B.l_thr, P, p);
+      dvcm *= (t * t);  // pathLength > 1 || isFiniteLight: always for area lights (:94-97)
+      dvcm /= fabsf(b.wi.z);
+      dvc /= fabsf(b.wi.z);
+      if (!b.delta) {  // lightStates.push_back (:101-102)
+        const int k = B.v_count[p];
+        const int slot = k * P + p;
+        st3(B.v_pos, kVMax * P, slot, h.p);
+        st3(B.v_n, kVMax * P, slot, h.n);
+        st3(B.v_wi, kVMax * P, slot, b.wi);
+        st3(B.v_thr, kVMax * P, slot, thr);
+        B.v_dvcm[slot] = dvcm;
+        B.v_dvc[slot] = dvc;
+        B.v_cont[slot] = b.cont;
+        B.v_pd[slot] = b.pd;
+        B.v_pg[slot] = b.pg;
+        B.v_len[slot] = len;
+        B.v_nspec[slot] = nspec;
+        B.v_mat[slot] = b.mat;
+        B.v_count[p] = k + 1;
+        if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
+          const DCam& cam = S.cam;
+          const V3 ip = t_point(cam.w2r, h.p);
+          if (check_raster(cam, ip.x, ip.y)) {
+            V3 dtc = cam.pos - h.p;
+            if (dot(-dtc, cam.fwd) > 0) {
+              const float d2 = sqr_len(dtc);
+              const float dist = sqrtf(d2);
+              dtc = div_guarded(dtc, dist);
+              float cos_to = 0.f, dp, rp;
+              const V3 f = bsdf_f(b, S.mats, dtc, &cos_to, &dp, &rp);
+              if (!black(f)) {
+                rp *= b.cont;
+                const float cos_at = dot(-dtc, cam.fwd);
+                const float ipd = cam.plane_dist / cos_at;
+                const float i2sa = (ipd * ipd) / cos_at;
+                const float i2s = i2sa * fabsf(cos_to) / d2;
+                const float pdf_a = i2s;
+                const float s2i = 1.f / i2s;
+                const V3 res = div_plain(mul(thr, f), static_cast<float>(A.P) * s2i);
 #ifdef WR_DEBUG_PATH
-                  if (A.base + p == WR_DEBUG_PATH && A.iter == WR_DEBUG_ITER)
-                    printf("[dbg gpu] len %d hit %a %a %a t %a prim %d thr %a %a %a f %a %a %a cos_to %a d2 %a i2s %a res %a %a %a black %d rp %a dvcm %a dvc %a\n",
-                           len, h.p.x, h.p.y, h.p.z, t, prim, thr.x, thr.y, thr.z, f.x, f.y, f.z, cos_to, d2, i2s,
-                           res.x, res.y, res.z, (int)black(res), rp, dvcm, dvc);
+                if (A.base + p == WR_DEBUG_PATH && A.iter == WR_DEBUG_ITER)
+                  printf("[dbg gpu] len %d hit %a %a %a t %a prim %d thr %a %a %a f %a %a %a cos_to %a d2 %a i2s %a res %a %a %a black %d rp %a dvcm %a dvc %a\n",
+                         len, h.p.x, h.p.y, h.p.z, t, prim, thr.x, thr.y, thr.z, f.x, f.y, f.z, cos_to, d2, i2s,
+                         res.x, res.y, res.z, (int)black(res), rp, dvcm, dvc);
 #endif
-                  if (!black(res)) {
-                    const float wl = (pdf_a / static_cast<float>(A.P)) * (dvcm + rp * dvc);
-                    const float w = WR_TEST_SPLAT_W / (wl + 1.f);
-                    splat = true;
-                    s_o = h.p;
-                    s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
-                    s_val = res * w;
-                    s_pix = pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W);
-                  }
+                if (!black(res)) {
+                  const float wl = (pdf_a / static_cast<float>(A.P)) * (dvcm + rp * dvc);
+                  const float w = WR_TEST_SPLAT_W / (wl + 1.f);
+                  splat = true;
+                  s_o = h.p;
+                  s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
+                  s_val = res * w;
+                  s_pix = pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W);
                 }
               }
             }
           }
         }
-        if (!(len + 2 > A.maxlen)) {  // (:123-127)
-          Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), B.l_ctr[p]};
-          V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
-          if (sample_scatter(S, rng, b, h.p, lo, ld, thr, dvcm, dvc, nspec)) {
-            ext = true;
-            ++len;
-            e_o = lo + ld * WR_EPS;
-            e_d = normalize(ld);
-            st3(B.l_o, P, p, lo);
-            st3(B.l_d, P, p, ld);
-            st3(B.l_thr, P, p, thr);
-            B.l_dvcm[p] = dvcm;
-            B.l_dvc[p] = dvc;
-            B.l_len[p] = len;
-            B.l_nspec[p] = nspec;
-          }
-          B.l_ctr[p] = rng.ctr;
+      }
+      if (!(len + 2 > A.maxlen)) {  // (:123-127)
+        Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), B.l_ctr[p]};
+        V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
+        if (sample_scatter(S, rng, b, h.p, lo, ld, thr, dvcm, dvc, nspec)) {
+          ext = true;
+          ++len;
+          e_o = lo + ld * WR_EPS;
+          e_d = normalize(ld);
+          st3(B.l_o, P, p, lo);
+          st3(B.l_d, P, p, ld);
+          st3(B.l_thr, P, p, thr);
+          B.l_dvcm[p] = dvcm;
+          B.l_dvc[p] = dvc;
+          B.l_len[p] = len;
+          B.l_nspec[p] = nspec;
         }
+        B.l_ctr[p] = rng.ctr;
       }
     }
   }
