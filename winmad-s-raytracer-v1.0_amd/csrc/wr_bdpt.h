@@ -6,19 +6,39 @@
 #pragma once
 
 // =============================================================== BDPT state
+// Light / camera subpath state (bidirPathTracing.h:7-18), one 64-byte record
+// per path: the vertex kernels gather it by path index (the queue's order), so
+// a lane's state is one cache line instead of 15 words in 15 arrays.
+enum : int {
+  PS_O = 0, PS_D = 3, PS_THR = 6, PS_DVCM = 9, PS_DVC = 10, PS_LEN = 11, PS_NSPEC = 12, PS_CTR = 13,
+  PS_VCOUNT = 14,  // light paths: stored light vertices
+  PS_PIX = 14,     // camera paths: film pixel
+  PS_WORDS = 16
+};
+__device__ __forceinline__ float& psf(float* s, int p, int k) { return s[size_t(p) * PS_WORDS + k]; }
+__device__ __forceinline__ int& psi(float* s, int p, int k) {
+  return reinterpret_cast<int*>(s)[size_t(p) * PS_WORDS + k];
+}
+__device__ __forceinline__ uint32_t& psu(float* s, int p, int k) {
+  return reinterpret_cast<uint32_t*>(s)[size_t(p) * PS_WORDS + k];
+}
+__device__ __forceinline__ V3 ld3r(const float* s, int p, int k) {
+  const float* r = s + size_t(p) * PS_WORDS + k;
+  return v3(r[0], r[1], r[2]);
+}
+__device__ __forceinline__ void st3r(float* s, int p, int k, V3 v) {
+  float* r = s + size_t(p) * PS_WORDS + k;
+  r[0] = v.x;
+  r[1] = v.y;
+  r[2] = v.z;
+}
+
 struct BdptBuf {
   int P = 0, cap_sq = 0;
-  // light subpath state (bidirPathTracing.h:7-18)
-  float *l_o, *l_d, *l_thr, *l_dvcm, *l_dvc;
-  int *l_len, *l_nspec;
-  uint32_t* l_ctr;
+  float *ls, *cs;  // light / camera subpath state, PS_WORDS floats per path
   // stored light vertices [kVMax][...][P]
   float *v_pos, *v_n, *v_wi, *v_thr, *v_dvcm, *v_dvc, *v_cont, *v_pd, *v_pg;
-  int *v_len, *v_nspec, *v_mat, *v_count;
-  // camera subpath state
-  float *c_o, *c_d, *c_thr, *c_dvcm, *c_dvc;
-  int *c_len, *c_nspec, *c_pix;
-  uint32_t* c_ctr;
+  int *v_len, *v_nspec, *v_mat;
   // extension-ray queues (double buffered)
   float *q_o[2], *q_d[2], *q_t[2];
   int *q_path[2], *q_prim[2];
@@ -96,15 +116,15 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_light_gen(BdptGro
     epdf *= lpp;
     dpdf *= lpp;
     thr = div_plain(thr, epdf);
-    st3(B.l_o, P, p, pos);
-    st3(B.l_d, P, p, dir);
-    st3(B.l_thr, P, p, thr);
-    B.l_dvcm[p] = dpdf / epdf;
-    B.l_dvc[p] = 1.f / epdf;  // AreaLight::isDelta() == 0
-    B.l_len[p] = 1;
-    B.l_nspec[p] = 0;
-    B.l_ctr[p] = rng.ctr;
-    B.v_count[p] = 0;
+    st3r(B.ls, p, PS_O, pos);
+    st3r(B.ls, p, PS_D, dir);
+    st3r(B.ls, p, PS_THR, thr);
+    psf(B.ls, p, PS_DVCM) = dpdf / epdf;
+    psf(B.ls, p, PS_DVC) = 1.f / epdf;  // AreaLight::isDelta() == 0
+    psi(B.ls, p, PS_LEN) = 1;
+    psi(B.ls, p, PS_NSPEC) = 0;
+    psu(B.ls, p, PS_CTR) = rng.ctr;
+    psi(B.ls, p, PS_VCOUNT) = 0;
     // Ray(origin + dir * EPS, dir) (:79-80)
     st3(B.q_o[0], P, p, pos + dir * WR_EPS);
     st3(B.q_d[0], P, p, normalize(dir));
@@ -157,14 +177,14 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
     Bsdf b;
     bsdf_init(b, -d, h.n, h.mat, S.mats);
     if (b.mat != 0) {
-      float dvcm = B.l_dvcm[p], dvc = B.l_dvc[p];
-      int len = B.l_len[p], nspec = B.l_nspec[p];
-      V3 thr = ld3(B.l_thr, P, p);
+      float dvcm = psf(B.ls, p, PS_DVCM), dvc = psf(B.ls, p, PS_DVC);
+      int len = psi(B.ls, p, PS_LEN), nspec = psi(B.ls, p, PS_NSPEC);
+      V3 thr = ld3r(B.ls, p, PS_THR);
       dvcm *= (t * t);  // pathLength > 1 || isFiniteLight: always for area lights (:94-97)
       dvcm /= fabsf(b.wi.z);
       dvc /= fabsf(b.wi.z);
       if (!b.delta) {  // lightStates.push_back (:101-102)
-        const int k = B.v_count[p];
+        const int k = psi(B.ls, p, PS_VCOUNT);
         const int slot = k * P + p;
         st3(B.v_pos, kVMax * P, slot, h.p);
         st3(B.v_n, kVMax * P, slot, h.n);
@@ -178,7 +198,7 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
         B.v_len[slot] = len;
         B.v_nspec[slot] = nspec;
         B.v_mat[slot] = b.mat;
-        B.v_count[p] = k + 1;
+        psi(B.ls, p, PS_VCOUNT) = k + 1;
         if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
           const DCam& cam = S.cam;
           const V3 ip = t_point(cam.w2r, h.p);
@@ -220,22 +240,22 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
         }
       }
       if (!(len + 2 > A.maxlen)) {  // (:123-127)
-        Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), B.l_ctr[p]};
-        V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
+        Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), psu(B.ls, p, PS_CTR)};
+        V3 lo = ld3r(B.ls, p, PS_O), ld = ld3r(B.ls, p, PS_D);
         if (sample_scatter(S, rng, b, h.p, lo, ld, thr, dvcm, dvc, nspec)) {
           ext = true;
           ++len;
           e_o = lo + ld * WR_EPS;
           e_d = normalize(ld);
-          st3(B.l_o, P, p, lo);
-          st3(B.l_d, P, p, ld);
-          st3(B.l_thr, P, p, thr);
-          B.l_dvcm[p] = dvcm;
-          B.l_dvc[p] = dvc;
-          B.l_len[p] = len;
-          B.l_nspec[p] = nspec;
+          st3r(B.ls, p, PS_O, lo);
+          st3r(B.ls, p, PS_D, ld);
+          st3r(B.ls, p, PS_THR, thr);
+          psf(B.ls, p, PS_DVCM) = dvcm;
+          psf(B.ls, p, PS_DVC) = dvc;
+          psi(B.ls, p, PS_LEN) = len;
+          psi(B.ls, p, PS_NSPEC) = nspec;
         }
-        B.l_ctr[p] = rng.ctr;
+        psu(B.ls, p, PS_CTR) = rng.ctr;
       }
     }
   }
@@ -331,15 +351,15 @@ __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
   const float cos_at = dot(cam.fwd, d);
   const float ipd = cam.plane_dist / cos_at;
   const float i2sa = (ipd * ipd) / cos_at;
-  st3(B.c_o, P, l, cam.pos);
-  st3(B.c_d, P, l, d);
-  st3(B.c_thr, P, l, v3(1.f, 1.f, 1.f));
-  B.c_dvcm[l] = static_cast<float>(A.P) / i2sa;  // lightPathNum / cameraPdf
-  B.c_dvc[l] = 0.f;
-  B.c_len[l] = 1;
-  B.c_nspec[l] = 0;
-  B.c_ctr[l] = rng.ctr;
-  B.c_pix[l] = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
+  st3r(B.cs, l, PS_O, cam.pos);
+  st3r(B.cs, l, PS_D, d);
+  st3r(B.cs, l, PS_THR, v3(1.f, 1.f, 1.f));
+  psf(B.cs, l, PS_DVCM) = static_cast<float>(A.P) / i2sa;  // lightPathNum / cameraPdf
+  psf(B.cs, l, PS_DVC) = 0.f;
+  psi(B.cs, l, PS_LEN) = 1;
+  psi(B.cs, l, PS_NSPEC) = 0;
+  psu(B.cs, l, PS_CTR) = rng.ctr;
+  psi(B.cs, l, PS_PIX) = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
   st3(B.q_o[0], P, s, cam.pos + d * WR_EPS);
   st3(B.q_d[0], P, s, normalize(d));
   B.q_path[0][s] = l;
@@ -375,12 +395,12 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
     bsdf_init(b, -d, h.n, h.mat, S.mats);
     if (b.mat != 0) {
       hp = h.p;
-      pix = B.c_pix[p];
-      dvcm = B.c_dvcm[p];
-      dvc = B.c_dvc[p];
-      len = B.c_len[p];
-      nspec = B.c_nspec[p];
-      thr = ld3(B.c_thr, P, p);
+      pix = psi(B.cs, p, PS_PIX);
+      dvcm = psf(B.cs, p, PS_DVCM);
+      dvc = psf(B.cs, p, PS_DVC);
+      len = psi(B.cs, p, PS_LEN);
+      nspec = psi(B.cs, p, PS_NSPEC);
+      thr = ld3r(B.cs, p, PS_THR);
       dvcm *= (t * t);  // (:180-182)
       dvcm /= fabsf(b.wi.z);
       dvc /= fabsf(b.wi.z);
@@ -407,7 +427,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
         }
       } else if (len < A.maxlen) {
         live = true;
-        Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(A.base + p)), B.c_ctr[p]};
+        Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(A.base + p)), psu(B.cs, p, PS_CTR)};
         if (!b.delta && len_ok(A.ctl, len + 1)) {  // getDirectIllumination (:205-217, :484-608)
           const float wlen = 1.f / (static_cast<float>(len) + 1.f - static_cast<float>(nspec));
           const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
@@ -478,19 +498,19 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
         }
         if (!b.delta) {
           conn_phase = true;
-          nv = B.v_count[p];
+          nv = psi(B.ls, p, PS_VCOUNT);
         }
-        V3 so = ld3(B.c_o, P, p), sd = ld3(B.c_d, P, p);
+        V3 so = ld3r(B.cs, p, PS_O), sd = ld3r(B.cs, p, PS_D);
         if (sample_scatter(S, rng, b, hp, so, sd, thr, dvcm, dvc, nspec)) {
           ext = true;
           e_o = so + sd * WR_EPS;
           e_d = normalize(sd);
         }
-        B.c_ctr[p] = rng.ctr;
+        psu(B.cs, p, PS_CTR) = rng.ctr;
         // state for the NEXT vertex; the connections below use the values of
         // THIS vertex, so keep them (thr/dvcm/dvc/nspec are re-read below)
-        st3(B.c_o, P, p, so);
-        st3(B.c_d, P, p, sd);
+        st3r(B.cs, p, PS_O, so);
+        st3r(B.cs, p, PS_D, sd);
       }
     }
   }
@@ -589,11 +609,11 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
   }
   if (live) {  // commit scattered state (:259-260) and the loop increment
     if (ext) {
-      st3(B.c_thr, P, p, thr);
-      B.c_dvcm[p] = dvcm;
-      B.c_dvc[p] = dvc;
-      B.c_nspec[p] = nspec;
-      B.c_len[p] = len + 1;
+      st3r(B.cs, p, PS_THR, thr);
+      psf(B.cs, p, PS_DVCM) = dvcm;
+      psf(B.cs, p, PS_DVC) = dvc;
+      psi(B.cs, p, PS_NSPEC) = nspec;
+      psi(B.cs, p, PS_LEN) = len + 1;
     }
   }
   const int ei = wave_append(&A.sc->ext[oslot], ext);

@@ -588,14 +588,8 @@ void layout_bdpt(Arena& a, BdptBuf& B, int P) {
   B.P = P;
   B.cap_sq = P * (kVMax + 2);  // per camera vertex: <= kVMax connections + NEE + DI-BSDF
   const size_t sP = P, sV = size_t(kVMax) * P, sQ = B.cap_sq;
-  B.l_o = a.take<float>(3 * sP);
-  B.l_d = a.take<float>(3 * sP);
-  B.l_thr = a.take<float>(3 * sP);
-  B.l_dvcm = a.take<float>(sP);
-  B.l_dvc = a.take<float>(sP);
-  B.l_len = a.take<int>(sP);
-  B.l_nspec = a.take<int>(sP);
-  B.l_ctr = a.take<uint32_t>(sP);
+  B.ls = a.take<float>(PS_WORDS * sP);
+  B.cs = a.take<float>(PS_WORDS * sP);
   B.v_pos = a.take<float>(3 * sV);
   B.v_n = a.take<float>(3 * sV);
   B.v_wi = a.take<float>(3 * sV);
@@ -608,16 +602,7 @@ void layout_bdpt(Arena& a, BdptBuf& B, int P) {
   B.v_len = a.take<int>(sV);
   B.v_nspec = a.take<int>(sV);
   B.v_mat = a.take<int>(sV);
-  B.v_count = a.take<int>(sP);
-  B.c_o = a.take<float>(3 * sP);
-  B.c_d = a.take<float>(3 * sP);
-  B.c_thr = a.take<float>(3 * sP);
-  B.c_dvcm = a.take<float>(sP);
-  B.c_dvc = a.take<float>(sP);
-  B.c_len = a.take<int>(sP);
-  B.c_nspec = a.take<int>(sP);
-  B.c_pix = a.take<int>(sP);
-  B.c_ctr = a.take<uint32_t>(sP);
+
   for (int q = 0; q < 2; ++q) {
     B.q_o[q] = a.take<float>(3 * sP);
     B.q_d[q] = a.take<float>(3 * sP);

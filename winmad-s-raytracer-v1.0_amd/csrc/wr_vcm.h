@@ -102,15 +102,15 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_vcm_light_gen(Vcm
     dpdf *= lpp;
     thr = div_plain(thr, epdf);
     const float dvc = cal / epdf;  // AreaLight: finite, not delta -> cosAtLight
-    st3(B.l_o, P, p, pos);
-    st3(B.l_d, P, p, dir);
-    st3(B.l_thr, P, p, thr);
-    B.l_dvcm[p] = dpdf / epdf;
-    B.l_dvc[p] = dvc;
+    st3r(B.ls, p, PS_O, pos);
+    st3r(B.ls, p, PS_D, dir);
+    st3r(B.ls, p, PS_THR, thr);
+    psf(B.ls, p, PS_DVCM) = dpdf / epdf;
+    psf(B.ls, p, PS_DVC) = dvc;
     V.l_dvm[p] = dvc * X.mis_vc;
-    B.l_len[p] = 1;
-    B.l_ctr[p] = rng.ctr;
-    B.v_count[p] = 0;
+    psi(B.ls, p, PS_LEN) = 1;
+    psu(B.ls, p, PS_CTR) = rng.ctr;
+    psi(B.ls, p, PS_VCOUNT) = 0;
     V.l_shas[p] = 0;
     st3(B.q_o[0], P, p, pos + dir * WR_EPS);  // Ray(origin + dir * EPS, dir) (:79-80)
     st3(B.q_d[0], P, p, normalize(dir));
@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
         Bsdf b;
         bsdf_init(b, -d, h.n, h.mat, S.mats);
         if (b.mat != 0) {
-          int len = B.l_len[p];
+          int len = psi(B.ls, p, PS_LEN);
           if (b.mat < 0) {
             if (len > 1) {
               b.pd = V.l_spd[p];
@@ -200,8 +200,8 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
             V.l_scont[p] = b.cont;
             V.l_shas[p] = 1;
           }
-          float dvcm = B.l_dvcm[p], dvc = B.l_dvc[p], dvm = V.l_dvm[p];
-          V3 thr = ld3(B.l_thr, P, p);
+          float dvcm = psf(B.ls, p, PS_DVCM), dvc = psf(B.ls, p, PS_DVC), dvm = V.l_dvm[p];
+          V3 thr = ld3r(B.ls, p, PS_THR);
           // `pathLength > 1 || isFiniteLight == 1` (:94-95): isFiniteLight is a
           // signed 1-bit field (vertexcm.h:31) that reads back -1, so only the
           // path length counts -- unlike BDPT
@@ -210,7 +210,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
           dvc /= fabsf(b.wi.z);
           dvm /= fabsf(b.wi.z);
           if (!b.delta) {  // lightVertices.push_back (:98-113)
-            const int k = B.v_count[p];
+            const int k = psi(B.ls, p, PS_VCOUNT);
             const int vs = k * P + p;
             st3(B.v_pos, kVMax * P, vs, h.p);
             st3(B.v_n, kVMax * P, vs, h.n);
@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
             B.v_pg[vs] = b.pg;
             B.v_len[vs] = len;
             B.v_mat[vs] = b.mat;
-            B.v_count[p] = k + 1;
+            psi(B.ls, p, PS_VCOUNT) = k + 1;
             if (b.mat > 0 && len + 1 >= X.minlen) {  // connectToCamera (:116-127, :332-384)
               const DCam& cam = S.cam;
               const V3 ip = t_point(cam.w2r, h.p);
@@ -259,22 +259,22 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
             }
           }
           if (b.mat > 0 && !(len + 2 > A.maxlen)) {  // (:129-133); an emitter's sample is black
-            Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), B.l_ctr[p]};
-            V3 lo = ld3(B.l_o, P, p), ld = ld3(B.l_d, P, p);
+            Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(p)), psu(B.ls, p, PS_CTR)};
+            V3 lo = ld3r(B.ls, p, PS_O), ld = ld3r(B.ls, p, PS_D);
             if (vcm_scatter(X, rng, b, h.p, lo, ld, thr, dvcm, dvc, dvm)) {
               ext = true;
               ++len;
               e_o = lo + ld * WR_EPS;
               e_d = normalize(ld);
-              st3(B.l_o, P, p, lo);
-              st3(B.l_d, P, p, ld);
-              st3(B.l_thr, P, p, thr);
-              B.l_dvcm[p] = dvcm;
-              B.l_dvc[p] = dvc;
+              st3r(B.ls, p, PS_O, lo);
+              st3r(B.ls, p, PS_D, ld);
+              st3r(B.ls, p, PS_THR, thr);
+              psf(B.ls, p, PS_DVCM) = dvcm;
+              psf(B.ls, p, PS_DVC) = dvc;
               V.l_dvm[p] = dvm;
-              B.l_len[p] = len;
+              psi(B.ls, p, PS_LEN) = len;
             }
-            B.l_ctr[p] = rng.ctr;
+            psu(B.ls, p, PS_CTR) = rng.ctr;
           }
         }
       }
@@ -322,7 +322,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_vcm_fixup(VcmGroup G_) {
       cont = V.l_scont[q];
     }
     if (cmpf(pd) == 0 && cmpf(pg) == 0) {
-      B.v_count[p] = 0;  // its only vertex (slot 0)
+      psi(B.ls, p, PS_VCOUNT) = 0;  // its only vertex (slot 0)
     } else {
       B.v_pd[p] = pd;
       B.v_pg[p] = pg;
@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_vgrid_count(VcmGroup G_) {
   const int gstride = gridDim.x * blockDim.x;
   const int nround = (P + gstride - 1) / gstride * gstride;
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < nround; p += gstride) {
-    const int nv = p < P ? B.v_count[p] : 0;
+    const int nv = p < P ? psi(B.ls, p, PS_VCOUNT) : 0;
     for (int k = 0; k < nv; ++k) {
       const V3 pos = ld3(B.v_pos, kVMax * P, k * P + p);
       atomicAdd(&X.V.cnt[vcm_bucket(X, pos)], 1);
@@ -358,7 +358,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_vgrid_scatter(VcmGroup G_) {
   const VcmBuf& V = X.V;
   const int P = X.a.P;
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-    const int nv = B.v_count[p];
+    const int nv = psi(B.ls, p, PS_VCOUNT);
     for (int k = 0; k < nv; ++k) {
       const int vs = k * P + p;
       const V3 pos = ld3(B.v_pos, kVMax * P, vs);
@@ -480,12 +480,12 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
         if (b.mat != 0) {
           hp = h.p;
           hn = h.n;
-          pix = B.c_pix[p];
-          dvcm = B.c_dvcm[p];
-          dvc = B.c_dvc[p];
+          pix = psi(B.cs, p, PS_PIX);
+          dvcm = psf(B.cs, p, PS_DVCM);
+          dvc = psf(B.cs, p, PS_DVC);
           dvm = V.c_dvm[p];
-          len = B.c_len[p];
-          thr = ld3(B.c_thr, P, p);
+          len = psi(B.cs, p, PS_LEN);
+          thr = ld3r(B.cs, p, PS_THR);
           dvcm *= (t * t);  // (:190-193)
           dvcm /= fabsf(b.wi.z);
           dvc /= fabsf(b.wi.z);
@@ -509,7 +509,7 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
               }
             }
           } else if (len < A.maxlen) {
-            Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), B.c_ctr[p]};
+            Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(p)), psu(B.cs, p, PS_CTR)};
             if (!b.delta && len + 1 >= X.minlen) {  // getDirectIllumination (:216-222, :516-573)
               const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
               const DLight L = S.lights[lid];
@@ -537,24 +537,24 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
             }
             if (!b.delta) {
               conn_phase = true;
-              nv = B.v_count[p];
+              nv = psi(B.ls, p, PS_VCOUNT);
               query = any_verts;  // vertex merging (:265-276): queued for the next launch
               cdvm = dvm;
             }
-            V3 so = ld3(B.c_o, P, p), sd = ld3(B.c_d, P, p);
+            V3 so = ld3r(B.cs, p, PS_O), sd = ld3r(B.cs, p, PS_D);
             if (vcm_scatter(X, rng, b, hp, so, sd, thr, dvcm, dvc, dvm)) {
               ext = true;
               e_o = so + sd * WR_EPS;
               e_d = normalize(sd);
-              st3(B.c_o, P, p, so);
-              st3(B.c_d, P, p, sd);
-              st3(B.c_thr, P, p, thr);
-              B.c_dvcm[p] = dvcm;
-              B.c_dvc[p] = dvc;
+              st3r(B.cs, p, PS_O, so);
+              st3r(B.cs, p, PS_D, sd);
+              st3r(B.cs, p, PS_THR, thr);
+              psf(B.cs, p, PS_DVCM) = dvcm;
+              psf(B.cs, p, PS_DVC) = dvc;
               V.c_dvm[p] = dvm;
-              B.c_len[p] = len + 1;
+              psi(B.cs, p, PS_LEN) = len + 1;
             }
-            B.c_ctr[p] = rng.ctr;
+            psu(B.cs, p, PS_CTR) = rng.ctr;
           }
         }
       }
