@@ -33,12 +33,53 @@ __device__ __forceinline__ void st3r(float* s, int p, int k, V3 v) {
   r[2] = v.z;
 }
 
+// Stored light vertices (lightStates, bidirPathTracing.cpp:101-102), one
+// 80-byte record per vertex slot k * P + p: the camera pass reads a path's
+// vertices by path index (connectVertices, :219-257).
+enum : int {
+  VS_POS = 0, VS_N = 3, VS_WI = 6, VS_THR = 9, VS_DVCM = 12, VS_DVC = 13, VS_CONT = 14, VS_PD = 15, VS_PG = 16,
+  VS_LEN = 17, VS_NSPEC = 18, VS_MAT = 19, VS_WORDS = 20
+};
+__device__ __forceinline__ float& vsf(float* s, int i, int k) { return s[size_t(i) * VS_WORDS + k]; }
+__device__ __forceinline__ int& vsi(float* s, int i, int k) {
+  return reinterpret_cast<int*>(s)[size_t(i) * VS_WORDS + k];
+}
+__device__ __forceinline__ V3 vld3(const float* s, int i, int k) {
+  const float* r = s + size_t(i) * VS_WORDS + k;
+  return v3(r[0], r[1], r[2]);
+}
+__device__ __forceinline__ void vst3(float* s, int i, int k, V3 v) {
+  float* r = s + size_t(i) * VS_WORDS + k;
+  r[0] = v.x;
+  r[1] = v.y;
+  r[2] = v.z;
+}
+
+// A camera vertex's direct-illumination record (getDirectIllumination,
+// :484-608), one 64-byte record per path, finalised by its last resolved ray
+enum : int {
+  DR_NEE = 0, DR_NEEW = 3, DR_BSDF = 4, DR_THR = 7, DR_WLEN = 10, DR_FLAGS = 11, DR_LIGHT = 12, DR_PIX = 13,
+  DR_STATE = 14, DR_WORDS = 16
+};
+__device__ __forceinline__ float& drf(float* s, int p, int k) { return s[size_t(p) * DR_WORDS + k]; }
+__device__ __forceinline__ int& dri(float* s, int p, int k) {
+  return reinterpret_cast<int*>(s)[size_t(p) * DR_WORDS + k];
+}
+__device__ __forceinline__ V3 drld3(const float* s, int p, int k) {
+  const float* r = s + size_t(p) * DR_WORDS + k;
+  return v3(r[0], r[1], r[2]);
+}
+__device__ __forceinline__ void drst3(float* s, int p, int k, V3 v) {
+  float* r = s + size_t(p) * DR_WORDS + k;
+  r[0] = v.x;
+  r[1] = v.y;
+  r[2] = v.z;
+}
+
 struct BdptBuf {
   int P = 0, cap_sq = 0;
   float *ls, *cs;  // light / camera subpath state, PS_WORDS floats per path
-  // stored light vertices [kVMax][...][P]
-  float *v_pos, *v_n, *v_wi, *v_thr, *v_dvcm, *v_dvc, *v_cont, *v_pd, *v_pg;
-  int *v_len, *v_nspec, *v_mat;
+  float* vs;       // stored light vertices, VS_WORDS floats per slot k * P + p (k < kVMax)
   // extension-ray queues (double buffered)
   float *q_o[2], *q_d[2], *q_t[2];
   int *q_path[2], *q_prim[2];
@@ -51,9 +92,7 @@ struct BdptBuf {
     int *meta, *pix, *prim;
   } sq[2];
   struct Di {
-    float *nee, *neew, *bsdf, *thr, *wlen;
-    int *flags, *light, *pix;
-    int* state;  // rays still to resolve | DI_VIS | DI_SAME (one atomic per resolved ray)
+    float* r;  // DR_WORDS floats per path (DR_*); DR_STATE: rays still to resolve | DI_VIS | DI_SAME
   } di[2];
   // direct-illumination records (getDirectIllumination, :484-608)
 };
@@ -186,18 +225,18 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
       if (!b.delta) {  // lightStates.push_back (:101-102)
         const int k = psi(B.ls, p, PS_VCOUNT);
         const int slot = k * P + p;
-        st3(B.v_pos, kVMax * P, slot, h.p);
-        st3(B.v_n, kVMax * P, slot, h.n);
-        st3(B.v_wi, kVMax * P, slot, b.wi);
-        st3(B.v_thr, kVMax * P, slot, thr);
-        B.v_dvcm[slot] = dvcm;
-        B.v_dvc[slot] = dvc;
-        B.v_cont[slot] = b.cont;
-        B.v_pd[slot] = b.pd;
-        B.v_pg[slot] = b.pg;
-        B.v_len[slot] = len;
-        B.v_nspec[slot] = nspec;
-        B.v_mat[slot] = b.mat;
+        vst3(B.vs, slot, VS_POS, h.p);
+        vst3(B.vs, slot, VS_N, h.n);
+        vst3(B.vs, slot, VS_WI, b.wi);
+        vst3(B.vs, slot, VS_THR, thr);
+        vsf(B.vs, slot, VS_DVCM) = dvcm;
+        vsf(B.vs, slot, VS_DVC) = dvc;
+        vsf(B.vs, slot, VS_CONT) = b.cont;
+        vsf(B.vs, slot, VS_PD) = b.pd;
+        vsf(B.vs, slot, VS_PG) = b.pg;
+        vsi(B.vs, slot, VS_LEN) = len;
+        vsi(B.vs, slot, VS_NSPEC) = nspec;
+        vsi(B.vs, slot, VS_MAT) = b.mat;
         psi(B.ls, p, PS_VCOUNT) = k + 1;
         if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
           const DCam& cam = S.cam;
@@ -485,15 +524,15 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
           // nor the BSDF ray the contribution is exactly zero (:533-607)
           const int nrays = (nee ? 1 : 0) + (dib ? 1 : 0);
           if (nrays > 0) {
-            D.flags[p] = flags;
-            st3(D.nee, P, p, nee_val);
-            D.neew[p] = nee_w;
-            st3(D.bsdf, P, p, bsdf_val);
-            st3(D.thr, P, p, thr);
-            D.wlen[p] = wlen;
-            D.light[p] = lid;
-            D.pix[p] = pix;
-            D.state[p] = nrays;
+            dri(D.r, p, DR_FLAGS) = flags;
+            drst3(D.r, p, DR_NEE, nee_val);
+            drf(D.r, p, DR_NEEW) = nee_w;
+            drst3(D.r, p, DR_BSDF, bsdf_val);
+            drst3(D.r, p, DR_THR, thr);
+            drf(D.r, p, DR_WLEN) = wlen;
+            dri(D.r, p, DR_LIGHT) = lid;
+            dri(D.r, p, DR_PIX) = pix;
+            dri(D.r, p, DR_STATE) = nrays;
           }
         }
         if (!b.delta) {
@@ -541,12 +580,12 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
       V3 sdir{}, stgt{}, sval{};
       if (conn_phase && k < nv) {
         const int slot = k * P + p;
-        const int llen = B.v_len[slot];
+        const int llen = vsi(B.vs, slot, VS_LEN);
         if (llen + 1 + len > A.maxlen) {
           nv = k;  // break (:237-239)
         } else {
           // connectVertices (:610-665)
-          const V3 lpos = ld3(B.v_pos, kVMax * P, slot);
+          const V3 lpos = vld3(B.vs, slot, VS_POS);
           V3 dir = lpos - hp;
           const float d2 = sqr_len(dir);
           const float dist = sqrtf(d2);
@@ -557,12 +596,12 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
             cdp *= b.cont;
             crp *= b.cont;
             Bsdf lb;
-            lb.mat = B.v_mat[slot];
-            lb.fr = frame_from_z(ld3(B.v_n, kVMax * P, slot));
-            lb.wi = ld3(B.v_wi, kVMax * P, slot);
-            lb.pd = B.v_pd[slot];
-            lb.pg = B.v_pg[slot];
-            lb.cont = B.v_cont[slot];
+            lb.mat = vsi(B.vs, slot, VS_MAT);
+            lb.fr = frame_from_z(vld3(B.vs, slot, VS_N));
+            lb.wi = vld3(B.vs, slot, VS_WI);
+            lb.pd = vsf(B.vs, slot, VS_PD);
+            lb.pg = vsf(B.vs, slot, VS_PG);
+            lb.cont = vsf(B.vs, slot, VS_CONT);
             float cos_l = 0.f, ldp, lrp;
             const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
             if (!black(lf)) {
@@ -574,7 +613,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
                 const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
                 const V3 res = mul(cf, lf) * G;
                 if (!black(res)) {
-                  const float wl = cdpa * (B.v_dvcm[slot] + lrp * B.v_dvc[slot]);
+                  const float wl = cdpa * (vsf(B.vs, slot, VS_DVCM) + lrp * vsf(B.vs, slot, VS_DVC));
                   const float wc = ldpa * (cdvcm + crp * cdvc);
                   const float w = WR_TEST_CONN_W / (wl + 1.f + wc);
                   const bool counts = len_ok(A.ctl, llen + 1 + len);
@@ -584,8 +623,8 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
                     stgt = hp + dir * dist;
                     if (counts) {
                       const float wlen = 1.f / (static_cast<float>(llen) + 1.f + static_cast<float>(len) -
-                                                static_cast<float>(B.v_nspec[slot]) - static_cast<float>(cnspec));
-                      const V3 lthr = ld3(B.v_thr, kVMax * P, slot);
+                                                static_cast<float>(vsi(B.vs, slot, VS_NSPEC)) - static_cast<float>(cnspec));
+                      const V3 lthr = vld3(B.vs, slot, VS_THR);
                       sval = mul(mul(cthr, lthr), res * w) * wlen;
                     }
                   }
@@ -704,8 +743,8 @@ __device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int
         is_closest = true;
         bool same = false;
         if (prim >= 0) {
-          const int m = S.prim_mat[prim];
-          same = m < 0 && -m - 1 == D.light[p];
+          const int m = __float_as_int(S.prim_rec[2 * static_cast<size_t>(prim) + 1].z);
+          same = m < 0 && -m - 1 == dri(D.r, p, DR_LIGHT);
         }
         di_bits = same ? DI_SAME : 0;
       } else {  // Scene::occluded: position equality (scene.cpp:55-69)
@@ -729,23 +768,23 @@ __device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int
         }
       }
       if (di_bits >= 0) {
-        const int st = atomicAdd(&D.state[p], di_bits - 1) + di_bits - 1;
+        const int st = atomicAdd(&dri(D.r, p, DR_STATE), di_bits - 1) + di_bits - 1;
         if ((st & DI_COUNT) == 0) {
-          const int flags = D.flags[p];
+          const int flags = dri(D.r, p, DR_FLAGS);
           V3 res = v3(0.f, 0.f, 0.f);
           float weight = 0.f;
           if ((flags & DI_NEE) && (st & DI_VIS)) {
-            weight = D.neew[p];
-            res = res + ld3(D.nee, P, p);
+            weight = drf(D.r, p, DR_NEEW);
+            res = res + drld3(D.r, p, DR_NEE);
           }
           V3 di;
           if (flags & DI_EARLY) {
             di = res;
           } else {
-            if ((flags & DI_BSDF) && (st & DI_SAME)) res = res + ld3(D.bsdf, P, p);
+            if ((flags & DI_BSDF) && (st & DI_SAME)) res = res + drld3(D.r, p, DR_BSDF);
             di = res * weight;
           }
-          film_add(A.film, D.pix[p], mul(ld3(D.thr, P, p), di) * D.wlen[p]);
+          film_add(A.film, dri(D.r, p, DR_PIX), mul(drld3(D.r, p, DR_THR), di) * drf(D.r, p, DR_WLEN));
         }
       }
     }

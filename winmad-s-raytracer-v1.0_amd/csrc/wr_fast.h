@@ -1191,9 +1191,8 @@ constexpr float kGrazeRel = 1e-5f;
 // tie-list entries: launch index, | kWalkEntry for a ray the KD walk settles
 constexpr int kWalkEntry = 1 << 30;
 __device__ __forceinline__ bool grazing_test(const DevScene& S, int prim, V3 dir) {
-  if (S.prim_type[prim] != 0) return false;
-  const float4 g = S.prim_tri[prim];
-  const float2 g2 = S.prim_tri2[prim];
+  const float4 g = S.prim_rec[2 * static_cast<size_t>(prim)], g2 = S.prim_rec[2 * static_cast<size_t>(prim) + 1];
+  if (__float_as_int(g2.w) != 0) return false;  // a sphere
   const float A = g.x, B = g.y, C = g.z, D = g.w, E = g2.x, F = g2.y;
   const float G = dir.x, H = dir.y, I = dir.z;
   const float EIHF = E * I - H * F, GFDI = G * F - D * I, DHEG = D * H - E * G;

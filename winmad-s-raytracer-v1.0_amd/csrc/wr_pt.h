@@ -5,11 +5,29 @@
 #pragma once
 
 // =============================================================== PT
+// PT path state, one 32-byte record per path (the vertex kernel gathers it by
+// path index): path weight, last BSDF pdf / specular flag, length, pixel, RNG counter
+enum : int { PT_PW = 0, PT_LPDF = 3, PT_LSPEC = 4, PT_LEN = 5, PT_PIX = 6, PT_CTR = 7, PT_WORDS = 8 };
+__device__ __forceinline__ float& ptf(float* s, int p, int k) { return s[size_t(p) * PT_WORDS + k]; }
+__device__ __forceinline__ int& pti(float* s, int p, int k) {
+  return reinterpret_cast<int*>(s)[size_t(p) * PT_WORDS + k];
+}
+__device__ __forceinline__ uint32_t& ptu(float* s, int p, int k) {
+  return reinterpret_cast<uint32_t*>(s)[size_t(p) * PT_WORDS + k];
+}
+__device__ __forceinline__ V3 pld3(const float* s, int p, int k) {
+  const float* r = s + size_t(p) * PT_WORDS + k;
+  return v3(r[0], r[1], r[2]);
+}
+__device__ __forceinline__ void pst3(float* s, int p, int k, V3 v) {
+  float* r = s + size_t(p) * PT_WORDS + k;
+  r[0] = v.x;
+  r[1] = v.y;
+  r[2] = v.z;
+}
 struct PtBuf {
   int P = 0;
-  float *o, *d, *pw, *last_pdf;
-  int *last_spec, *len, *pix;
-  uint32_t* ctr;
+  float* st;  // PT_WORDS floats per path
   float *q_o[2], *q_d[2], *q_t[2];
   int *q_path[2], *q_prim[2];
   // NEE shadow rays, two buffers: those of step `slot` are [slot & 1], so a
@@ -48,14 +66,12 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_gen(PtGroup G_
     const V3 pr = sample_rect_strat(rng.v(), v0, v1, v2, static_cast<int>(A.k), A.grid_len);
     const V3 wp = t_point(cam.r2w, v3(pr.x, pr.y, 0.f));
     const V3 d = normalize(wp - cam.pos);
-    st3(T.o, P, p, cam.pos);
-    st3(T.d, P, p, d);
-    st3(T.pw, P, p, v3(1.f, 1.f, 1.f));
-    T.last_pdf[p] = 1.f;
-    T.last_spec[p] = 1;
-    T.len[p] = 1;
-    T.pix[p] = i * A.W + jj;
-    T.ctr[p] = rng.ctr;
+    pst3(T.st, p, PT_PW, v3(1.f, 1.f, 1.f));
+    ptf(T.st, p, PT_LPDF) = 1.f;
+    pti(T.st, p, PT_LSPEC) = 1;
+    pti(T.st, p, PT_LEN) = 1;
+    pti(T.st, p, PT_PIX) = i * A.W + jj;
+    ptu(T.st, p, PT_CTR) = rng.ctr;
     st3(T.q_o[0], P, p, cam.pos);  // Ray r(ray): no EPS offset for the primary ray
     st3(T.q_d[0], P, p, d);
     T.q_path[0][p] = p;
@@ -73,14 +89,12 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_pt_gen_rays(PtGro
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
     const wr_ray r = rays[p];
     const V3 o = v3(r.o[0], r.o[1], r.o[2]), d = v3(r.d[0], r.d[1], r.d[2]);
-    st3(T.o, P, p, o);
-    st3(T.d, P, p, d);
-    st3(T.pw, P, p, v3(1.f, 1.f, 1.f));
-    T.last_pdf[p] = 1.f;
-    T.last_spec[p] = 1;
-    T.len[p] = 1;
-    T.pix[p] = p;
-    T.ctr[p] = 0;
+    pst3(T.st, p, PT_PW, v3(1.f, 1.f, 1.f));
+    ptf(T.st, p, PT_LPDF) = 1.f;
+    pti(T.st, p, PT_LSPEC) = 1;
+    pti(T.st, p, PT_LEN) = 1;
+    pti(T.st, p, PT_PIX) = p;
+    ptu(T.st, p, PT_CTR) = 0;
     st3(T.q_o[0], P, p, o);
     st3(T.q_d[0], P, p, d);
     T.q_path[0][p] = p;
@@ -111,25 +125,25 @@ __device__ __forceinline__ void pt_shade_body(const PtArgs& A, int slot, int bid
         const Hit h = rebuild_hit(S, prim, t, o, d);
         Bsdf b;
         bsdf_init(b, -d, h.n, h.mat, S.mats);
-        pix = T.pix[p];
+        pix = pti(T.st, p, PT_PIX);
         if (b.mat != 0) {
-          V3 pw = ld3(T.pw, P, p);
-          const int len = T.len[p];
+          V3 pw = pld3(T.st, p, PT_PW);
+          const int len = pti(T.st, p, PT_LEN);
           if (b.mat < 0) {  // (:53-73)
             const DLight L = S.lights[-b.mat - 1];
             float dpa, ep;
             const V3 c = light_radiance(L, d, &dpa, &ep);
             if (!black(c)) {
               float mw = 1.f;
-              if (len > 1 && !T.last_spec[p]) {
+              if (len > 1 && !pti(T.st, p, PT_LSPEC)) {
                 const float dp = dpa * (t * t) / fabsf(b.wi.z);  // pdfAtoW
-                const float lp = T.last_pdf[p];
+                const float lp = ptf(T.st, p, PT_LPDF);
                 mw = lp / (lp + dp * lpp);
               }
               film_add(A.film, pix, mul(pw, c) * mw);
             }
           } else if (!(len > A.max_depth) && cmpf(b.cont) != 0) {
-            Rng rng{stream_key(A.seed, A.k, 2, static_cast<uint32_t>(p)), T.ctr[p]};
+            Rng rng{stream_key(A.seed, A.k, 2, static_cast<uint32_t>(p)), ptu(T.st, p, PT_CTR)};
             if (!b.delta) {  // (:81-118)
               const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
               const DLight L = S.lights[lid];
@@ -170,13 +184,13 @@ __device__ __forceinline__ void pt_shade_body(const PtArgs& A, int slot, int bid
                 ext = true;
                 e_o = h.p + dn * WR_EPS;
                 e_d = dn;  // r.dir stays un-normalised (:144-145)
-                st3(T.pw, P, p, pw);
-                T.last_spec[p] = lspec;
-                T.last_pdf[p] = lpdf;
-                T.len[p] = len + 1;
+                pst3(T.st, p, PT_PW, pw);
+                pti(T.st, p, PT_LSPEC) = lspec;
+                ptf(T.st, p, PT_LPDF) = lpdf;
+                pti(T.st, p, PT_LEN) = len + 1;
               }
             }
-            T.ctr[p] = rng.ctr;
+            ptu(T.st, p, PT_CTR) = rng.ctr;
           }
         }
       }

@@ -590,18 +590,7 @@ void layout_bdpt(Arena& a, BdptBuf& B, int P) {
   const size_t sP = P, sV = size_t(kVMax) * P, sQ = B.cap_sq;
   B.ls = a.take<float>(PS_WORDS * sP);
   B.cs = a.take<float>(PS_WORDS * sP);
-  B.v_pos = a.take<float>(3 * sV);
-  B.v_n = a.take<float>(3 * sV);
-  B.v_wi = a.take<float>(3 * sV);
-  B.v_thr = a.take<float>(3 * sV);
-  B.v_dvcm = a.take<float>(sV);
-  B.v_dvc = a.take<float>(sV);
-  B.v_cont = a.take<float>(sV);
-  B.v_pd = a.take<float>(sV);
-  B.v_pg = a.take<float>(sV);
-  B.v_len = a.take<int>(sV);
-  B.v_nspec = a.take<int>(sV);
-  B.v_mat = a.take<int>(sV);
+  B.vs = a.take<float>(VS_WORDS * sV);
 
   for (int q = 0; q < 2; ++q) {
     B.q_o[q] = a.take<float>(3 * sP);
@@ -621,30 +610,14 @@ void layout_bdpt(Arena& a, BdptBuf& B, int P) {
     q.meta = a.take<int>(sQ);
     q.pix = a.take<int>(sQ);
     q.prim = a.take<int>(sQ);
-    BdptBuf::Di& d = B.di[k];
-    d.nee = a.take<float>(3 * sP);
-    d.neew = a.take<float>(sP);
-    d.bsdf = a.take<float>(3 * sP);
-    d.thr = a.take<float>(3 * sP);
-    d.wlen = a.take<float>(sP);
-    d.flags = a.take<int>(sP);
-    d.light = a.take<int>(sP);
-    d.pix = a.take<int>(sP);
-    d.state = a.take<int>(sP);
+    B.di[k].r = a.take<float>(DR_WORDS * sP);
   }
 }
 
 void layout_pt(Arena& a, PtBuf& T, int P) {
   T.P = P;
   const size_t sP = P;
-  T.o = a.take<float>(3 * sP);
-  T.d = a.take<float>(3 * sP);
-  T.pw = a.take<float>(3 * sP);
-  T.last_pdf = a.take<float>(sP);
-  T.last_spec = a.take<int>(sP);
-  T.len = a.take<int>(sP);
-  T.pix = a.take<int>(sP);
-  T.ctr = a.take<uint32_t>(sP);
+  T.st = a.take<float>(PT_WORDS * sP);
   for (int q = 0; q < 2; ++q) {
     T.q_o[q] = a.take<float>(3 * sP);
     T.q_d[q] = a.take<float>(3 * sP);
@@ -1530,7 +1503,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
     a.take<uint4>(nn); a.take<uint2>(nn); a.take<uint4>(kRecU4 * nn); a.take<float4>(nr); a.take<float4>(nr);
     a.take<float2>(nr);
     a.take<int>(np); a.take<int>(np); a.take<float4>(np); a.take<float2>(np); a.take<float4>(np);
-    a.take<float4>(np); a.take<float2>(np); a.take<DLight>(lights.size() + 1); a.take<DMat>(mats.size());
+    a.take<float4>(np); a.take<float2>(np); a.take<float4>(2 * np); a.take<DLight>(lights.size() + 1);
+    a.take<DMat>(mats.size());
     a.take<DevCounters>(1);
   });
   if (int rc = c->scene_mem.reserve(total)) {
@@ -1555,12 +1529,21 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   float4* dpsph = A.take<float4>(np);
   float4* dpsb0 = A.take<float4>(np);
   float2* dpsb1 = A.take<float2>(np);
+  float4* dprec = A.take<float4>(2 * np);
+  std::vector<float4> prec(2 * np);
+  for (size_t i = 0; i < np; ++i) {
+    prec[2 * i] = ptri[i];
+    float mb, tb;  // the int fields' bits (host code: no __int_as_float)
+    std::memcpy(&mb, &pmat[i], 4);
+    std::memcpy(&tb, &ptype[i], 4);
+    prec[2 * i + 1] = make_float4(ptri2[i].x, ptri2[i].y, mb, tb);
+  }
   DLight* dl = A.take<DLight>(lights.size() + 1);
   DMat* dm = A.take<DMat>(mats.size());
   c->ctr = A.take<DevCounters>(1);
   hipError_t e = hipSuccess;
   for (hipError_t x : {up(dn, nrec), up(dnr, nrec_r), up(dn3, nrec3), up(dra, ra), up(drb, rb), up(drc, rcv), up(dpm, pmat), up(dpt, ptype),
-                       up(dptri, ptri), up(dptri2, ptri2), up(dpsph, psph), up(dpsb0, psb0), up(dpsb1, psb1),
+                       up(dptri, ptri), up(dptri2, ptri2), up(dpsph, psph), up(dpsb0, psb0), up(dpsb1, psb1), up(dprec, prec),
                        up(dm, mats)})
     if (x != hipSuccess) e = x;
   if (!lights.empty() && e == hipSuccess) e = up(dl, lights);
@@ -1579,6 +1562,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   d.prim_tri = dptri;
   d.prim_tri2 = dptri2;
   d.prim_sph = dpsph;
+  d.prim_rec = dprec;
   d.prim_sbox0 = dpsb0;
   d.prim_sbox1 = dpsb1;
   d.root_l = v3(s.root_l.x, s.root_l.y, s.root_l.z);

@@ -41,6 +41,9 @@ struct DevScene {
   const float4* prim_tri;   // (A, B, C, D) per primitive (winner normal)
   const float2* prim_tri2;  // (E, F)
   const float4* prim_sph;   // (cx, cy, cz, r)
+  // the same per primitive as one 32-byte record (the vertex kernels gather it
+  // by primitive): (A, B, C, D), (E, F, matId bits, type bits)
+  const float4* prim_rec;
   const float4* prim_sbox0; // (lx, ly, lz, rx) AABB after extend()
   const float2* prim_sbox1; // (ry, rz)
   V3 root_l, root_r;
@@ -970,8 +973,9 @@ __device__ __forceinline__ Hit rebuild_hit(const DevScene& S, int prim, float t,
   Hit h;
   h.t = t;
   h.p = o + d * t;
-  h.mat = S.prim_mat[prim];
-  if (S.prim_type[prim] != 0) {
+  const float4 r0 = S.prim_rec[2 * static_cast<size_t>(prim)], r1 = S.prim_rec[2 * static_cast<size_t>(prim) + 1];
+  h.mat = __float_as_int(r1.z);
+  if (__float_as_int(r1.w) != 0) {
     float4 cs = S.prim_sph[prim];
     h.n = normalize(h.p - v3(cs.x, cs.y, cs.z));
     float tt;
@@ -979,10 +983,8 @@ __device__ __forceinline__ Hit rebuild_hit(const DevScene& S, int prim, float t,
     sph_hit(S, prim, o, d, 0.f, WR_INF, tt, &in);
     h.inside = in;
   } else {
-    float4 g = S.prim_tri[prim];
-    float2 g2 = S.prim_tri2[prim];
     // (p1 - p0) x (p2 - p0) == (p0 - p1) x (p0 - p2) exactly
-    h.n = normalize(cross(v3(g.x, g.y, g.z), v3(g.w, g2.x, g2.y)));
+    h.n = normalize(cross(v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y)));
     h.inside = (dot(d, h.n) < WR_EPS) ? 0 : 1;
   }
   return h;

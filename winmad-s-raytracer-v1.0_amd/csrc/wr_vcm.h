@@ -212,18 +212,18 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
           if (!b.delta) {  // lightVertices.push_back (:98-113)
             const int k = psi(B.ls, p, PS_VCOUNT);
             const int vs = k * P + p;
-            st3(B.v_pos, kVMax * P, vs, h.p);
-            st3(B.v_n, kVMax * P, vs, h.n);
-            st3(B.v_wi, kVMax * P, vs, b.wi);
-            st3(B.v_thr, kVMax * P, vs, thr);
-            B.v_dvcm[vs] = dvcm;
-            B.v_dvc[vs] = dvc;
+            vst3(B.vs, vs, VS_POS, h.p);
+            vst3(B.vs, vs, VS_N, h.n);
+            vst3(B.vs, vs, VS_WI, b.wi);
+            vst3(B.vs, vs, VS_THR, thr);
+            vsf(B.vs, vs, VS_DVCM) = dvcm;
+            vsf(B.vs, vs, VS_DVC) = dvc;
             V.v_dvm[vs] = dvm;
-            B.v_cont[vs] = b.cont;
-            B.v_pd[vs] = b.pd;
-            B.v_pg[vs] = b.pg;
-            B.v_len[vs] = len;
-            B.v_mat[vs] = b.mat;
+            vsf(B.vs, vs, VS_CONT) = b.cont;
+            vsf(B.vs, vs, VS_PD) = b.pd;
+            vsf(B.vs, vs, VS_PG) = b.pg;
+            vsi(B.vs, vs, VS_LEN) = len;
+            vsi(B.vs, vs, VS_MAT) = b.mat;
             psi(B.ls, p, PS_VCOUNT) = k + 1;
             if (b.mat > 0 && len + 1 >= X.minlen) {  // connectToCamera (:116-127, :332-384)
               const DCam& cam = S.cam;
@@ -324,9 +324,9 @@ __global__ void __launch_bounds__(kShadeBlock) k_vcm_fixup(VcmGroup G_) {
     if (cmpf(pd) == 0 && cmpf(pg) == 0) {
       psi(B.ls, p, PS_VCOUNT) = 0;  // its only vertex (slot 0)
     } else {
-      B.v_pd[p] = pd;
-      B.v_pg[p] = pg;
-      B.v_cont[p] = cont;
+      vsf(B.vs, p, VS_PD) = pd;
+      vsf(B.vs, p, VS_PG) = pg;
+      vsf(B.vs, p, VS_CONT) = cont;
     }
   }
 }
@@ -341,7 +341,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_vgrid_count(VcmGroup G_) {
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < nround; p += gstride) {
     const int nv = p < P ? psi(B.ls, p, PS_VCOUNT) : 0;
     for (int k = 0; k < nv; ++k) {
-      const V3 pos = ld3(B.v_pos, kVMax * P, k * P + p);
+      const V3 pos = vld3(B.vs, k * P + p, VS_POS);
       atomicAdd(&X.V.cnt[vcm_bucket(X, pos)], 1);
     }
     const unsigned long long tot = wave_sum(static_cast<unsigned long long>(nv));
@@ -361,15 +361,15 @@ __global__ void __launch_bounds__(kShadeBlock) k_vgrid_scatter(VcmGroup G_) {
     const int nv = psi(B.ls, p, PS_VCOUNT);
     for (int k = 0; k < nv; ++k) {
       const int vs = k * P + p;
-      const V3 pos = ld3(B.v_pos, kVMax * P, vs);
+      const V3 pos = vld3(B.vs, vs, VS_POS);
       const uint32_t h = vcm_bucket(X, pos);
       const int idx = V.start[h] + atomicSub(&V.cnt[h], 1) - 1;
-      const Frame fr = frame_from_z(ld3(B.v_n, kVMax * P, vs));
-      const V3 ldir = to_world(fr, ld3(B.v_wi, kVMax * P, vs));  // BSDF::wiWorld (bsdf.h:101-104)
-      const V3 thr = ld3(B.v_thr, kVMax * P, vs);
-      V.rpos[idx] = make_float4(pos.x, pos.y, pos.z, __int_as_float(B.v_len[vs]));
-      V.rdat[2 * static_cast<size_t>(idx)] = make_float4(ldir.x, ldir.y, ldir.z, B.v_cont[vs]);
-      V.rdat[2 * static_cast<size_t>(idx) + 1] = make_float4(thr.x, thr.y, thr.z, B.v_dvcm[vs]);
+      const Frame fr = frame_from_z(vld3(B.vs, vs, VS_N));
+      const V3 ldir = to_world(fr, vld3(B.vs, vs, VS_WI));  // BSDF::wiWorld (bsdf.h:101-104)
+      const V3 thr = vld3(B.vs, vs, VS_THR);
+      V.rpos[idx] = make_float4(pos.x, pos.y, pos.z, __int_as_float(vsi(B.vs, vs, VS_LEN)));
+      V.rdat[2 * static_cast<size_t>(idx)] = make_float4(ldir.x, ldir.y, ldir.z, vsf(B.vs, vs, VS_CONT));
+      V.rdat[2 * static_cast<size_t>(idx) + 1] = make_float4(thr.x, thr.y, thr.z, vsf(B.vs, vs, VS_DVCM));
       V.rdvm[idx] = V.v_dvm[vs];
     }
   }
@@ -593,12 +593,12 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
         V3 sdir{}, stgt{}, sval{};
         if (conn_phase && k < nv) {
           const int vs = k * P + p;
-          const int llen = B.v_len[vs];
+          const int llen = vsi(B.vs, vs, VS_LEN);
           if (llen + 1 + len > A.maxlen) {
             nv = k;  // break (:242-244)
-          } else if (llen + 1 + len >= X.minlen && B.v_mat[vs] > 0) {  // emitter vertices: BSDF::f is black
+          } else if (llen + 1 + len >= X.minlen && vsi(B.vs, vs, VS_MAT) > 0) {  // emitter vertices: BSDF::f is black
             // connectVertices (:575-636)
-            const V3 lpos = ld3(B.v_pos, kVMax * P, vs);
+            const V3 lpos = vld3(B.vs, vs, VS_POS);
             V3 dir = lpos - hp;
             const float d2 = sqr_len(dir);
             const float dist = sqrtf(d2);
@@ -609,12 +609,12 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
               cdp *= b.cont;
               crp *= b.cont;
               Bsdf lb;
-              lb.mat = B.v_mat[vs];
-              lb.fr = frame_from_z(ld3(B.v_n, kVMax * P, vs));
-              lb.wi = ld3(B.v_wi, kVMax * P, vs);
-              lb.pd = B.v_pd[vs];
-              lb.pg = B.v_pg[vs];
-              lb.cont = B.v_cont[vs];
+              lb.mat = vsi(B.vs, vs, VS_MAT);
+              lb.fr = frame_from_z(vld3(B.vs, vs, VS_N));
+              lb.wi = vld3(B.vs, vs, VS_WI);
+              lb.pd = vsf(B.vs, vs, VS_PD);
+              lb.pg = vsf(B.vs, vs, VS_PG);
+              lb.cont = vsf(B.vs, vs, VS_CONT);
               float cos_l = 0.f, ldp, lrp;
               const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
               if (!black(lf)) {
@@ -624,7 +624,7 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
                 if (!(cmpf(G) < 0)) {
                   const float cdpa = cdp * fabsf(cos_l) / (dist * dist);  // pdfWtoA (math.cpp:13-16)
                   const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
-                  const float wl = cdpa * (X.mis_vm + B.v_dvcm[vs] + B.v_dvc[vs] * lrp);
+                  const float wl = cdpa * (X.mis_vm + vsf(B.vs, vs, VS_DVCM) + vsf(B.vs, vs, VS_DVC) * lrp);
                   const float wc = ldpa * (X.mis_vm + cdvcm + cdvc * crp);
                   const float w = 1.f / (wl + 1.f + wc);
                   const V3 res = mul(cf, lf) * w * G;
@@ -632,7 +632,7 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
                     shoot = true;
                     sdir = normalize(dir);
                     stgt = hp + dir * dist;
-                    sval = mul(mul(cthr, ld3(B.v_thr, kVMax * P, vs)), res);
+                    sval = mul(mul(cthr, vld3(B.vs, vs, VS_THR)), res);
                   }
                 }
               }
