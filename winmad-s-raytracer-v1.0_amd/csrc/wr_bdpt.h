@@ -728,7 +728,7 @@ __device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int
   const DevScene& S = A.S;
   const BdptBuf::Sq& Q = B.sq[slot & 1];
   const BdptBuf::Di& D = B.di[slot & 1];
-  const int n = A.sc->sq[slot], cap = B.cap_sq, P = B.P;  // P: buffer stride
+  const int n = A.sc->sq[slot], cap = B.cap_sq;
   const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
   for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {
