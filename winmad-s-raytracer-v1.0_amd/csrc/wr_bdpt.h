@@ -13,6 +13,7 @@ enum : int {
   PS_O = 0, PS_D = 3, PS_THR = 6, PS_DVCM = 9, PS_DVC = 10, PS_LEN = 11, PS_NSPEC = 12, PS_CTR = 13,
   PS_VCOUNT = 14,  // light paths: stored light vertices
   PS_PIX = 14,     // camera paths: film pixel
+  PS_DVM = 15,     // VCM: dVM (vertexcm.h:36)
   PS_WORDS = 16
 };
 __device__ __forceinline__ float& psf(float* s, int p, int k) { return s[size_t(p) * PS_WORDS + k]; }

@@ -512,6 +512,7 @@ struct wr_context {
   bool fast_ok = false;   // scene supports it
   bool fast_on = false;   // WR_TRACE_BVH mode selected
   int fast_blocks = 4096; // resident one-wave workgroups of k_trace_fast
+  int resolve_blocks = 0; // k_fast_resolve's one-wave workgroups (0: fast_blocks; env WR_RESOLVE_GRID per CU)
   bool verify = false;      // WR_BVH_VERIFY=1: every BVH answer checked against the KD walk
   // BDPT hard rays off the critical path (env WR_DEFER=1; off by default)
   int defer = -1;
@@ -654,12 +655,7 @@ size_t vcm_scan_bytes(uint32_t T) {
 void layout_vcm(Arena& a, VcmBuf& V, int P) {
   const size_t sP = P, sV = size_t(kVMax) * P;
   const uint32_t T = vcm_table(P);
-  V.l_dvm = a.take<float>(sP);
-  V.c_dvm = a.take<float>(sP);
-  V.l_spd = a.take<float>(sP);
-  V.l_spg = a.take<float>(sP);
-  V.l_scont = a.take<float>(sP);
-  V.l_shas = a.take<int>(sP);
+  V.l_sb = a.take<float4>(sP);
   V.v_dvm = a.take<float>(sV);
   V.pending = a.take<int>(sP);
   V.cnt = a.take<int>(size_t(T) + 1);
@@ -943,7 +939,8 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     if (c->trace_log) (void)hipEventRecord(fa, stream);
     int* hard = reinterpret_cast<int*>(ts.t2 + ts.t2_cap);
     hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
-                       dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), 0, stream, c->ds, c->fs,
+                       dim3(std::max(1, std::min(c->resolve_blocks > 0 ? c->resolve_blocks : c->fast_blocks, blocks))),
+                       dim3(kTraceBlock), 0, stream, c->ds, c->fs,
                        Q, ctr, ts.t2, hard, ts.hard_n, static_cast<int>(ts.t2_cap));
     if (c->trace_log) (void)hipEventRecord(fb, stream);
     // the hard rays are a few in 10^4: a small grid drains any count (one
@@ -1395,12 +1392,15 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   if (const char* e = std::getenv("WR_TIE_WAVE_MAX")) c->tie_wave_max = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("WR_ISSUE_THREADS")) c->issue_threads = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   if (const char* e = std::getenv("WR_DEFER")) c->defer = std::atoi(e) != 0 ? 1 : 0;
+  if (const char* e = std::getenv("WR_RESOLVE_GRID")) c->resolve_blocks = std::max(0, std::atoi(e));  // per CU; scaled below
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
     // grid-stride vertex / resolve kernels: blocks per CU (knob WR_SHADE_GRID).
     // 2 = one resident round of both group members at 4 waves/SIMD; measured
-    // against 8: C2 +0.9 %, C3 +1.9 %, VCM +1.3 % (16 and 32 lose 1-2 %)
-    int per_cu = 2;
+    // against 8: C2 +0.9 %, C3 +1.9 %, VCM +1.3 % (16 and 32 lose 1-2 %).
+    // With the path state in records (round 3) 1 does better again: C2 20 it.
+    // +2.0 %, 256 it. +2.7 %, C4 +2.6 %, VCM +3 %, C3 -0.4 % (profiles/r3/shade_grid)
+    int per_cu = 1;
     if (const char* e = std::getenv("WR_SHADE_GRID")) per_cu = std::max(1, std::min(64, std::atoi(e)));
     c->grid = std::max(256, prop.multiProcessorCount * per_cu);
   }
@@ -1610,6 +1610,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       return per_cu;
     };
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    c->resolve_blocks *= c->cus;  // WR_RESOLVE_GRID was blocks per CU
     c->trace_blocks = c->cus * resident(TRACE_PLAIN);
     c->trace_blocks_dense = c->cus * resident(TRACE_DENSE);
   }

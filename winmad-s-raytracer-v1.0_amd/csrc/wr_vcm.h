@@ -21,11 +21,11 @@
 // contributions differs.
 
 struct VcmBuf {
-  float *l_dvm, *c_dvm;  // dVM of the light / camera subpath state (vertexcm.h:36)
+  // (dVM of the light / camera subpath state, vertexcm.h:36: word PS_DVM of
+  // BdptBuf's path records)
   // Probabilities of the last non-emitter BSDF built on each light path (the
-  // emitter-vertex quirk, k_vcm_light_shade)
-  float *l_spd, *l_spg, *l_scont;
-  int* l_shas;
+  // emitter-vertex quirk, k_vcm_light_shade): (pd, pg, continueProb, has one)
+  float4* l_sb;
   float* v_dvm;    // [kVMax][P] beside BdptBuf's vertex store
   int* pending;    // light paths whose first vertex is an emitter
   int* cnt;        // [T + 1] vertices per grid bucket, then 0 after the scatter
@@ -107,11 +107,11 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_vcm_light_gen(Vcm
     st3r(B.ls, p, PS_THR, thr);
     psf(B.ls, p, PS_DVCM) = dpdf / epdf;
     psf(B.ls, p, PS_DVC) = dvc;
-    V.l_dvm[p] = dvc * X.mis_vc;
+    psf(B.ls, p, PS_DVM) = dvc * X.mis_vc;
     psi(B.ls, p, PS_LEN) = 1;
     psu(B.ls, p, PS_CTR) = rng.ctr;
     psi(B.ls, p, PS_VCOUNT) = 0;
-    V.l_shas[p] = 0;
+    V.l_sb[p] = make_float4(0.f, 0.f, 0.f, __int_as_float(0));
     st3(B.q_o[0], P, p, pos + dir * WR_EPS);  // Ray(origin + dir * EPS, dir) (:79-80)
     st3(B.q_d[0], P, p, normalize(dir));
     B.q_path[0][p] = p;
@@ -187,20 +187,18 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
           int len = psi(B.ls, p, PS_LEN);
           if (b.mat < 0) {
             if (len > 1) {
-              b.pd = V.l_spd[p];
-              b.pg = V.l_spg[p];
-              b.cont = V.l_scont[p];
+              const float4 sb = V.l_sb[p];
+              b.pd = sb.x;
+              b.pg = sb.y;
+              b.cont = sb.z;
               b.delta = (cmpf(b.pd) == 0 && cmpf(b.pg) == 0);
             } else {
               pend = true;  // decided by k_vcm_fixup
             }
           } else {
-            V.l_spd[p] = b.pd;
-            V.l_spg[p] = b.pg;
-            V.l_scont[p] = b.cont;
-            V.l_shas[p] = 1;
+            V.l_sb[p] = make_float4(b.pd, b.pg, b.cont, __int_as_float(1));
           }
-          float dvcm = psf(B.ls, p, PS_DVCM), dvc = psf(B.ls, p, PS_DVC), dvm = V.l_dvm[p];
+          float dvcm = psf(B.ls, p, PS_DVCM), dvc = psf(B.ls, p, PS_DVC), dvm = psf(B.ls, p, PS_DVM);
           V3 thr = ld3r(B.ls, p, PS_THR);
           // `pathLength > 1 || isFiniteLight == 1` (:94-95): isFiniteLight is a
           // signed 1-bit field (vertexcm.h:31) that reads back -1, so only the
@@ -271,7 +269,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
               st3r(B.ls, p, PS_THR, thr);
               psf(B.ls, p, PS_DVCM) = dvcm;
               psf(B.ls, p, PS_DVC) = dvc;
-              V.l_dvm[p] = dvm;
+              psf(B.ls, p, PS_DVM) = dvm;
               psi(B.ls, p, PS_LEN) = len;
             }
             psu(B.ls, p, PS_CTR) = rng.ctr;
@@ -314,12 +312,13 @@ __global__ void __launch_bounds__(kShadeBlock) k_vcm_fixup(VcmGroup G_) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int p = V.pending[i];
     int q = p - 1;
-    while (q >= 0 && V.l_shas[q] == 0) --q;
+    while (q >= 0 && __float_as_int(V.l_sb[q].w) == 0) --q;
     float pd = 0.f, pg = 0.f, cont = 0.f;
     if (q >= 0) {
-      pd = V.l_spd[q];
-      pg = V.l_spg[q];
-      cont = V.l_scont[q];
+      const float4 sb = V.l_sb[q];
+      pd = sb.x;
+      pg = sb.y;
+      cont = sb.z;
     }
     if (cmpf(pd) == 0 && cmpf(pg) == 0) {
       psi(B.ls, p, PS_VCOUNT) = 0;  // its only vertex (slot 0)
@@ -440,7 +439,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_vcm_camera_gen(Vc
   const VcmArgs& X = G_.a[blockIdx.y];
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < X.a.P; s += gridDim.x * blockDim.x) {
     const int p = camera_gen_one(X.a, s);
-    X.V.c_dvm[p] = 0.f;
+    psf(X.a.B.cs, p, PS_DVM) = 0.f;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) X.a.sc->ext[kCamSlot] = X.a.P;
 }
@@ -483,7 +482,7 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
           pix = psi(B.cs, p, PS_PIX);
           dvcm = psf(B.cs, p, PS_DVCM);
           dvc = psf(B.cs, p, PS_DVC);
-          dvm = V.c_dvm[p];
+          dvm = psf(B.cs, p, PS_DVM);
           len = psi(B.cs, p, PS_LEN);
           thr = ld3r(B.cs, p, PS_THR);
           dvcm *= (t * t);  // (:190-193)
@@ -551,7 +550,7 @@ __device__ __forceinline__ void vcm_camera_shade_body(const VcmArgs& X, int slot
               st3r(B.cs, p, PS_THR, thr);
               psf(B.cs, p, PS_DVCM) = dvcm;
               psf(B.cs, p, PS_DVC) = dvc;
-              V.c_dvm[p] = dvm;
+              psf(B.cs, p, PS_DVM) = dvm;
               psi(B.cs, p, PS_LEN) = len + 1;
             }
             psu(B.cs, p, PS_CTR) = rng.ctr;
