@@ -511,6 +511,10 @@ void build_fast(const wr::Scene& s, FastHost& out) {
     return;
   }
   const size_t n = s.prims.size();
+  if (n >= (size_t(1) << 30)) {  // the search marks near-ties in bit 30 of a primitive index (wr_fast.h)
+    out.why = "2^30 primitives or more";
+    return;
+  }
   std::vector<Box> box(n);
   std::vector<float> cen(3 * n);
   std::vector<int> tri_prim(n), idx(n);

@@ -891,6 +891,11 @@ __device__ __forceinline__ auto qfield(const TraceQueues& Q, int q, Fn field) {
   return v;
 }
 
+// the search's near-tie mark on a hit primitive (queue out_prim, between the
+// search and k_fast_resolve, which clears it; scenes have < 2^30 primitives)
+constexpr int kTieMark = 1 << 30;
+__device__ __forceinline__ int unmark(int p) { return p >= 0 ? (p & ~kTieMark) : p; }
+
 template <bool COUNT>
 __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, int* fetch,
                                            float* t2buf, int2* spill, uint32_t* lds, FastCounters& ctr,
@@ -1173,9 +1178,16 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         ctr.max_tests = max(ctr.max_tests, rt);
         ctr.long_rays += rn > 256u ? 1u : 0u;
       }
+      // a near-tie (t2 within EPS of t1: the reference's first-found rule may
+      // pick another hit) travels as a mark on p1 instead of t2 itself -- 4
+      // bytes per ray less written here and read by k_fast_resolve.  The
+      // diagnostic probes (F.diag) keep t2, as they may skip the kernels that
+      // clear the mark.
+      int po = p1;
+      if (F.diag) t2buf[lidx] = t2;
+      else if (p1 >= 0 && !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0)) po = p1 | kTieMark;
       qfield(Q, qi, [](const RayQueue& x) { return x.out_t; })[r] = p1 >= 0 ? t1 : WR_INF;
-      qfield(Q, qi, [](const RayQueue& x) { return x.out_prim; })[r] = p1;
-      t2buf[lidx] = t2;
+      qfield(Q, qi, [](const RayQueue& x) { return x.out_prim; })[r] = po;
       r = -1;
     }
   }
@@ -1235,9 +1247,10 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
     if (idx < QI.n) {
       QI.locate(idx, q, r);
       // every load that does not depend on p1 in flight at once
-      p1 = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r];
+      const int pm = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r];
+      p1 = unmark(pm);
       t1 = qfield(Q, q, [](const RayQueue& x) { return x.out_t; })[r];
-      const float t2 = t2buf[idx];
+      const float t2 = F.diag ? t2buf[idx] : 0.f;
       const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
       const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
       const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
@@ -1255,7 +1268,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
         need = true;
         walk = true;
       } else if (p1 >= 0) {  // (no hit anywhere: a miss for the reference too)
-        const bool tie = !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0);
+        const bool tie = F.diag ? !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0) : (pm & kTieMark) != 0;
         if (tie) {
           // a tie on a many-leaf primitive (walls, floors: up to thousands of
           // leaves) is resolved by one wave (scan list, marked), the others
@@ -1424,7 +1437,7 @@ __device__ __forceinline__ ListedRay listed_ray(const TraceQueues& Q, const Queu
   L.outp = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; });
   L.outt = qfield(Q, q, [](const RayQueue& x) { return x.out_t; });
   L.t1 = L.outt[r];
-  L.p1 = L.outp[r];
+  L.p1 = unmark(L.outp[r]);
   const float* o3 = qfield(Q, q, [](const RayQueue& x) { return x.o3; });
   const float* d3 = qfield(Q, q, [](const RayQueue& x) { return x.d3; });
   const int cap = qfield(Q, q, [](const RayQueue& x) { return x.cap; });
