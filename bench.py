@@ -409,7 +409,7 @@ def main():
         if trace == "bvh":
             out["trace_note"] = ("verified BVH traversal: every ray gets the reference KD walk's (t, primitive) "
                                  "answer, bit for bit (argument in DESIGN.md 4b, one near-grazing case open; 0 mismatches over "
-                                 "the full bench workloads, 3.75e9 rays, profiles/r3/bvh_verify.json); the same rays are "
+                                 "2.2e10 rays of the bench workloads, profiles/r3/bvh_verify*.json); the same rays are "
                                  "traced and counted")
         if other:
             out["other_trace"] = other

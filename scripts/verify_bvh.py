@@ -4,7 +4,7 @@ every ray of the renders is traced twice -- the BVH mode's answer, then the
 reference's KD walk (k_fast_verify, WR_BVH_VERIFY=1) -- and the (t, primitive)
 pairs are compared bit for bit.  Writes one JSON line per configuration.
 
-    python scripts/verify_bvh.py [--configs c2,vcm,c3,c4] [--iters 256,64,64,16] [--out FILE]
+    python scripts/verify_bvh.py [--configs c2,vcm,c3,c4] [--iters 256,64,64,16] [--seed S] [--out FILE]
 """
 import argparse
 import json
@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--configs", default="c2,vcm,c3,c4")
     ap.add_argument("--iters", default="256,64,64,16")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--seed", type=int, default=5489, help="another seed traces another ray set")
     a = ap.parse_args()
     W, H = 1920, 1080
     tmp = tempfile.mkdtemp(prefix="wr_verify_")
@@ -38,14 +39,14 @@ def main():
         t0 = time.perf_counter()
         integ = bench.CONFIGS[cfg]["integrator"]
         if integ == "pt":
-            _, st = ctx.render_path(W, H, spp=512, max_depth=7, seed=5489, sample_begin=0, sample_count=k)
+            _, st = ctx.render_path(W, H, spp=512, max_depth=7, seed=a.seed, sample_begin=0, sample_count=k)
         elif integ == "vcm":
-            _, st = ctx.render_vcm(W, H, iterations=k, seed=5489)
+            _, st = ctx.render_vcm(W, H, iterations=k, seed=a.seed)
         else:
-            _, st = ctx.render_bdpt(W, H, iterations=k, seed=5489)
+            _, st = ctx.render_bdpt(W, H, iterations=k, seed=a.seed)
         rays = st.closest_rays + st.shadow_rays
         d = {"config": cfg, "workload": f"{bench.CONFIGS[cfg]['desc']} {W}x{H}, {k} "
-             f"{'samples' if integ == 'pt' else 'iterations'}, seed 5489",
+             f"{'samples' if integ == 'pt' else 'iterations'}, seed {a.seed}",
              "rays": int(rays), "verified_rays": int(st.verify_rays), "mismatches": int(st.verify_mismatches),
              "seconds": round(time.perf_counter() - t0, 1)}
         assert st.verify_rays == rays, (st.verify_rays, rays)
