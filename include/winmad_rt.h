@@ -174,6 +174,10 @@ int wr_scene_load(const char* scene_path, wr_scene** out);
  * null arrays, bad type, an emitter matId without its light). */
 int wr_scene_from_desc(const wr_scene_desc* desc, wr_scene** out);
 int wr_scene_info_get(const wr_scene* scene, wr_scene_info* out);
+/* 64-bit FNV-1a of what a render reads from the scene (primitives, lights,
+ * materials, camera).  Checkpoints store it (with the integrator's settings)
+ * so that a film is never resumed into a render of another scene. */
+int wr_scene_fingerprint(const wr_scene* scene, uint64_t* out);
 /* Text dump in the format of oracle/ref_driver.cpp `scene` (parity tests). */
 int wr_scene_dump(const wr_scene* scene, const char* out_path);
 void wr_scene_free(wr_scene* scene);
@@ -215,7 +219,9 @@ int wr_film_reduce(wr_context* ctx, float* film_dev, int64_t nfloat, int root);
  * ~5 GB per pair of iterations at 1080p): iterations / samples are dealt
  * round-robin to them so that one stream's late-bounce traversal tail overlaps
  * another's full launches.  1..16; default = the process's hardware queues
- * (GPU_MAX_HW_QUEUES, HIP default 4) up to 16, or env WR_PIPES.
+ * (GPU_MAX_HW_QUEUES) up to 16, or env WR_PIPES.  Loading the library raises
+ * GPU_MAX_HW_QUEUES to 16 (unless set higher, or env WR_HW_QUEUES=n asks for n):
+ * effective when the library loads before the process's first HIP call.
  * GPU-specific scheduling; no reference counterpart. */
 int wr_set_pipelines(wr_context* ctx, int n);
 
@@ -229,14 +235,15 @@ enum { WR_INTEGRATOR_BDPT = 0, WR_INTEGRATOR_VCM = 1, WR_INTEGRATOR_PATH = 2 };
 int wr_reserve(wr_context* ctx, int integrator, int32_t width, int32_t height);
 
 /* Traversal mode of every later call on the context.
- *   WR_TRACE_REFERENCE (default): the reference's KD tree, walked exactly as
+ *   WR_TRACE_REFERENCE: the reference's KD tree, walked exactly as
  *     KDtreeAccel::traverse (scene/KDtreeAccel.cpp:309-388) walks it.
- *   WR_TRACE_BVH: a BVH search for the smallest hit, accepted only when the
- *     winner is provably the reference's (unique within EPS, and in a KD leaf
- *     the reference's traversal reaches); every other ray is traced in the
+ *   WR_TRACE_BVH (default for scenes of triangles only): a BVH search for the
+ *     smallest hit, accepted only when the winner is provably the reference's
+ *     (unique within EPS, in a KD leaf the reference's traversal reaches, the
+ *     ray not grazing the winner's plane); every other ray is traced in the
  *     reference mode.  Same rays, same (t, primitive) answers; see DESIGN.md 4b.
- * Env WR_TRACE_BVH=1 selects the BVH mode at wr_create.  WR_E_SCENE if the
- * scene cannot use it (spheres). */
+ * Scenes with spheres always use WR_TRACE_REFERENCE (WR_E_SCENE if asked for
+ * the BVH).  Env WR_TRACE_BVH=0 / 1 sets the mode at wr_create. */
 enum { WR_TRACE_REFERENCE = 0, WR_TRACE_BVH = 1 };
 int wr_set_trace_mode(wr_context* ctx, int mode);
 
@@ -308,7 +315,10 @@ typedef struct {
   int32_t kind;         /* WR_CKPT_*                                         */
   int32_t done, total;  /* iterations (samples) summed in the film / wanted */
   uint32_t seed;
-  int32_t reserved[2];
+  uint32_t fingerprint[2]; /* (lo, hi) of a 64-bit hash of the scene
+                              (wr_scene_fingerprint) and the integrator's
+                              settings, set by the writer; a resume whose
+                              own hash differs is refused (0 = not recorded) */
 } wr_checkpoint_info; /* 32 bytes */
 int wr_checkpoint_save(const char* path, const wr_checkpoint_info* info, const float* film);
 /* film == NULL reads the header only; else film_floats must be height*width*3.

@@ -47,7 +47,10 @@ def normalize_f32(d):
                                         ("cbox64x48", lambda: _scenes.cbox(64, 48)),
                                         ("spheres64", lambda: _scenes.spheres(64, 64))])
 def test_trace_closest_bit_exact_vs_reference(name, maker):
+    """The reference's own outputs: the library default (verified BVH on
+    triangle scenes) and the KD walk, forced."""
     _check_golden_corpus(ctx(maker()), name)
+    _check_golden_corpus(native.Context(native.Scene(maker()), 0, trace=native.TRACE_REFERENCE), name)
 
 
 @pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),
@@ -57,7 +60,7 @@ def test_trace_dense_variant_bit_exact_vs_reference(name, maker, monkeypatch):
     """TRACE_DENSE (PT's launches: owner rays by ds_bpermute, 20 waves/CU),
     forced on the API: the reference's corpus, closest hits and occlusion."""
     monkeypatch.setenv("WR_TRACE_DENSE", "1")
-    _check_golden_corpus(native.Context(native.Scene(maker()), 0), name)
+    _check_golden_corpus(native.Context(native.Scene(maker()), 0, trace=native.TRACE_REFERENCE), name)
 
 
 def _check_golden_corpus(c, name):
@@ -315,7 +318,7 @@ def test_trace_wide_stack_variant_bit_exact(monkeypatch):
     monkeypatch.setenv("WR_TRACE_WIDE", "1")
     path = _scenes.torus(64, 64)
     s = native.Scene(path)
-    c = native.Context(s, 0)
+    c = native.Context(s, 0, trace=native.TRACE_REFERENCE)
     rays = np.fromfile(os.path.join(GOLD, f"rays_torus64.f32"), np.float32).reshape(-1, 9)
     assert _check_trace_vs_oracle(c, _oracle.Scene(path), rays) > 500
 
@@ -328,7 +331,7 @@ def test_trace_1m_triangle_scene_matches_oracle(tmp_path, monkeypatch):
     path = scenes.write(str(tmp_path / "torus_1m.scene"), scenes.torus_scene(64, 64, torus_obj=obj))
     s = native.Scene(path)
     assert s.info()["kd_inner"] + s.info()["kd_leaves"] > 65536
-    c = native.Context(s, 0)
+    c = native.Context(s, 0, trace=native.TRACE_REFERENCE)
     rng = np.random.default_rng(42)
     n = 4096
     o = rng.uniform([-250, -150, -120], [280, 350, 90], size=(n, 3))
@@ -337,8 +340,9 @@ def test_trace_1m_triangle_scene_matches_oracle(tmp_path, monkeypatch):
     rays[:, 0:3], rays[:, 3:6] = o, d
     orc = _oracle.Scene(path)
     assert _check_trace_vs_oracle(c, orc, rays) > n // 4
+    assert _check_trace_vs_oracle(native.Context(s, 0), orc, rays) > n // 4  # library default (BVH)
     monkeypatch.setenv("WR_TRACE_DENSE", "1")  # wide stack + TRACE_DENSE
-    assert _check_trace_vs_oracle(native.Context(s, 0), orc, rays) > n // 4
+    assert _check_trace_vs_oracle(native.Context(s, 0, trace=native.TRACE_REFERENCE), orc, rays) > n // 4
 
 
 def test_trace_large_batch_matches_oracle_and_small_batches():
@@ -421,6 +425,34 @@ def test_bdpt_pieces_render_like_whole_iterations(W, H, monkeypatch):
     assert np.allclose(got, ref, rtol=1e-4, atol=1e-6)
     assert np.allclose(one, ref1, rtol=1e-4, atol=1e-6)
     orc, ost = _oracle.Scene(path).bdpt(W, H, 3, 21, mode=1)
+    assert_film_parity(got, orc)
+    assert_ray_counts(gs, ost)
+
+
+@pytest.mark.parametrize("W,H,cap,pipes", [(100, 60, 3000, 1), (100, 60, 1000, 2), (99, 61, 2049, 1)])
+def test_bdpt_pieces_never_exceed_the_buffer_capacity(W, H, cap, pipes, monkeypatch):
+    """A film whose sides are not multiples of 8 (64-path units) with a
+    WR_PIECE_CAP that is not a multiple of 64: the iteration's last piece ends
+    at the iteration's end, not on a unit, and must still fit the buffer set
+    (cut_pieces counts whole units per piece).  Same rays and film as whole
+    iterations on one pipeline, and the oracle's film."""
+    path = _scenes.torus(W, H)
+    s = native.Scene(path)
+    monkeypatch.setenv("WR_PIECE_MIN", "64")
+    monkeypatch.setenv("WR_PIECE_CAP", str(cap))
+    cut = native.Context(s, 0)
+    cut.set_pipelines(pipes)
+    got, gs = cut.render_bdpt(W, H, iterations=2, seed=33)
+    cut.close()
+    monkeypatch.setenv("WR_PIECE_MIN", str(1 << 30))
+    monkeypatch.setenv("WR_PIECE_CAP", str(1 << 21))
+    whole = native.Context(s, 0)
+    whole.set_pipelines(1)
+    ref, rs = whole.render_bdpt(W, H, iterations=2, seed=33)
+    whole.close()
+    assert gs.closest_rays == rs.closest_rays and gs.shadow_rays == rs.shadow_rays
+    assert np.allclose(got, ref, rtol=1e-4, atol=1e-6)
+    orc, ost = _oracle.Scene(path).bdpt(W, H, 2, 33, mode=1)
     assert_film_parity(got, orc)
     assert_ray_counts(gs, ost)
 

@@ -141,6 +141,12 @@ def test_cli_checkpoint_resume_and_devices(mode, tmp_path):
     assert "stopped" in stop and ck.exists() and not (tmp_path / "part.pfm").exists()
     _, info = native.checkpoint_load(str(ck))
     assert info["done"] == 4 and info["total"] == 6
+    assert info["fingerprint"] != 0
+    # a checkpoint of another scene (same film size, kind, total, seed) is refused
+    other = _scenes.cbox(W, H) if mode == "-bpt" else _scenes.torus(W, H, "pt")
+    r = subprocess.run([os.path.join(native.PKG_DIR, "wr_tot"), *map(str, [other, tmp_path / "x.pfm", *base[2:],
+                        "--checkpoint", ck])], capture_output=True, text=True, cwd=tmp_path, timeout=300)
+    assert r.returncode != 0 and "another scene" in r.stderr, (r.returncode, r.stderr)
     _tot([base[0], tmp_path / "resumed.pfm", *base[2:], "--checkpoint", ck, "--checkpoint-every", 2], tmp_path)
     assert np.allclose(_pfm(tmp_path / "resumed.pfm"), _pfm(tmp_path / "full.pfm"), rtol=1e-4, atol=1e-6)
     two = _tot([base[0], tmp_path / "two.pfm", *base[2:], "--devices", "0,0", "--trace", "reference"], tmp_path)

@@ -32,9 +32,8 @@ def pair(path):
     """(reference-mode context, BVH-mode context) on one scene."""
     if path not in _cache:
         s = native.Scene(path)
-        a = native.Context(s, 0)
-        b = native.Context(s, 0)
-        b.set_trace_mode(native.TRACE_BVH)
+        a = native.Context(s, 0, trace=native.TRACE_REFERENCE)
+        b = native.Context(s, 0, trace=native.TRACE_BVH)
         _cache[path] = (s, a, b)
     return _cache[path][1], _cache[path][2]
 
@@ -63,7 +62,16 @@ def test_bvh_mode_refused_with_spheres():
 
 
 def _unit(v):
-    return normalize_f32(v.astype(np.float32))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return normalize_f32(v.astype(np.float32))
+
+
+def _valid(o, d):
+    """Rays with finite origins and unit directions only (a zero-length
+    direction normalises to NaN; neither mode is asked about such rays)."""
+    ok = np.isfinite(o).all(axis=1) & np.isfinite(d).all(axis=1)
+    ok &= np.abs(np.sqrt((d.astype(np.float64) ** 2).sum(axis=1)) - 1.0) < 1e-3
+    return ok
 
 
 def _corpus(ref, n, seed):
@@ -94,8 +102,8 @@ def _corpus(ref, n, seed):
     # shadow rays: hit point -> another hit point, no offset (BDPT connections)
     q = p[rng.permutation(m)]
     sd = _unit(q - p)
-    ok = np.isfinite(sd).all(axis=1)
-    rays = [native.rays_from_arrays(o0, d0), native.rays_from_arrays(ext_o, dd),
+    ok0, oke, ok = _valid(o0, d0), _valid(ext_o, dd), _valid(p, sd)
+    rays = [native.rays_from_arrays(o0[ok0], d0[ok0]), native.rays_from_arrays(ext_o[oke], dd[oke]),
             native.rays_from_arrays(p[ok], sd[ok])]
     return np.concatenate(rays), (p[ok], sd[ok], q[ok])
 
@@ -228,3 +236,63 @@ def test_deferred_hard_rays_render_the_same_film(name, maker, W, H, its, monkeyp
     assert st.deferred_rays > 0
     assert st.verify_rays == st.closest_rays + st.shadow_rays
     assert st.verify_mismatches == 0, (st.verify_mismatches, st.verify_rays)
+
+
+def _plane_grazing_rays(ref, n, seed):
+    """Rays that run along the plane of the surface they leave (DESIGN.md 4b,
+    the near-grazing case of the margins argument): from hit points on every
+    surface, directions in the surface's plane tilted out of it by log-uniform
+    angles in [1e-8, 3e-3] rad either way, from the hit point itself and from
+    points lifted off the plane by log-uniform 1e-7..1e-3 of the scene's size.
+    On flat walls and floors every coplanar neighbour's plane is grazed too.
+
+    Hit points come from random rays whose origins fill the box spanned by a
+    first sample of hits, so a closed scene (the Cornell box, seen from inside)
+    yields its quota as well as an open one."""
+    rng = np.random.default_rng(seed)
+    o = (rng.uniform(-1, 1, (4 * n, 3)) * np.repeat([2000.0, 400.0, 60.0, 3.0], n)[:, None]).astype(np.float32)
+    h = ref.trace_closest(native.rays_from_arrays(o, _unit(rng.normal(size=(4 * n, 3)))))
+    first = h["p"][h["prim"] >= 0].astype(np.float64)
+    assert first.shape[0] > 100, "no hits from the first sample"
+    lo, hi = first.min(axis=0), first.max(axis=0)
+    pad = 0.05 * (hi - lo)
+    ps, ns = [], []
+    got = 0
+    for _ in range(32):
+        o = rng.uniform(lo - pad, hi + pad, (n, 3)).astype(np.float32)
+        h = ref.trace_closest(native.rays_from_arrays(o, _unit(rng.normal(size=(n, 3)))))
+        hit = h["prim"] >= 0
+        ps.append(h["p"][hit].astype(np.float64))
+        ns.append(h["n"][hit].astype(np.float64))
+        got += int(hit.sum())
+        if got >= n:
+            break
+    p, nn = np.concatenate(ps)[:n], np.concatenate(ns)[:n]
+    m = p.shape[0]
+    scale = float(np.abs(p).max())
+    u = np.cross(nn, rng.normal(size=(m, 3)))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+    ang = 10.0 ** rng.uniform(-8, np.log10(3e-3), m) * np.where(rng.random(m) < 0.5, 1.0, -1.0)
+    dd = _unit(u * np.cos(ang)[:, None] + nn * np.sin(ang)[:, None])
+    lift = np.where(rng.random(m) < 0.5, 0.0, 10.0 ** rng.uniform(-7, -3, m) * scale)
+    lift *= np.where(rng.random(m) < 0.5, 1.0, -1.0)
+    oo = (p + nn * lift[:, None]).astype(np.float32)
+    ok = _valid(oo, dd)
+    return native.rays_from_arrays(oo[ok], dd[ok])
+
+
+@pytest.mark.parametrize("name,maker", SCENES + [("torus1m", lambda: big_torus(64, 64))])
+def test_bvh_matches_reference_mode_on_plane_grazing_rays(name, maker):
+    """The targeted probe of DESIGN.md 4b's near-grazing case: BVH mode vs the
+    reference's KD walk, (t, primitive) bit for bit, on rays grazing the plane
+    of the surface they leave (and of its coplanar neighbours)."""
+    ref, fast = pair(maker())
+    n = 600_000 if name != "torus1m" else 200_000
+    rays = _plane_grazing_rays(ref, n, 99)
+    assert rays.shape[0] >= 0.9 * n, (name, rays.shape[0], n)
+    a = ref.trace_closest(rays)
+    b = fast.trace_closest(rays)
+    ok = _same_hits(a, b)
+    print(name, rays.shape[0], "rays,", int((a["prim"] >= 0).sum()), "hits,", int((~ok).sum()), "mismatches")
+    assert ok.all(), (name, int((~ok).sum()), rays.shape[0], np.nonzero(~ok)[0][:8])

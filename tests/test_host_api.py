@@ -83,10 +83,11 @@ def test_checkpoint_round_trip_and_corruption(tmp_path):
     rng = np.random.default_rng(3)
     film = rng.random((6, 10, 3), dtype=np.float32)
     p = str(tmp_path / "ck.bin")
-    native.checkpoint_save(p, film, native.CKPT_BDPT, 3, 8, 5489)
+    native.checkpoint_save(p, film, native.CKPT_BDPT, 3, 8, 5489, fingerprint=0x0123456789ABCDEF)
     got, info = native.checkpoint_load(p)
     assert np.array_equal(got, film)
-    assert info == {"width": 10, "height": 6, "kind": native.CKPT_BDPT, "done": 3, "total": 8, "seed": 5489}
+    assert info == {"width": 10, "height": 6, "kind": native.CKPT_BDPT, "done": 3, "total": 8, "seed": 5489,
+                    "fingerprint": 0x0123456789ABCDEF}
     assert not os.path.exists(p + ".tmp")
     raw = bytearray(open(p, "rb").read())
     raw[-5] ^= 0x40  # one flipped bit in the film
@@ -102,3 +103,13 @@ def test_checkpoint_round_trip_and_corruption(tmp_path):
     with pytest.raises(native.WrError) as e:  # done > total
         native.checkpoint_save(p, film, native.CKPT_BDPT, 9, 8, 1)
     assert e.value.code == native.WR_E_ARG
+
+
+def test_scene_fingerprint_tells_scenes_apart(tmp_path):
+    """wr_scene_fingerprint (what a checkpoint is bound to): equal for the same
+    scene loaded twice, different for another scene, another camera or
+    another material."""
+    a = native.Scene(_scenes.torus(64, 64)).fingerprint()
+    assert a == native.Scene(_scenes.torus(64, 64)).fingerprint() != 0
+    assert a != native.Scene(_scenes.cbox(64, 64)).fingerprint()
+    assert a != native.Scene(_scenes.torus(64, 48)).fingerprint()  # camera resolution

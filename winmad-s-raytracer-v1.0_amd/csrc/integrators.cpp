@@ -50,11 +50,28 @@ void SurfaceIntegrator::setTraceMode(int mode) {
 
 void SurfaceIntegrator::reserve() { ok(wr_reserve(ctx_, integrator_, width, height)); }
 
+// FNV-1a 64 of the scene's fingerprint and the integrator's settings: what a
+// resumed film must have been rendered with, beyond the header's size, kind,
+// total and seed
+uint64_t SurfaceIntegrator::settingsHash(const std::vector<double>& settings) const {
+  uint64_t scene = 0;
+  ok(wr_scene_fingerprint(scene_, &scene));
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  };
+  mix(&scene, sizeof scene);
+  for (double v : settings) mix(&v, sizeof v);
+  return h ? h : 1;  // 0 means "not recorded"
+}
+
 template <class Batch>
-void SurfaceIntegrator::batched(int kind, int total, uint32_t seed, Batch batch) {
+void SurfaceIntegrator::batched(int kind, int total, uint32_t seed, const std::vector<double>& settings, Batch batch) {
   int done = 0;
   stopped = false;
-  wr_checkpoint_info want{width, height, kind, 0, total, seed, {0, 0}};
+  const uint64_t fp = settingsHash(settings);
+  wr_checkpoint_info want{width, height, kind, 0, total, seed, {uint32_t(fp), uint32_t(fp >> 32)}};
   if (!checkpointPath.empty()) {
     wr_checkpoint_info have{};
     if (FILE* f = std::fopen(checkpointPath.c_str(), "rb")) {  // resume
@@ -63,6 +80,9 @@ void SurfaceIntegrator::batched(int kind, int total, uint32_t seed, Batch batch)
       if (have.width != width || have.height != height || have.kind != kind || have.total != total ||
           have.seed != seed)
         throw std::runtime_error("checkpoint " + checkpointPath + " belongs to another render");
+      if (have.fingerprint[0] != want.fingerprint[0] || have.fingerprint[1] != want.fingerprint[1])
+        throw std::runtime_error("checkpoint " + checkpointPath +
+                                 " was rendered from another scene or with other integrator settings");
       ok(wr_checkpoint_load(checkpointPath.c_str(), &have, film.data(), static_cast<int64_t>(film.size())));
       done = have.done;
     }
@@ -93,7 +113,7 @@ void BidirPathTracing::init(const char* filename, Parameters& para) {
 }
 
 void BidirPathTracing::render() {
-  batched(WR_CKPT_BDPT, iterations, seed, [&](int begin, int count) {  // :25-26
+  batched(WR_CKPT_BDPT, iterations, seed, {double(maxPathLength), double(controlLength)}, [&](int begin, int count) {  // :25-26
     wr_bdpt_params p{};
     p.width = width;
     p.height = height;
@@ -122,7 +142,7 @@ void VertexCM::init(const char* filename, Parameters& para) {
 }
 
 void VertexCM::render() {
-  batched(WR_CKPT_VCM, iterations, seed, [&](int begin, int count) {
+  batched(WR_CKPT_VCM, iterations, seed, {double(minPathLength), double(maxPathLength), double(baseRadiusFactor), double(radiusAlpha)}, [&](int begin, int count) {
     wr_vcm_params p{};
     p.width = width;
     p.height = height;
@@ -154,7 +174,7 @@ void PathIntegrator::init(const char* filename, Parameters& para) {
 }
 
 void PathIntegrator::render() {
-  batched(WR_CKPT_PT, samplesPerPixel, seed, [&](int begin, int count) {
+  batched(WR_CKPT_PT, samplesPerPixel, seed, {double(maxTracingDepth), double(samplesOfLight), double(samplesOfHemisphere)}, [&](int begin, int count) {
     wr_path_params p{};
     p.width = width;
     p.height = height;

@@ -29,7 +29,7 @@ class SurfaceIntegrator {
   int width = 0, height = 0, samplesPerPixel = 0;
   int device = 0;
   std::vector<int> devices;  // more than one: the GPUs of this node share the render (wr_create_multi)
-  int traceMode = -1;        // -1: the library's default (WR_TRACE_REFERENCE); WR_TRACE_REFERENCE / WR_TRACE_BVH
+  int traceMode = -1;        // -1: the library's default (WR_TRACE_BVH for triangle scenes); WR_TRACE_REFERENCE / WR_TRACE_BVH
   // Film checkpoint (the reference keeps the film in memory only,
   // bidirPathTracing.cpp:23-27): with a path set, render() resumes from a
   // matching checkpoint and saves one every checkpointEvery iterations
@@ -59,7 +59,10 @@ class SurfaceIntegrator {
   // the render loop in batches: renders [done, total) through batch(begin, count),
   // resuming from / saving checkpoints of `kind`
   template <class Batch>
-  void batched(int kind, int total, uint32_t seed, Batch batch);
+  void batched(int kind, int total, uint32_t seed, const std::vector<double>& settings, Batch batch);
+  // hash of the scene (wr_scene_fingerprint) and `settings`: stored in the
+  // checkpoint, a resume with another scene or settings is refused
+  uint64_t settingsHash(const std::vector<double>& settings) const;
 };
 
 // src/surfaceIntegrator/bidirPathTracing.{h,cpp}

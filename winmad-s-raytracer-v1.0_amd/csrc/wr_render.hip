@@ -39,6 +39,45 @@ using namespace wrd;
 
 // =============================================================== errors
 static int fail(int code, const std::string& msg) { return wr::set_error(code, msg); }
+// Load-time set-up: one hardware queue per render pipeline.  HIP gives a
+// process GPU_MAX_HW_QUEUES queues (default 4; the GPU box exports 4), and
+// pipelines beyond them share a queue and serialize (concurrent
+// pipelines).  When the library is loaded before the process's first HIP call
+// -- a C++ program linked to it, like the reference's main.cpp with the
+// SurfaceIntegrator mirror -- this raises the variable to 16
+// so that the library default is the measured configuration.  A plain setenv
+// before HIP initialises (never a re-exec).  WR_HW_QUEUES=n sets exactly n
+// instead (e.g. 4 keeps HIP's default); a larger GPU_MAX_HW_QUEUES is kept.
+// When HIP is already initialised (a Python process that touched the GPU
+// first) the variable no longer matters to HIP, and wr_create sizes the
+// pipelines by what HIP saw: see hwq_at_load below.
+static int g_hwq_at_load = 0;  // GPU_MAX_HW_QUEUES as the library found it (0 = unset)
+__attribute__((constructor)) static void wr_raise_hw_queues() {
+  const char* cur = std::getenv("GPU_MAX_HW_QUEUES");
+  g_hwq_at_load = cur ? std::atoi(cur) : 0;
+  if (const char* w = std::getenv("WR_HW_QUEUES")) {
+    const int n = std::atoi(w);
+    if (n > 0) setenv("GPU_MAX_HW_QUEUES", std::to_string(std::min(n, 32)).c_str(), 1);
+    return;
+  }
+  if (!cur || std::atoi(cur) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+}
+
+// Every C-ABI entry that selects a device (hipSetDevice) leaves the caller's
+// current device as it found it: a multi-device render or reduce ends on its
+// last device otherwise, and a PyTorch caller's next default-device work would
+// run there.
+struct DeviceGuard {
+  int dev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  ~DeviceGuard() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
 #define HIPCHK(expr)                                                                          \
   do {                                                                                        \
     hipError_t e_ = (expr);                                                                   \
@@ -1052,15 +1091,21 @@ int64_t flat_round(int64_t f, int P, int unit) {
   return it * P + std::min<int64_t>(P, (off + unit / 2) / unit * unit);
 }
 // [a, b) cut at iteration ends and into near-equal unit-aligned pieces of at
-// most cap paths
+// most cap paths.  The stretch is counted in units (the last one may be
+// partial: an iteration's end need not be unit-aligned) and each piece gets
+// at most floor(cap / unit) of them, so no piece exceeds cap even when the
+// stretch is not a multiple of the unit (cap is a whole number of units, or
+// the frame itself).
 void cut_pieces(int64_t a, int64_t b, int P, int unit, int cap, std::vector<Piece>& out) {
+  const int64_t cap_units = std::max<int64_t>(1, cap / unit);
   while (a < b) {
     const int64_t it = a / P, off = a % P;
     const int64_t len = std::min<int64_t>(b - a, P - off);  // up to the iteration's end
-    const int64_t cuts = (len + cap - 1) / cap;
+    const int64_t units = (len + unit - 1) / unit;
+    const int64_t cuts = (units + cap_units - 1) / cap_units;
     for (int64_t j = 0; j < cuts; ++j) {
-      int64_t lo = off + (len * j / cuts) / unit * unit, hi = off + (len * (j + 1) / cuts) / unit * unit;
-      if (j == cuts - 1) hi = off + len;
+      const int64_t lo = off + std::min(len, units * j / cuts * unit);
+      const int64_t hi = off + std::min(len, units * (j + 1) / cuts * unit);
       if (hi > lo) out.push_back(Piece{static_cast<int>(it), static_cast<int>(lo), static_cast<int>(hi - lo)});
     }
     a += len;
@@ -1320,6 +1365,12 @@ int wr_scene_info_get(const wr_scene* sc, wr_scene_info* o) {
   return WR_OK;
 }
 
+int wr_scene_fingerprint(const wr_scene* sc, uint64_t* out) {
+  if (!sc || !out) return fail(WR_E_ARG, "null argument");
+  *out = wr::scene_fingerprint(sc->s);
+  return WR_OK;
+}
+
 int wr_scene_dump(const wr_scene* sc, const char* path) {
   if (!sc || !path) return fail(WR_E_ARG, "null argument");
   std::string txt = wr::dump_scene(sc->s);
@@ -1342,6 +1393,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   if (!sc || !out) return fail(WR_E_ARG, "null argument");
   *out = nullptr;
   if (int rc = check_device()) return rc;
+  DeviceGuard dg;
   const wr::Scene& s = sc->s;
   if (s.prims.empty()) return fail(WR_E_SCENE, "scene has no primitives");
   for (const auto& p : s.prims)  // the reference would index materials[] out of range
@@ -1693,6 +1745,9 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       // diagnostic: WR_FAST_WAVES_PER_CU caps the search's resident waves
       if (const char* e = std::getenv("WR_FAST_WAVES_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
       c->fast_blocks = c->cus * per_cu;
+      // the verified BVH is the default traversal of triangle scenes (same
+      // answers as the KD walk); WR_TRACE_BVH=0 selects the walk
+      c->fast_on = true;
       if (const char* e = std::getenv("WR_TRACE_BVH")) c->fast_on = std::atoi(e) != 0;
       if (const char* e = std::getenv("WR_BVH_DIAG")) fs.diag = std::atoi(e);
       if (const char* e = std::getenv("WR_BVH_VERIFY")) c->verify = std::atoi(e) != 0;
@@ -1722,6 +1777,7 @@ int wr_set_pipelines(wr_context* c, int n) {
 
 void wr_destroy(wr_context* c) {
   if (!c) return;
+  DeviceGuard dg;
   for (wr_context* d : c->subs) wr_destroy(d);
   c->subs.clear();
   for (ncclComm_t m : c->dev_comms) (void)rccl().destroy(m);
@@ -1867,12 +1923,14 @@ static int trace_multi(wr_context* c, const wr_ray* rays, const float* targets, 
 int wr_trace_closest(wr_context* c, const wr_ray* rays, int64_t n, wr_hit* hits) {
   if (!hits && n) return fail(WR_E_ARG, "null hits");
   if (!c || (!rays && n) || n < 0) return fail(WR_E_ARG, "bad argument");
+  DeviceGuard dg;
   return trace_multi(c, rays, nullptr, n, hits, nullptr);
 }
 
 int wr_occluded(wr_context* c, const wr_ray* rays, const float* targets, int64_t n, uint8_t* occluded) {
   if ((!targets || !occluded) && n) return fail(WR_E_ARG, "null targets / output");
   if (!c || (!rays && n) || n < 0) return fail(WR_E_ARG, "bad argument");
+  DeviceGuard dg;
   return trace_multi(c, rays, targets, n, nullptr, occluded);
 }
 
@@ -1918,20 +1976,25 @@ static int issue_round(wr_context* c, int live, int nsteps, Fn&& fn, int np) {
   };
   if (T <= 1) return run(0);
   std::vector<int> rcs(T, WR_OK);
+  std::vector<std::string> msg(T);  // wr_last_error is thread-local: carry it over
   std::vector<std::thread> th;
   th.reserve(T - 1);
   for (int t = 1; t < T; ++t)
     th.emplace_back([&, t] {
-      if (hipSetDevice(c->device) != hipSuccess) {
+      const hipError_t e = hipSetDevice(c->device);
+      if (e != hipSuccess) {
         rcs[t] = WR_E_HIP;
+        msg[t] = std::string("issue thread hipSetDevice: ") + hipGetErrorString(e);
         return;
       }
       rcs[t] = run(t);
+      if (rcs[t] != WR_OK) msg[t] = wr::last_error();
     });
   rcs[0] = run(0);
+  if (rcs[0] != WR_OK) msg[0] = wr::last_error();
   for (auto& x : th) x.join();
-  for (int rc : rcs)
-    if (rc) return rc;
+  for (int t = 0; t < T; ++t)
+    if (rcs[t] != WR_OK) return fail(rcs[t], msg[t]);
   return WR_OK;
 }
 }  // extern "C++"
@@ -1974,6 +2037,13 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   if (fit < 1) return WR_E_HIP;  // message set by the allocation
   const PiecePlan plan = plan_pieces(f_lo, f_hi, P, unit, cap, fit, c->piece_min);
   const int np = plan.pipes();
+  // the buffer sets, queues and shadow-queue bounds below are laid out for `cap`
+  // paths: a larger piece would write past them
+  for (const auto& pp : plan.per_pipe)
+    for (const auto& g : pp)
+      for (const Piece& pc : g)
+        if (pc.n > cap || pc.n <= 0)
+          return fail(WR_E_ARG, "piece plan: a piece of " + std::to_string(pc.n) + " paths exceeds the buffer capacity " + std::to_string(cap));
   {  // WR_TRACE_BVH t2 scratch: a launch takes <= kGroup x (shadow / aux + extension) queues.
      // Laid out on every pipeline that fits, as the work buffers are: a short
      // render (a warm-up) on few of them leaves nothing to allocate to a long one
@@ -2605,6 +2675,7 @@ int wr_reserve(wr_context* c, int integrator, int32_t width, int32_t height) {
   if (integrator < WR_INTEGRATOR_BDPT || integrator > WR_INTEGRATOR_PATH) return fail(WR_E_ARG, "bad integrator");
   if (width <= 0 || height <= 0) return fail(WR_E_ARG, "bad film size");
   if (static_cast<int64_t>(width) * height >= (1 << 30) / (kVMax + 2)) return fail(WR_E_ARG, "film too large for one context");
+  DeviceGuard dg;
   if (int rc = reserve_one(c, integrator, width, height)) return rc;
   for (wr_context* d : c->subs)
     if (int rc = reserve_one(d, integrator, width, height)) return rc;
@@ -2613,6 +2684,7 @@ int wr_reserve(wr_context* c, int integrator, int32_t width, int32_t height) {
 
 int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int film_on_device, wr_stats* st) {
   if (int rc = check_bdpt(c, prm, film)) return rc;
+  DeviceGuard dg;
   const int P = prm->width * prm->height;
   const int64_t T = static_cast<int64_t>(prm->iterations) * P;
   if (c->subs.empty()) return render_bdpt_one(c, prm, 0, T, film, film_on_device, st);
@@ -2630,6 +2702,7 @@ int wr_render_bdpt(wr_context* c, const wr_bdpt_params* prm, float* film, int fi
 
 int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film_on_device, wr_stats* st) {
   if (int rc = check_vcm(c, prm, film)) return rc;
+  DeviceGuard dg;
   if (c->subs.empty()) return render_vcm_one(c, prm, film, film_on_device, st);
   // whole iterations per device: an iteration's merge grid holds all of its
   // light vertices (vertexcm.cpp:152)
@@ -2647,6 +2720,7 @@ int wr_render_vcm(wr_context* c, const wr_vcm_params* prm, float* film, int film
 
 int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int film_on_device, wr_stats* st) {
   if (int rc = check_path(c, prm, film)) return rc;
+  DeviceGuard dg;
   if (c->subs.empty()) return render_path_one(c, prm, film, film_on_device, st);
   const int k0 = prm->sample_begin, k1 = prm->sample_count > 0 ? k0 + prm->sample_count : prm->spp;
   return multi_render(c, size_t(prm->width) * prm->height * 3, film, film_on_device, st,
@@ -2663,6 +2737,7 @@ int wr_render_path(wr_context* c, const wr_path_params* prm, float* film, int fi
 int wr_path_radiance(wr_context* c, const wr_ray* rays, int64_t n64, int32_t max_depth, uint32_t seed,
                      int32_t sample, float* rgb, wr_stats* st) {
   if (int rc = check_radiance(c, rays, n64, max_depth, rgb)) return rc;
+  DeviceGuard dg;
   return path_radiance_one(c, rays, n64, max_depth, seed, sample, rgb, st);  // devices[0]
 }
 
@@ -2670,6 +2745,7 @@ int wr_create_multi(const wr_scene* sc, const int* devices, int n, wr_context** 
   if (!sc || !devices || !out || n < 1 || n > 64) return fail(WR_E_ARG, "bad argument (1..64 devices)");
   *out = nullptr;
   if (int rc = check_device()) return rc;
+  DeviceGuard dg;
   int have = 0;
   (void)hipGetDeviceCount(&have);
   for (int k = 0; k < n; ++k)
@@ -2742,6 +2818,7 @@ int wr_comm_init(wr_context* c, const uint8_t id[128], int nranks, int rank) {
   if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(WR_E_ARG, "bad argument");
   if (!c->subs.empty()) return fail(WR_E_ARG, "a multi-device context reduces over its own devices");
   if (!rccl().ok) return fail(WR_E_HIP, rccl().why);
+  DeviceGuard dg;
   HIPCHK(hipSetDevice(c->device));
   if (c->comm) (void)rccl().destroy(c->comm);
   c->comm = nullptr;
@@ -2757,6 +2834,7 @@ int wr_film_reduce(wr_context* c, float* film, int64_t nfloat, int root) {
   if (!c || (!film && nfloat) || nfloat < 0) return fail(WR_E_ARG, "bad argument");
   if (!c->comm) return fail(WR_E_ARG, "no communicator: call wr_comm_init first");
   if (root < 0 || root >= c->comm_ranks) return fail(WR_E_ARG, "bad root rank");
+  DeviceGuard dg;
   HIPCHK(hipSetDevice(c->device));
   // ordered after the caller's work on the legacy null stream, like a render
   (void)hipEventRecord(c->t_null, nullptr);

@@ -919,4 +919,21 @@ int set_error(int code, const std::string& msg) {
 }
 const char* last_error() { return g_err.c_str(); }
 
+uint64_t scene_fingerprint(const Scene& s) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  };
+  const uint64_t n[3] = {s.prims.size(), s.lights.size(), s.mats.size()};
+  mix(n, sizeof n);
+  // all-4-byte-field records: no padding bytes enter the hash
+  static_assert(sizeof(Prim) % 4 == 0 && sizeof(Light) % 4 == 0 && sizeof(Material) % 4 == 0, "packed records");
+  if (!s.prims.empty()) mix(s.prims.data(), s.prims.size() * sizeof(Prim));
+  if (!s.lights.empty()) mix(s.lights.data(), s.lights.size() * sizeof(Light));
+  if (!s.mats.empty()) mix(s.mats.data(), s.mats.size() * sizeof(Material));
+  mix(&s.cam, sizeof s.cam);
+  return h;
+}
+
 }  // namespace wr

@@ -104,6 +104,11 @@ void build_kdtree(Scene& s);
 // Text dump with the exact format of oracle/ref_driver.cpp `scene`.
 std::string dump_scene(const Scene& s);
 
+// 64-bit FNV-1a over what a render reads from the scene: primitives (type,
+// material, geometry), lights, materials and the camera.  Checkpoints carry
+// it so that a film is never resumed into a render of another scene.
+uint64_t scene_fingerprint(const Scene& s);
+
 // Camera::setup (camera.cpp:3-29).
 void setup_camera(Camera& c, F3 pos, F3 fwd, F3 up, float xres, float yres, float fov);
 

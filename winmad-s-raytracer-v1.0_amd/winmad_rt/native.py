@@ -6,6 +6,7 @@ loaded every call raises.
 """
 import ctypes as C
 import os
+import sys
 
 import numpy as np
 
@@ -19,7 +20,7 @@ TRACE_REFERENCE, TRACE_BVH = 0, 1
 INTEGRATOR_BDPT, INTEGRATOR_VCM, INTEGRATOR_PATH = 0, 1, 2
 
 # every entry point declared in include/winmad_rt.h
-EXPORTS = ["wr_scene_load", "wr_scene_from_desc", "wr_scene_info_get", "wr_scene_dump", "wr_scene_free",
+EXPORTS = ["wr_scene_load", "wr_scene_from_desc", "wr_scene_info_get", "wr_scene_fingerprint", "wr_scene_dump", "wr_scene_free",
            "wr_device_count", "wr_create", "wr_create_multi", "wr_context_devices", "wr_destroy", "wr_comm_unique_id",
            "wr_comm_init", "wr_film_reduce", "wr_set_pipelines", "wr_set_trace_mode", "wr_trace_closest", "wr_occluded",
            "wr_render_bdpt", "wr_render_path", "wr_render_vcm", "wr_path_radiance", "wr_film_write_ppm",
@@ -55,7 +56,7 @@ class WrSceneDesc(C.Structure):
 
 class WrCheckpointInfo(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("kind", C.c_int32), ("done", C.c_int32),
-                ("total", C.c_int32), ("seed", C.c_uint32), ("reserved", C.c_int32 * 2)]
+                ("total", C.c_int32), ("seed", C.c_uint32), ("fingerprint", C.c_uint32 * 2)]
 
 
 class WrBdptParams(C.Structure):
@@ -117,6 +118,21 @@ def _share_torch_runtime():
         pass
 
 
+def _keep_hw_queues_if_hip_is_up():
+    """The library raises GPU_MAX_HW_QUEUES to 16 when it loads (one hardware
+    queue per render pipeline), which only takes effect if HIP has not been
+    initialised yet.  When torch already initialised it, HIP keeps the queues it
+    read then: pin the library to that value (WR_HW_QUEUES) so that it does not
+    start more pipelines than there are queues (they would serialize)."""
+    torch = sys.modules.get("torch")
+    try:
+        up = torch is not None and torch.cuda.is_initialized()
+    except Exception:
+        up = False
+    if up and "WR_HW_QUEUES" not in os.environ:
+        os.environ["WR_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES") or "4"
+
+
 def lib():
     """Load the in-tree HIP library (raises if it has not been built)."""
     global _lib
@@ -125,6 +141,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C {PKG_DIR}` "
                                "(or __graft_entry__.build()); there is no CPU fallback")
+        _keep_hw_queues_if_hip_is_up()
         L = C.CDLL(LIB_PATH)
         P, I, I64 = C.c_void_p, C.c_int, C.c_int64
         L.wr_scene_load.argtypes = [C.c_char_p, C.POINTER(P)]
@@ -138,6 +155,7 @@ def lib():
         L.wr_checkpoint_load.argtypes = [C.c_char_p, C.POINTER(WrCheckpointInfo), C.POINTER(C.c_float), I64]
         L.wr_scene_info_get.argtypes = [P, C.POINTER(WrSceneInfo)]
         L.wr_scene_dump.argtypes = [P, C.c_char_p]
+        L.wr_scene_fingerprint.argtypes = [P, C.POINTER(C.c_uint64)]
         L.wr_scene_free.argtypes = [P]
         L.wr_scene_free.restype = None
         L.wr_create.argtypes = [P, I, C.POINTER(P)]
@@ -225,6 +243,12 @@ class Scene:
         check(lib().wr_scene_info_get(self.h, C.byref(i)))
         return {k: getattr(i, k) for k, _ in i._fields_}
 
+    def fingerprint(self):
+        """wr_scene_fingerprint: 64-bit hash of the primitives, lights, materials, camera."""
+        v = C.c_uint64()
+        check(lib().wr_scene_fingerprint(self.h, C.byref(v)))
+        return v.value
+
     def dump(self, path):
         check(lib().wr_scene_dump(self.h, os.fsencode(path)))
         with open(path) as f:
@@ -268,7 +292,9 @@ class Context:
     """Scene resident in HBM on one device (or on several: `devices`, a list of
     HIP device ids, wr_create_multi) + its HIP streams."""
 
-    def __init__(self, scene, device=0, devices=None):
+    def __init__(self, scene, device=0, devices=None, trace=None):
+        """trace: None keeps the library default (the verified BVH for triangle
+        scenes, the KD walk with spheres), else TRACE_REFERENCE / TRACE_BVH."""
         h = C.c_void_p()
         if devices is not None:
             ids = (C.c_int * len(devices))(*devices)
@@ -277,6 +303,8 @@ class Context:
             check(lib().wr_create(scene.h, device, C.byref(h)))
         self.h = h
         self.scene = scene
+        if trace is not None:
+            self.set_trace_mode(trace)
 
     def devices(self):
         buf = (C.c_int * 64)()
@@ -397,23 +425,27 @@ def comm_unique_id():
     return bytes(buf)
 
 
-def checkpoint_save(path, film, kind, done, total, seed):
-    """wr_checkpoint_save: the accumulated film + how many iterations it sums."""
+def checkpoint_save(path, film, kind, done, total, seed, fingerprint=0):
+    """wr_checkpoint_save: the accumulated film + how many iterations it sums
+    (+ the 64-bit scene / settings fingerprint the resume must match)."""
     film = np.ascontiguousarray(film, np.float32)
     if film.ndim != 3 or film.shape[2] != 3:
         raise ValueError(f"film must have shape (height, width, 3), got {film.shape}")
-    info = WrCheckpointInfo(film.shape[1], film.shape[0], kind, done, total, seed)
+    info = WrCheckpointInfo(film.shape[1], film.shape[0], kind, done, total, seed,
+                            (C.c_uint32 * 2)(fingerprint & 0xFFFFFFFF, (fingerprint >> 32) & 0xFFFFFFFF))
     check(lib().wr_checkpoint_save(os.fsencode(path), C.byref(info), film.ctypes.data_as(C.POINTER(C.c_float))))
 
 
 def checkpoint_load(path):
-    """wr_checkpoint_load -> (film, dict(width, height, kind, done, total, seed))."""
+    """wr_checkpoint_load -> (film, dict(width, height, kind, done, total, seed, fingerprint))."""
     info = WrCheckpointInfo()
     check(lib().wr_checkpoint_load(os.fsencode(path), C.byref(info), None, 0))
     film = np.zeros((info.height, info.width, 3), np.float32)
     check(lib().wr_checkpoint_load(os.fsencode(path), C.byref(info), film.ctypes.data_as(C.POINTER(C.c_float)),
                                    film.size))
-    return film, {k: getattr(info, k) for k in ("width", "height", "kind", "done", "total", "seed")}
+    d = {k: getattr(info, k) for k in ("width", "height", "kind", "done", "total", "seed")}
+    d["fingerprint"] = int(info.fingerprint[0]) | (int(info.fingerprint[1]) << 32)
+    return film, d
 
 
 def write_ppm(film, path, scale=1.0, gamma=2.2, transpose=False):
