@@ -12,6 +12,13 @@
 //   refdrv bdpt   SCENE PARA ITERS SEED OUT.f32  BidirPathTracing::render, film pre-transpose
 //   refdrv pt     SCENE PARA SEED OUT.f32        PathIntegrator via SurfaceIntegrator::render
 //   refdrv vcm    SCENE PARA ITERS SEED OUT.f32  VertexCM::render (ref_driver_vcm.cpp)
+//   refdrv image  H W ITERS TRANSPOSE IN.f32 OUT.rgb
+//                 the 8-bit pixels ImageFilm::outputImage hands to cvSaveImage
+//                 (film.cpp:39-64): a float film (H x W x 3) -> [transpose, as
+//                 BidirPathTracing/VertexCM::outputImage do first,
+//                 bidirPathTracing.cpp:31-41] -> ImageFilm::scale(1.f / ITERS)
+//                 -> clamp -> gamma(2.2) -> Color3::R/G/B (color.h:47-75),
+//                 written as RGB rows (the reference stores B, G, R per pixel)
 //
 // Every command chdir()s to $REFDRV_CWD (if set) after static initialisation so the
 // reference's debug files (bidirPathTracing.cpp:3, vertexcm.h:10) land in a scratch directory.
@@ -215,10 +222,49 @@ static double now() {
     return ts.tv_sec + 1e-9 * ts.tv_nsec;
 }
 
+// refdrv image: the reference's own ImageFilm / Color3 members on a loaded film
+static int cmd_image(int argc, char** argv) {
+    if (argc < 8) { fprintf(stderr, "usage: refdrv image H W ITERS TRANSPOSE IN.f32 OUT.rgb\n"); return 2; }
+    const int h = atoi(argv[2]), w = atoi(argv[3]), iters = atoi(argv[4]), tr = atoi(argv[5]);
+    ImageFilm film(h, w);
+    FILE* f = fopen(argv[6], "rb");
+    if (!f) { perror(argv[6]); return 1; }
+    for (int i = 0; i < h; i++)
+        for (int j = 0; j < w; j++) {
+            float v[3];
+            if (fread(v, sizeof(float), 3, f) != 3) { fprintf(stderr, "short film\n"); return 1; }
+            film.color[i][j] = Color3(v[0], v[1], v[2]);
+        }
+    fclose(f);
+    if (tr)  // the in-place swap of bidirPathTracing.cpp:31-41 (square films)
+        for (int i = 0; i < h; i++)
+            for (int j = 0; j < i; j++) {
+                Color3 t = film.color[i][j];
+                film.color[i][j] = film.color[j][i];
+                film.color[j][i] = t;
+            }
+    // film->outputImage(filename, 1.f / iterations, 2.2) up to cvSaveImage
+    // (film.cpp:45-60); PT passes (1.f, 2.2f), i.e. ITERS = 1
+    const Real scale = 1.f / iters, gamma = 2.2;
+    film.scale(scale);
+    film.clamp();
+    film.gamma(gamma);
+    FILE* o = fopen(argv[7], "wb");
+    if (!o) { perror(argv[7]); return 1; }
+    for (int i = 0; i < h; i++)
+        for (int j = 0; j < w; j++) {
+            unsigned char px[3] = {film.color[i][j].R(), film.color[i][j].G(), film.color[i][j].B()};
+            fwrite(px, 1, 3, o);
+        }
+    fclose(o);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { fprintf(stderr, "usage: see header\n"); return 2; }
     const char* cwd = getenv("REFDRV_CWD");
     std::string cmd = argv[1];
+    if (cmd == "image") return cmd_image(argc, argv);
     if (cmd == "mt") {
         RNG rng((uint32_t)strtoul(argv[2], 0, 10));
         int n = atoi(argv[3]);

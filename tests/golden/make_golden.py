@@ -7,7 +7,8 @@ outputs as fixtures.  Only data is written here (inputs and expected outputs);
 no reference source text.  Needs /root/reference (this container only); the GPU
 box uses the committed fixtures.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py          (everything)
+    python tests/golden/make_golden.py image    (the 8-bit image fixtures only)
 """
 import hashlib
 import json
@@ -70,7 +71,46 @@ def ray_corpus(scene_dump, n, seed):
     return out
 
 
+# 8-bit output (film.cpp:39-64 + color.h:47-75): (name, height, width, ITERS, transpose)
+IMAGE_CASES = [("sq37", 37, 37, 3, 1), ("r23x41", 23, 41, 1, 0), ("bdpt_torus64_i4_s5489", 64, 64, 4, 1)]
+
+
+def image_film(name, h, w):
+    """Input films of the image fixtures: random radiance over six decades,
+    the exact float boundaries of the 8-bit levels (x with pow(x, 1/2.2) * 255
+    at or next to an integer, and one ulp either side), zero, negatives,
+    values above the clamp, NaN and infinities.  The BDPT case is the
+    reference's own torus film."""
+    if name.startswith("bdpt_"):
+        return np.fromfile(os.path.join(HERE, name + ".f32"), np.float32).reshape(h, w, 3)
+    rng = np.random.default_rng(2024 + h * w)
+    f = (10.0 ** rng.uniform(-4, 2, (h, w, 3))).astype(np.float32)
+    flat = f.reshape(-1)
+    k = np.arange(256, dtype=np.float64)
+    edge = ((k / 255.0) ** 2.2).astype(np.float32)
+    specials = np.concatenate([edge, np.nextafter(edge, np.float32(0)), np.nextafter(edge, np.float32(2)),
+                               np.array([0, -0.0, -1, -1e-30, 1, 1.0000001, 3, 1e30, np.nan, np.inf, -np.inf],
+                                        np.float32)])
+    idx = rng.choice(flat.size, specials.size, replace=False)
+    flat[idx] = specials * np.float32(1 if name != "sq37" else 3)  # ITERS = 3 scales them back
+    return f
+
+
+def image_fixtures(tmp):
+    for name, h, w, iters, tr in IMAGE_CASES:
+        film = image_film(name, h, w)
+        src = os.path.join(HERE, f"image_in_{name}.f32")
+        if not name.startswith("bdpt_"):
+            film.astype(np.float32).tofile(src)
+        else:
+            src = os.path.join(HERE, name + ".f32")
+        refdrv("image", h, w, iters, tr, src, os.path.join(HERE, f"image_{name}.rgb"), cwd=tmp)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "image":  # the image fixtures alone
+        image_fixtures(tempfile.mkdtemp(prefix="wr_golden_"))
+        return
     if not os.path.exists(REFDRV):
         sys.exit("build the reference driver first: make -C oracle ref")
     tmp = tempfile.mkdtemp(prefix="wr_golden_")
@@ -154,6 +194,7 @@ def main():
         sp, pp = os.path.join(tmp, name + ".scene"), os.path.join(tmp, name + ".para")
         extra = [] if rf is None else [rf]
         refdrv("vcm", sp, pp, it, seed, os.path.join(HERE, vcm_fixture(name, it, seed, rf)), *extra, cwd=tmp)
+    image_fixtures(tmp)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print(json.dumps({k: v for k, v in meta.items() if "block32_mean" not in v}, indent=1))

@@ -117,21 +117,55 @@ def test_create_without_gpu_fails_loudly():
     assert e.value.code == native.WR_E_NODEVICE
 
 
-def test_film_writer_matches_reference_pipeline(tmp_path):
-    """scale -> clamp -> pow(1/2.2) -> (uchar)(x*255.0) (film.cpp:39-64, color.h:47-75)."""
-    rng = np.random.default_rng(3)
-    film = (rng.random((5, 5, 3)) * 1.5).astype(np.float32)
+IMAGE_CASES = [("sq37", 37, 37, 3, 1), ("r23x41", 23, 41, 1, 0), ("bdpt_torus64_i4_s5489", 64, 64, 4, 1)]
+
+
+def _png_rgb(raw, h, w):
+    """Decode the writer's PNG (stored-deflate IDAT, filter 0 rows)."""
+    import zlib
+    assert raw[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat = 8, b""
+    while pos < len(raw):
+        n = int.from_bytes(raw[pos:pos + 4], "big")
+        if raw[pos + 4:pos + 8] == b"IDAT":
+            idat += raw[pos + 8:pos + 8 + n]
+        pos += 12 + n
+    rows = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 3 * w + 1)
+    assert (rows[:, 0] == 0).all()
+    return rows[:, 1:].reshape(h, w, 3)
+
+
+@pytest.mark.parametrize("name,h,w,iters,tr", IMAGE_CASES)
+def test_film_writer_bytes_equal_the_reference(name, h, w, iters, tr, tmp_path):
+    """8-bit output, bit-exact against the reference's own ImageFilm::scale ->
+    clamp -> gamma(2.2) -> Color3::R/G/B (film.cpp:11-30, 45-60; color.h:47-75)
+    run by oracle/_ref/refdrv `image` on the same float film (after the BDPT
+    transpose, bidirPathTracing.cpp:31-41, for the square cases): every byte of
+    .ppm, .bmp and .png, NaN / inf / negative inputs and the exact float
+    boundaries of the 8-bit levels included (tests/golden/make_golden.py)."""
+    src = os.path.join(GOLD, f"image_in_{name}.f32" if not name.startswith("bdpt_") else name + ".f32")
+    film = np.fromfile(src, np.float32).reshape(h, w, 3)
+    want = np.fromfile(os.path.join(GOLD, f"image_{name}.rgb"), np.uint8).reshape(h, w, 3)
+    scale = float(np.float32(1) / np.float32(iters))  # 1.f / iterations (bidirPathTracing.cpp:45)
     p = tmp_path / "f.ppm"
-    native.write_ppm(film, str(p), scale=0.5, gamma=2.2, transpose=True)
+    native.write_ppm(film, str(p), scale=scale, gamma=2.2, transpose=bool(tr))
     raw = p.read_bytes()
-    hdr = b"P6\n5 5\n255\n"
+    hdr = f"P6\n{w} {h}\n255\n".encode()
     assert raw.startswith(hdr)
-    img = np.frombuffer(raw[len(hdr):], np.uint8).reshape(5, 5, 3)
-    f = np.transpose(film, (1, 0, 2)) * np.float32(0.5)
-    f = np.minimum(np.float32(1), np.maximum(f, np.float32(0)))
-    f = np.power(f, np.float32(1) / np.float32(2.2))
-    exp = (f.astype(np.float64) * 255.0).astype(np.uint8)
-    assert np.abs(img.astype(int) - exp.astype(int)).max() <= 1
+    got = np.frombuffer(raw[len(hdr):], np.uint8).reshape(h, w, 3)
+    assert np.array_equal(got, want), int((got != want).sum())
+    for ext in (".ppm", ".bmp", ".png"):
+        q = tmp_path / f"g{ext}"
+        native.write_image(film, str(q), scale=scale, gamma=2.2, transpose=bool(tr))
+        raw = q.read_bytes()
+        if ext == ".ppm":
+            img = np.frombuffer(raw[len(hdr):], np.uint8).reshape(h, w, 3)
+        elif ext == ".bmp":  # bottom-up BGR rows padded to 4 bytes
+            row = (3 * w + 3) & ~3
+            img = np.frombuffer(raw[54:], np.uint8).reshape(h, row)[::-1, :3 * w].reshape(h, w, 3)[..., ::-1]
+        else:
+            img = _png_rgb(raw, h, w)
+        assert np.array_equal(img, want), (ext, int((img != want).sum()))
 
 
 def test_cli_mirrors_reference_main(tmp_path):
