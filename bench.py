@@ -40,21 +40,28 @@ sys.path.insert(0, os.path.join(REPO, "winmad-s-raytracer-v1.0_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2, 8 XCDs x 4 MiB, ~34.5 TB/s aggregate
-# HBM bytes per k_trace launch from the PMC passes of the same bench command
-# (scripts/profile_round.sh + scripts/summarize_profile.py; counters cannot be
-# read from inside the timed run); the newest round's file wins
+# HBM bytes per traversal launch from the PMC passes of the same bench command
+# and configuration (scripts/profile_round.sh + scripts/summarize_profile.py:
+# rocprofv3 counters cannot be read from inside the timed run, which is not
+# run under the profiler).  One file per configuration
+# (profiles/<round>/traffic_<config>.json; C2's older rounds: traffic.json);
+# the newest round's file wins and its name is in the line (traffic_source).
 PROFILES = os.path.join(REPO, "profiles")
-TRAFFIC_JSON = next((p for p in (os.path.join(PROFILES, r, "traffic.json") for r in ("r3", "r2", "r1"))
-                     if os.path.exists(p)), os.path.join(PROFILES, "r1", "traffic.json"))
+ROUNDS = ("r4", "r3", "r2", "r1")
 
 
-def pmc_traffic():
-    try:
-        with open(TRAFFIC_JSON) as f:
-            t = json.load(f)
-        return t.get("hbm_bytes_per_launch"), os.path.relpath(TRAFFIC_JSON, REPO)
-    except (OSError, ValueError):
-        return None, None
+def pmc_traffic(config):
+    names = [f"traffic_{config}.json"] + (["traffic.json"] if config == "c2" else [])
+    for r in ROUNDS:
+        for n in names:
+            p = os.path.join(PROFILES, r, n)
+            try:
+                with open(p) as f:
+                    t = json.load(f)
+            except (OSError, ValueError):
+                continue
+            return t, os.path.relpath(p, REPO)
+    return None, None
 
 
 def algorithmic_bytes(rays, inner, leaves, refs, tests):
@@ -128,8 +135,12 @@ def cpu_reference(cfg_name, kind, W, H, tmp, shrink):
         return None
     sec = float(next(l for l in r.stdout.splitlines() if l.startswith("render_seconds")).split()[1])
     # all cores of this box's CPU share: the same sample in `ncores` concurrent
-    # single-threaded reference processes (the reference has no threading)
-    ncores = max(1, min(16, os.cpu_count() or 1))
+    # single-threaded reference processes (the reference has no threading).
+    # The GPU box gives one job 16 CPUs (OMP_NUM_THREADS / MAX_JOBS = 16 there)
+    # while os.cpu_count() shows the whole machine's: capped at the share
+    machine_cpus = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS") or 16)
+    ncores = max(1, min(share, 16, machine_cpus))
     procs = [subprocess.Popen([REFDRV, *map(str, args[:-1]), out + f".{k}"], stdout=subprocess.PIPE,
                               stderr=subprocess.DEVNULL, text=True, env=env) for k in range(ncores)]
     outs = [p.communicate(timeout=900) for p in procs]
@@ -153,8 +164,10 @@ def cpu_reference(cfg_name, kind, W, H, tmp, shrink):
            "film_bit_exact": bool(np.array_equal(film.view(np.uint32), ref.view(np.uint32)))}
     if ok:
         res["all_cores"] = {"value": round(ncores * rays / wall_all / 1e6, 4), "unit": "Mrays/s", "cores": ncores,
+                            "machine_cpus": machine_cpus,
                             "sample": f"{ncores} concurrent refdrv processes of the same sample, "
-                                      f"slowest render() {wall_all:.2f} s"}
+                                      f"slowest render() {wall_all:.2f} s; {ncores} = this job's CPU share "
+                                      f"(the machine shows {machine_cpus} CPUs)"}
     return res
 
 
@@ -318,7 +331,8 @@ def main():
         avg_launch_s = trace_ms / 1e3 / max(1, trace_launches)
         wall_s = st.trace_wall_ms / 1e3
         achieved = total_bytes / wall_s / 1e9 if wall_s > 0 else 0.0
-        traffic, traffic_src = pmc_traffic() if args.config == "c2" else (None, None)
+        tr_rec, traffic_src = pmc_traffic(args.config)
+        traffic = tr_rec.get("hbm_bytes_per_launch") if tr_rec else None
         # The scene is cache-resident (torus: 1.8 MB, L2; 1M triangles: 78 MB,
         # Infinity Cache), so the algorithmic bytes are served by L2, not HBM:
         # PMC HBM traffic per launch is ~1 % of them.  The bytes are priced
@@ -331,7 +345,8 @@ def main():
             hbm_gbs = traffic * trace_launches / wall_s / 1e9
             hbm = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "source": "PMC FETCH_SIZE x2 + WRITE_SIZE per launch "
-                   "x launches / trace_wall_ms"}
+                   "x launches / trace_wall_ms", "l2_hit_rate": tr_rec.get("l2_hit_rate"),
+                   "pmc_build": tr_rec.get("head")}
         roofline = {"bound": "l2", "achieved": round(achieved, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / L2_PEAK_GBS, 4),
                     "limiter": "latency of dependent L2 round trips + VALU issue (PMC, DESIGN.md section 4)",

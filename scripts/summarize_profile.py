@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """Condense a scripts/profile_round.sh output directory into profiles/<tag>/.
 
-    python scripts/summarize_profile.py gpurun_out/prof_<tag> profiles/<tag>
+    python scripts/summarize_profile.py gpurun_out/prof_<tag> profiles/<tag> [config]
 
 Writes
-  kernel_stats.csv  rocprofv3 --kernel-trace --stats summary (copied as is)
-  pmc_summary.json  per kernel: dispatches and the per-dispatch mean of every
+  kernel_stats_<config>.csv  rocprofv3 --kernel-trace --stats summary (copied as is)
+  pmc_summary_<config>.json  per kernel: dispatches and the per-dispatch mean of every
                     PMC counter collected in the separate --pmc passes
-  traffic.json      HBM bytes per traversal step (k_trace, or the BVH mode's
+  traffic_<config>.json (config c2 when not given)
+                    HBM bytes per traversal step (k_trace, or the BVH mode's
                     three kernels), per MI355X_MICROARCH.md
                     "HBM [CDNA4]": FETCH_SIZE / WRITE_SIZE are in KiB, and on
                     gfx950 FETCH_SIZE counts half the bytes of a read, so
@@ -37,10 +38,11 @@ def short(name):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
+    config = sys.argv[3] if len(sys.argv) > 3 else "c2"
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
-        shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+        shutil.copy(stats, os.path.join(dst, f"kernel_stats_{config}.csv"))
     per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values (one per dispatch)
     for f in sorted(glob.glob(os.path.join(src, "pmc*", "run_counter_collection.csv"))):
         with open(f) as fh:
@@ -49,7 +51,7 @@ def main():
     summary = {}
     for k, counters in per.items():
         summary[k] = {c: {"dispatches": len(v), "mean": sum(v) / len(v)} for c, v in counters.items()}
-    with open(os.path.join(dst, "pmc_summary.json"), "w") as fh:
+    with open(os.path.join(dst, f"pmc_summary_{config}.json"), "w") as fh:
         json.dump(summary, fh, indent=1, sort_keys=True)
 
     # one traversal step = k_trace (reference mode) or k_trace_fast +
@@ -59,7 +61,13 @@ def main():
     lead = fam[0]
     tr = [k for k in summary if k.startswith(fam) and not k.startswith("k_trace_fast") or k.startswith(lead)]
     tr = [k for k in summary if any(k.startswith(f + "<") or k == f for f in fam)]
-    out = {"kernel": " + ".join(fam), "variants": tr}
+    out = {"kernel": " + ".join(fam), "variants": tr, "config": config}
+    try:  # the build the counters describe (run here, after the box's files are pulled)
+        import subprocess
+        out["head"] = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True,
+                                     cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip() or None
+    except OSError:
+        out["head"] = None
     if tr:
         steps = len([v for k in tr if k.startswith(lead + "<") or k == lead for v in per[k].get("FETCH_SIZE", [])])
 
@@ -74,7 +82,7 @@ def main():
                     "hbm_bytes_per_launch": (2 * 1024 * fetch + 1024 * write)
                     if fetch is not None and write is not None else None,
                     "l2_hit_rate": hit / (hit + miss) if hit is not None and miss else None})
-    with open(os.path.join(dst, "traffic.json"), "w") as fh:
+    with open(os.path.join(dst, f"traffic_{config}.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))
 
@@ -88,7 +96,7 @@ def main():
             lines = [l for l in fh if l.startswith('{"metric"')]
         line = json.loads(lines[-1]) if lines else None
     if line and os.path.exists(stats):
-        with open(os.path.join(dst, "bench_profiled_run.json"), "w") as fh:
+        with open(os.path.join(dst, f"bench_profiled_run_{config}.json"), "w") as fh:
             fh.write(json.dumps(line) + "\n")
         rows = [r for r in csv.DictReader(open(stats))
                 if any(short(r["Name"]).startswith(f + "<false") for f in fam)]
@@ -99,7 +107,7 @@ def main():
                 "rocprof_steps": calls, "rocprof_avg_ms_per_step": round(tot / max(1, calls) / 1e6, 4),
                 "bench_launches": r["launches"], "bench_event_avg_ms": r["avg_launch_ms"],
                 "ratio_events_over_rocprof": round(r["avg_launch_ms"] / (tot / max(1, calls) / 1e6), 3)}
-        with open(os.path.join(dst, "duration_check.json"), "w") as fh:
+        with open(os.path.join(dst, f"duration_check_{config}.json"), "w") as fh:
             json.dump(cmp_, fh, indent=1)
         print(json.dumps(cmp_))
 

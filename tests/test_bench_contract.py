@@ -28,7 +28,7 @@ def run_bench(*args):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", ["c2", "c3", "vcm"])
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c4", "vcm"])
 def test_bench_line(cfg):
     d = run_bench("--config", cfg)
     for k in KEYS:

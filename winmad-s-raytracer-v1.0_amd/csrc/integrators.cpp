@@ -41,6 +41,10 @@ void SurfaceIntegrator::load(const char* filename) {
     ok(wr_create(scene_, devices.empty() ? device : devices[0], &ctx_));
   if (traceMode >= 0) ok(wr_set_trace_mode(ctx_, traceMode));
   film.assign(static_cast<size_t>(height) * width * 3, 0.f);
+  // the render's GPU work buffers now, as the reference's init allocates its
+  // film and vertex arrays before render() (bidirPathTracing.cpp:5-21): the
+  // render call then only renders
+  if (reserveAtInit) ok(wr_reserve(ctx_, integrator_, width, height));
 }
 
 void SurfaceIntegrator::setTraceMode(int mode) {

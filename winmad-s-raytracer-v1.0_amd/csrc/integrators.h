@@ -29,6 +29,7 @@ class SurfaceIntegrator {
   int width = 0, height = 0, samplesPerPixel = 0;
   int device = 0;
   std::vector<int> devices;  // more than one: the GPUs of this node share the render (wr_create_multi)
+  bool reserveAtInit = true;  // init() allocates the render's work buffers (wr_reserve)
   int traceMode = -1;        // -1: the library's default (WR_TRACE_BVH for triangle scenes); WR_TRACE_REFERENCE / WR_TRACE_BVH
   // Film checkpoint (the reference keeps the film in memory only,
   // bidirPathTracing.cpp:23-27): with a path set, render() resumes from a
@@ -48,7 +49,8 @@ class SurfaceIntegrator {
   // wr_set_trace_mode after init (throws, e.g. WR_TRACE_BVH on a scene with spheres)
   void setTraceMode(int mode);
   // wr_reserve after init / setTraceMode: the render's GPU buffers now, so that
-  // render() only renders (optional; render() allocates them otherwise)
+  // render() only renders (init() already does it unless reserveAtInit is false;
+  // render() allocates whatever is missing otherwise)
   void reserve();
 
  protected:
