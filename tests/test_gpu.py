@@ -429,6 +429,34 @@ def test_bdpt_pieces_render_like_whole_iterations(W, H, monkeypatch):
     assert_ray_counts(gs, ost)
 
 
+@pytest.mark.parametrize("name,maker,W,H", [("torus", lambda: _scenes.torus(96, 64), 96, 64),
+                                             ("cbox", lambda: _scenes.cbox(64, 48, "bdpt"), 64, 48),
+                                             ("spheres", lambda: _scenes.spheres(64, 64), 64, 64)])
+@pytest.mark.parametrize("ctl", [3, 0])
+def test_bdpt_overlapped_passes_equal_the_sequential_schedule(name, maker, W, H, ctl, monkeypatch):
+    """The overlapped schedule (light and camera passes bounce by bounce in
+    one launch; each (light vertex, camera vertex) pair connected by the
+    vertex made second, wr_bdpt.h) against the reference's order (the whole
+    light pass, then the camera pass; WR_BDPT_OVERLAP=0): the same rays, the
+    same film up to the order of float atomics, and the oracle's film --
+    controlLength 3 and every path length (connections of all lengths, the
+    Cornell box and spheres where they carry 12-15 % of the image)."""
+    path = maker()
+    s = native.Scene(path)
+    films = {}
+    for ov in ("1", "0"):
+        monkeypatch.setenv("WR_BDPT_OVERLAP", ov)
+        c = native.Context(s, 0)
+        films[ov] = c.render_bdpt(W, H, iterations=3, seed=77, control_length=ctl)
+        c.close()
+    (fa, sa), (fb, sb) = films["1"], films["0"]
+    assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
+    assert np.allclose(fa, fb, rtol=1e-4, atol=1e-6)
+    orc, ost = _oracle.Scene(path).bdpt(W, H, 3, 77, mode=1, control_length=ctl)
+    assert_film_parity(fa, orc)
+    assert_ray_counts(sa, ost)
+
+
 @pytest.mark.parametrize("W,H,cap,pipes", [(100, 60, 3000, 1), (100, 60, 1000, 2), (99, 61, 2049, 1)])
 def test_bdpt_pieces_never_exceed_the_buffer_capacity(W, H, cap, pipes, monkeypatch):
     """A film whose sides are not multiples of 8 (64-path units) with a

@@ -1,8 +1,20 @@
 // BidirPathTracing::runIteration (surfaceIntegrator/bidirPathTracing.cpp:53-265)
-// as wavefront kernels: light pass gen -> [trace -> shade] x 9, camera pass
-// gen -> [trace -> resolve + shade] x 11.  Included by wr_render.hip inside its
-// anonymous namespace (uses its device helpers: wave_append, ld3/st3,
-// film_add, the counter slots).
+// as wavefront kernels.  Two schedules (wr_render.hip, render_bdpt_one):
+//   sequential: light pass gen -> [trace -> shade] x 9, then camera pass gen ->
+//     [trace -> resolve + shade] x 11, as the reference orders them;
+//   overlapped (default): both passes start together and bounce b of each is
+//     traced by one launch (gen, then 11 steps).  A light vertex of length l
+//     and a camera vertex of length c of the same path (the only pairing,
+//     :130, :222-229) are connected by the vertex created second: the camera
+//     side connects the light vertices stored so far (l <= c: the light
+//     kernel of a step runs before the camera kernel), the light side the
+//     camera vertices stored at earlier steps (c < l; camera vertices that
+//     can still meet a later light vertex, c <= (maxlen - 2) / 2, are kept in
+//     a small store, CV_*).  Every pair the reference connects (:219-257) is
+//     connected once, with the same floats (connect_pair); only the order of
+//     the film's float additions differs.
+// Included by wr_render.hip inside its anonymous namespace (uses its device
+// helpers: wave_append, ld3/st3, film_add, the counter slots).
 #pragma once
 
 // =============================================================== BDPT state
@@ -14,6 +26,7 @@ enum : int {
   PS_VCOUNT = 14,  // light paths: stored light vertices
   PS_PIX = 14,     // camera paths: film pixel
   PS_DVM = 15,     // VCM: dVM (vertexcm.h:36)
+  PS_CVCOUNT = 15, // BDPT camera paths, overlapped schedule: stored camera vertices (CV_*)
   PS_WORDS = 16
 };
 __device__ __forceinline__ float& psf(float* s, int p, int k) { return s[size_t(p) * PS_WORDS + k]; }
@@ -77,13 +90,42 @@ __device__ __forceinline__ void drst3(float* s, int p, int k, V3 v) {
   r[2] = v.z;
 }
 
+// Stored camera vertices of the overlapped schedule, one 96-byte record per
+// slot j * P + p (j < kCvMax): what connectVertices (:610-665) reads of the
+// camera side when a LATER light vertex of the path makes the connection.
+// Only vertices with length <= (maxlen - 2) / 2 can meet a later light vertex
+// (c < l and l + 1 + c <= maxlen), so kCvMax = 4 slots for maxlen <= 10.
+enum : int {
+  CV_POS = 0, CV_N = 3, CV_WI = 6, CV_THR = 9, CV_DVCM = 12, CV_DVC = 13, CV_CONT = 14, CV_PD = 15, CV_PG = 16,
+  CV_LEN = 17, CV_NSPEC = 18, CV_MAT = 19, CV_PIX = 20, CV_WORDS = 24
+};
+constexpr int kCvMax = (kVMax + 1 - 2) / 2;
+__device__ __forceinline__ float& cvf(float* s, int i, int k) { return s[size_t(i) * CV_WORDS + k]; }
+__device__ __forceinline__ int& cvi(float* s, int i, int k) {
+  return reinterpret_cast<int*>(s)[size_t(i) * CV_WORDS + k];
+}
+__device__ __forceinline__ V3 cvld3(const float* s, int i, int k) {
+  const float* r = s + size_t(i) * CV_WORDS + k;
+  return v3(r[0], r[1], r[2]);
+}
+__device__ __forceinline__ void cvst3(float* s, int i, int k, V3 v) {
+  float* r = s + size_t(i) * CV_WORDS + k;
+  r[0] = v.x;
+  r[1] = v.y;
+  r[2] = v.z;
+}
+
 struct BdptBuf {
   int P = 0, cap_sq = 0;
   float *ls, *cs;  // light / camera subpath state, PS_WORDS floats per path
   float* vs;       // stored light vertices, VS_WORDS floats per slot k * P + p (k < kVMax)
-  // extension-ray queues (double buffered)
+  float* cv;       // overlapped schedule: stored camera vertices, CV_WORDS floats per slot j * P + p (j < kCvMax)
+  // extension-ray queues (double buffered).  The overlapped schedule gives the
+  // camera pass its own pair (qc_*); its kernels see them as q_* (camera_view)
   float *q_o[2], *q_d[2], *q_t[2];
   int *q_path[2], *q_prim[2];
+  float *qc_o[2], *qc_d[2], *qc_t[2];
+  int *qc_path[2], *qc_prim[2];
   // shadow + aux closest-hit queue (splat / connection / NEE / DI-BSDF)
   // shadow / aux queue and DI records, two each: the ones of step `slot` are
   // [slot & 1], so a step's resolve and the next step's vertex shading (which
@@ -109,7 +151,20 @@ struct BdptArgs {
                    // them at local index l = p - base (stride B.P >= n)
   uint32_t seed, iter;
   int ctl, maxlen, faithful;
+  int overlap = 0;  // 1: the overlapped schedule (light splats into the step's sq, CV store, light-side connections)
 };
+// The camera kernels of the overlapped schedule read and write the camera
+// pass's own extension queues under the q_* names
+__host__ __device__ inline BdptBuf camera_view(BdptBuf B) {
+  for (int q = 0; q < 2; ++q) {
+    B.q_o[q] = B.qc_o[q];
+    B.q_d[q] = B.qc_d[q];
+    B.q_t[q] = B.qc_t[q];
+    B.q_path[q] = B.qc_path[q];
+    B.q_prim[q] = B.qc_prim[q];
+  }
+  return B;
+}
 struct BdptGroup {
   BdptArgs a[kGroup];
 };
@@ -201,6 +256,86 @@ __device__ __forceinline__ bool sample_scatter(const DevScene& S, Rng& rng, cons
   return true;
 }
 
+// connectVertices (:610-665) for one (camera vertex, stored light vertex)
+// pair of path p: the camera vertex's BSDF b at hp with its state (cthr,
+// cdvcm, cdvc, cnspec, length len) and light-vertex slot `slot` of length
+// llen.  True when the shadow ray is cast (its contribution counts, or every
+// ray is traced: faithful); sdir / stgt / sval then hold the ray and the value
+// splatted if unoccluded.  One function for both sides of the overlapped
+// schedule, so a pair's floats do not depend on which vertex came second.
+__device__ __forceinline__ bool connect_pair(const BdptArgs& A, const Bsdf& b, V3 hp, V3 cthr, float cdvcm, float cdvc,
+                                             int cnspec, int len, int slot, int llen, V3& sdir, V3& stgt, V3& sval) {
+  const BdptBuf& B = A.B;
+  const DevScene& S = A.S;
+  bool shoot = false;
+  const V3 lpos = vld3(B.vs, slot, VS_POS);
+  V3 dir = lpos - hp;
+  const float d2 = sqr_len(dir);
+  const float dist = sqrtf(d2);
+  dir = div_guarded(dir, dist);
+  float cos_c = 0.f, cdp, crp;
+  const V3 cf = bsdf_f(b, S.mats, dir, &cos_c, &cdp, &crp);
+  if (!black(cf)) {
+    cdp *= b.cont;
+    crp *= b.cont;
+    Bsdf lb;
+    lb.mat = vsi(B.vs, slot, VS_MAT);
+    lb.fr = frame_from_z(vld3(B.vs, slot, VS_N));
+    lb.wi = vld3(B.vs, slot, VS_WI);
+    lb.pd = vsf(B.vs, slot, VS_PD);
+    lb.pg = vsf(B.vs, slot, VS_PG);
+    lb.cont = vsf(B.vs, slot, VS_CONT);
+    float cos_l = 0.f, ldp, lrp;
+    const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
+    if (!black(lf)) {
+      ldp *= lb.cont;
+      lrp *= lb.cont;
+      const float G = cos_l * cos_c / d2;
+      if (!(cmpf(G) < 0)) {
+        const float cdpa = cdp * fabsf(cos_l) / (dist * dist);
+        const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
+        const V3 res = mul(cf, lf) * G;
+        if (!black(res)) {
+          const float wl = cdpa * (vsf(B.vs, slot, VS_DVCM) + lrp * vsf(B.vs, slot, VS_DVC));
+          const float wc = ldpa * (cdvcm + crp * cdvc);
+          const float w = WR_TEST_CONN_W / (wl + 1.f + wc);
+          const bool counts = len_ok(A.ctl, llen + 1 + len);
+          if (counts || A.faithful) {
+            shoot = true;
+            sdir = normalize(dir);
+            stgt = hp + dir * dist;
+            if (counts) {
+              const float wlen = 1.f / (static_cast<float>(llen) + 1.f + static_cast<float>(len) -
+                                        static_cast<float>(vsi(B.vs, slot, VS_NSPEC)) - static_cast<float>(cnspec));
+              const V3 lthr = vld3(B.vs, slot, VS_THR);
+              sval = mul(mul(cthr, lthr), res * w) * wlen;
+            }
+          }
+        }
+      }
+    }
+  }
+  return shoot;
+}
+
+// queue a connection's shadow ray (every lane of the wave calls it)
+__device__ __forceinline__ void queue_connection(const BdptArgs& A, int qslot, bool shoot, int p, int pix, V3 hp,
+                                                 V3 sdir, V3 stgt, V3 sval) {
+  const BdptBuf& B = A.B;
+  const BdptBuf::Sq& Q = B.sq[qslot & 1];
+  const int cap = B.cap_sq;
+  const int si = wave_append(&A.sc->sq[qslot], shoot);
+  if (shoot) {
+    st3(Q.o, cap, si, hp);
+    st3(Q.d, cap, si, sdir);
+    st3(Q.tgt, cap, si, stgt);
+    st3(Q.val, cap, si, sval);
+    Q.cut[si] = occl_cut(hp, stgt, dot(stgt - hp, sdir));
+    Q.meta[si] = (SQ_CONN << 30) | p;
+    Q.pix[si] = pix;
+  }
+}
+
 // One light-subpath vertex (:77-128): path p's ray (o, d) hit prim at t
 // (prim < 0: a miss, or a pending hard ray -- nothing to do).  Every lane of
 // the wave calls it (queue appends).  oslot: the step whose queue gets the
@@ -212,6 +347,7 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
   bool ext = false, splat = false;
   V3 e_o, e_d, s_o, s_d, s_val;
   int s_pix = -1;
+  int lconn = 0, lslot = -1, llen = 0;  // overlapped: the stored vertex's slot, camera vertices to connect
   if (prim >= 0) {
     const Hit h = rebuild_hit(S, prim, t, o, d);
     Bsdf b;
@@ -239,6 +375,11 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
         vsi(B.vs, slot, VS_NSPEC) = nspec;
         vsi(B.vs, slot, VS_MAT) = b.mat;
         psi(B.ls, p, PS_VCOUNT) = k + 1;
+        if (A.overlap) {  // the camera vertices stored at earlier steps (lengths < len)
+          lslot = slot;
+          llen = len;
+          lconn = psi(B.cs, p, PS_CVCOUNT);
+        }
         if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
           const DCam& cam = S.cam;
           const V3 ip = t_point(cam.w2r, h.p);
@@ -305,9 +446,12 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
     st3(B.q_d[nxt], P, ei, e_d);
     B.q_path[nxt][ei] = p;
   }
-  const int si = wave_append(&A.sc->sq[kCamSlot], splat);  // traced with the camera primaries
+  // sequential schedule: traced with the camera primaries; overlapped: with
+  // the next step's extension rays, like the camera vertices' rays
+  const int sslot = A.overlap ? kCamSlot + oslot : kCamSlot;
+  const int si = wave_append(&A.sc->sq[sslot], splat);
   if (splat) {
-    const BdptBuf::Sq& Q = B.sq[kCamSlot & 1];
+    const BdptBuf::Sq& Q = B.sq[sslot & 1];
     st3(Q.o, B.cap_sq, si, s_o);
     st3(Q.d, B.cap_sq, si, s_d);
     st3(Q.tgt, B.cap_sq, si, S.cam.pos);
@@ -315,6 +459,35 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
     Q.cut[si] = occl_cut(s_o, S.cam.pos, dot(S.cam.pos - s_o, s_d));
     Q.meta[si] = (SQ_SPLAT << 30) | p;  // (the local path: diagnostics only)
     Q.pix[si] = s_pix;
+  }
+  // overlapped schedule: this light vertex connects to the path's camera
+  // vertices stored at earlier steps (:219-257 reached from the camera side)
+  if (A.overlap && __ballot(lconn > 0)) {
+    for (int j = 0; __ballot(j < lconn); ++j) {
+      bool shoot = false;
+      int pix = -1;
+      V3 hp{}, sdir{}, stgt{}, sval{};
+      if (j < lconn) {
+        const int cs = j * P + p;
+        const int clen = cvi(B.cv, cs, CV_LEN);
+        if (llen + 1 + clen > A.maxlen) {
+          lconn = j;  // camera vertices are stored by increasing length
+        } else {
+          Bsdf cb;
+          cb.mat = cvi(B.cv, cs, CV_MAT);
+          cb.fr = frame_from_z(cvld3(B.cv, cs, CV_N));
+          cb.wi = cvld3(B.cv, cs, CV_WI);
+          cb.pd = cvf(B.cv, cs, CV_PD);
+          cb.pg = cvf(B.cv, cs, CV_PG);
+          cb.cont = cvf(B.cv, cs, CV_CONT);
+          hp = cvld3(B.cv, cs, CV_POS);
+          pix = cvi(B.cv, cs, CV_PIX);
+          shoot = connect_pair(A, cb, hp, cvld3(B.cv, cs, CV_THR), cvf(B.cv, cs, CV_DVCM), cvf(B.cv, cs, CV_DVC),
+                               cvi(B.cv, cs, CV_NSPEC), clen, lslot, llen, sdir, stgt, sval);
+        }
+      }
+      queue_connection(A, sslot, shoot, p, pix, hp, sdir, stgt, sval);
+    }
   }
 }
 
@@ -400,6 +573,7 @@ __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
   psi(B.cs, l, PS_NSPEC) = 0;
   psu(B.cs, l, PS_CTR) = rng.ctr;
   psi(B.cs, l, PS_PIX) = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
+  psi(B.cs, l, PS_CVCOUNT) = 0;  // (BDPT only: VertexCM's camera gen sets PS_DVM here after this)
   st3(B.q_o[0], P, s, cam.pos + d * WR_EPS);
   st3(B.q_d[0], P, s, normalize(d));
   B.q_path[0][s] = l;
@@ -539,6 +713,26 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
         if (!b.delta) {
           conn_phase = true;
           nv = psi(B.ls, p, PS_VCOUNT);
+          // overlapped schedule: a vertex a later light vertex may still meet
+          // (len < l, l + 1 + len <= maxlen) is kept for that light vertex
+          if (A.overlap && 2 * len + 2 <= A.maxlen) {
+            const int j = psi(B.cs, p, PS_CVCOUNT);
+            const int cs = j * P + p;
+            cvst3(B.cv, cs, CV_POS, hp);
+            cvst3(B.cv, cs, CV_N, h.n);
+            cvst3(B.cv, cs, CV_WI, b.wi);
+            cvst3(B.cv, cs, CV_THR, cthr);
+            cvf(B.cv, cs, CV_DVCM) = cdvcm;
+            cvf(B.cv, cs, CV_DVC) = cdvc;
+            cvf(B.cv, cs, CV_CONT) = b.cont;
+            cvf(B.cv, cs, CV_PD) = b.pd;
+            cvf(B.cv, cs, CV_PG) = b.pg;
+            cvi(B.cv, cs, CV_LEN) = len;
+            cvi(B.cv, cs, CV_NSPEC) = cnspec;
+            cvi(B.cv, cs, CV_MAT) = b.mat;
+            cvi(B.cv, cs, CV_PIX) = pix;
+            psi(B.cs, p, PS_CVCOUNT) = j + 1;
+          }
         }
         V3 so = ld3r(B.cs, p, PS_O), sd = ld3r(B.cs, p, PS_D);
         if (sample_scatter(S, rng, b, hp, so, sd, thr, dvcm, dvc, nspec)) {
@@ -585,66 +779,10 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
         if (llen + 1 + len > A.maxlen) {
           nv = k;  // break (:237-239)
         } else {
-          // connectVertices (:610-665)
-          const V3 lpos = vld3(B.vs, slot, VS_POS);
-          V3 dir = lpos - hp;
-          const float d2 = sqr_len(dir);
-          const float dist = sqrtf(d2);
-          dir = div_guarded(dir, dist);
-          float cos_c = 0.f, cdp, crp;
-          const V3 cf = bsdf_f(b, S.mats, dir, &cos_c, &cdp, &crp);
-          if (!black(cf)) {
-            cdp *= b.cont;
-            crp *= b.cont;
-            Bsdf lb;
-            lb.mat = vsi(B.vs, slot, VS_MAT);
-            lb.fr = frame_from_z(vld3(B.vs, slot, VS_N));
-            lb.wi = vld3(B.vs, slot, VS_WI);
-            lb.pd = vsf(B.vs, slot, VS_PD);
-            lb.pg = vsf(B.vs, slot, VS_PG);
-            lb.cont = vsf(B.vs, slot, VS_CONT);
-            float cos_l = 0.f, ldp, lrp;
-            const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
-            if (!black(lf)) {
-              ldp *= lb.cont;
-              lrp *= lb.cont;
-              const float G = cos_l * cos_c / d2;
-              if (!(cmpf(G) < 0)) {
-                const float cdpa = cdp * fabsf(cos_l) / (dist * dist);
-                const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
-                const V3 res = mul(cf, lf) * G;
-                if (!black(res)) {
-                  const float wl = cdpa * (vsf(B.vs, slot, VS_DVCM) + lrp * vsf(B.vs, slot, VS_DVC));
-                  const float wc = ldpa * (cdvcm + crp * cdvc);
-                  const float w = WR_TEST_CONN_W / (wl + 1.f + wc);
-                  const bool counts = len_ok(A.ctl, llen + 1 + len);
-                  if (counts || A.faithful) {
-                    shoot = true;
-                    sdir = normalize(dir);
-                    stgt = hp + dir * dist;
-                    if (counts) {
-                      const float wlen = 1.f / (static_cast<float>(llen) + 1.f + static_cast<float>(len) -
-                                                static_cast<float>(vsi(B.vs, slot, VS_NSPEC)) - static_cast<float>(cnspec));
-                      const V3 lthr = vld3(B.vs, slot, VS_THR);
-                      sval = mul(mul(cthr, lthr), res * w) * wlen;
-                    }
-                  }
-                }
-              }
-            }
-          }
+          shoot = connect_pair(A, b, hp, cthr, cdvcm, cdvc, cnspec, len, slot, llen, sdir, stgt, sval);
         }
       }
-      const int si = wave_append(&A.sc->sq[oslot], shoot);
-      if (shoot) {
-        st3(Q.o, cap, si, hp);
-        st3(Q.d, cap, si, sdir);
-        st3(Q.tgt, cap, si, stgt);
-        st3(Q.val, cap, si, sval);
-        Q.cut[si] = occl_cut(hp, stgt, dot(stgt - hp, sdir));
-        Q.meta[si] = (SQ_CONN << 30) | p;
-        Q.pix[si] = pix;
-      }
+      queue_connection(A, oslot, shoot, p, pix, hp, sdir, stgt, sval);
     }
   }
   if (live) {  // commit scattered state (:259-260) and the loop increment

@@ -555,6 +555,8 @@ struct wr_context {
   bool verify = false;      // WR_BVH_VERIFY=1: every BVH answer checked against the KD walk
   // BDPT hard rays off the critical path (env WR_DEFER=1; off by default)
   int defer = -1;
+  // BDPT light and camera passes overlapped (wr_bdpt.h; env WR_BDPT_OVERLAP=0: sequential)
+  bool bdpt_overlap = true;
   float* api_t2 = nullptr;  // t2 scratch of the API path
   size_t api_t2_cap = 0;
   int2* api_spill = nullptr;  // the API path's search stack spill area
@@ -624,13 +626,29 @@ __global__ void __launch_bounds__(256) k_film_accumulate(float* dst, const float
   for (size_t i = blockIdx.x * size_t(256) + threadIdx.x; i < n; i += size_t(gridDim.x) * 256) dst[i] += src[i];
 }
 
-void layout_bdpt(Arena& a, BdptBuf& B, int P) {
+// overlapped: the BDPT render's own layout (the camera pass's extension queues
+// and the camera-vertex store); VertexCM's BDPT part runs the sequential
+// schedule and goes without them
+void layout_bdpt(Arena& a, BdptBuf& B, int P, bool overlapped) {
   B.P = P;
-  B.cap_sq = P * (kVMax + 2);  // per camera vertex: <= kVMax connections + NEE + DI-BSDF
+  // shadow / aux rays queued by one step, per path: sequential schedule, a
+  // camera vertex's <= kVMax connections + NEE + DI-BSDF (the light splats of
+  // one path: <= kVMax); overlapped, at the step making vertices of length s:
+  // camera side <= min(s, 9 - s) connections + NEE + DI-BSDF, light side
+  // <= min(s - 1, 9 - s) connections + its splat: <= 11 as well
+  B.cap_sq = P * (kVMax + 2);
   const size_t sP = P, sV = size_t(kVMax) * P, sQ = B.cap_sq;
   B.ls = a.take<float>(PS_WORDS * sP);
   B.cs = a.take<float>(PS_WORDS * sP);
   B.vs = a.take<float>(VS_WORDS * sV);
+  B.cv = overlapped ? a.take<float>(CV_WORDS * size_t(kCvMax) * P) : nullptr;
+  for (int q = 0; q < 2; ++q) {
+    B.qc_o[q] = overlapped ? a.take<float>(3 * sP) : nullptr;
+    B.qc_d[q] = overlapped ? a.take<float>(3 * sP) : nullptr;
+    B.qc_t[q] = overlapped ? a.take<float>(sP) : nullptr;
+    B.qc_path[q] = overlapped ? a.take<int>(sP) : nullptr;
+    B.qc_prim[q] = overlapped ? a.take<int>(sP) : nullptr;
+  }
 
   for (int q = 0; q < 2; ++q) {
     B.q_o[q] = a.take<float>(3 * sP);
@@ -730,13 +748,13 @@ void layout_set(Arena& a, Pipe* dst, int g, int kind, int P) {
     layout_pt(a, dst ? dst->pb[g] : t, P);
     return;
   }
-  layout_bdpt(a, dst ? dst->bb[g] : b, P);
+  layout_bdpt(a, dst ? dst->bb[g] : b, P, kind == 1);
   if (kind == 3) layout_vcm(a, dst ? dst->vb[g] : v, P);
 }
 
 int ensure_work(Pipe& p, int kind, int P, int sets) {
-  // a VCM layout starts with the complete BDPT layout, so it serves BDPT too
-  const bool same = p.work_kind == kind || (kind == 1 && p.work_kind == 3);
+  // (a VCM layout holds the sequential BDPT layout only: no camera-pass queues)
+  const bool same = p.work_kind == kind;
   if (same && p.work_key == static_cast<size_t>(P) && p.work_sets >= sets) return WR_OK;
   p.work_kind = 0;
   auto lay = [&](Arena& a, Pipe* dst) {
@@ -1444,6 +1462,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   if (const char* e = std::getenv("WR_TIE_WAVE_MAX")) c->tie_wave_max = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("WR_ISSUE_THREADS")) c->issue_threads = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   if (const char* e = std::getenv("WR_DEFER")) c->defer = std::atoi(e) != 0 ? 1 : 0;
+  if (const char* e = std::getenv("WR_BDPT_OVERLAP")) c->bdpt_overlap = std::atoi(e) != 0;
   if (const char* e = std::getenv("WR_RESOLVE_GRID")) c->resolve_blocks = std::max(0, std::atoi(e));  // per CU; scaled below
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
@@ -2048,7 +2067,8 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
      // Laid out on every pipeline that fits, as the work buffers are: a short
      // render (a warm-up) on few of them leaves nothing to allocate to a long one
     const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
-    const size_t per = kGroup * (std::max(cap_sq, size_t(cap)) + size_t(cap));
+    // (+ the camera pass's extension queue: the overlapped schedule traces both passes' at once)
+    const size_t per = kGroup * (std::max(cap_sq, size_t(cap)) + 2 * size_t(cap));
     for (int i = 0; i < fit; ++i)
       if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
   }
@@ -2062,7 +2082,10 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   // hides under the next search instead of lengthening the chain.  A path is
   // deferred once per pass, and each pass gets one step more (the light pass a
   // bounce step, the camera pass extension rays at its last step).
-  const bool defer = c->fast_on && !c->stamps && defer_enabled(c, np);
+  // The overlapped schedule (wr_bdpt.h; WR_BDPT_OVERLAP=0: the sequential one,
+  // which the deferred hard rays need)
+  const bool overlap = c->bdpt_overlap && !(c->fast_on && !c->stamps && defer_enabled(c, np));
+  const bool defer = !overlap && c->fast_on && !c->stamps && defer_enabled(c, np);
   if (defer)
     for (int i = 0; i < fit; ++i)
       if (int rc = ensure_late(c->pipes[i], cap, late_records(cap))) return rc;
@@ -2080,6 +2103,7 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   A0.ctl = prm->control_length;
   A0.maxlen = prm->max_path_length > 0 ? prm->max_path_length : 10;
   A0.faithful = prm->faithful;
+  A0.overlap = overlap ? 1 : 0;
   const int maxlen = A0.maxlen;
   const bool count = prm->count_work != 0;
   // One group of pieces on one pipeline, issued step by step: step 0 clears
@@ -2089,13 +2113,60 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   struct GroupIssue {
     Pipe* pp = nullptr;
     BdptGroup GA;
+    BdptGroup GC;  // overlapped: the camera kernels' view (camera_view: their own extension queues)
     int gn = 0, nmax = 0;
     bool late[kSlots] = {};  // late work issued at step slot
   };
-  // steps: light gen, light bounces b = 0 .. lb_n - 1, camera gen, camera bounces b = 0 .. maxlen
+  // steps: light gen, light bounces b = 0 .. lb_n - 1, camera gen, camera bounces b = 0 .. maxlen;
+  // overlapped: both gens, then bounces b = 0 .. maxlen of both passes together
   const int lb_n = maxlen - 1 + (defer ? 1 : 0);
-  const int nsteps = lb_n + maxlen + 3;
+  const int nsteps = overlap ? maxlen + 2 : lb_n + maxlen + 3;
+  // The overlapped schedule: step 0 starts both subpaths of every path; step
+  // b + 1 traces, per group member, the shadow / aux rays queued by the
+  // vertices of bounce b - 1 (sq slot kCamSlot + b: light splats and
+  // connections, camera DI rays and connections), the light pass's extension
+  // rays of bounce b (b <= maxlen - 2) and the camera pass's (b < maxlen),
+  // then shades the light vertices of bounce b and after them (same stream)
+  // resolves the step's shadow / aux rays and shades its camera vertices.
+  auto issue_overlap = [&](GroupIssue& G, int step) -> int {
+    Pipe& pp = *G.pp;
+    const hipStream_t sm = pp.stream;
+    Timer tm(c, &pp);
+    const int gn = G.gn;
+    const BdptArgs* A = G.GA.a;
+    const int g = shade_grid(c, G.nmax);
+    if (step == 0) {
+      HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
+      hipLaunchKernelGGL(k_light_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA);
+      hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GC);
+      tm.mark(WR_K_GEN);
+      return WR_OK;
+    }
+    const int b = step - 1, slot = kCamSlot + b;
+    const bool light = b <= maxlen - 2, more = b < maxlen;
+    QueueList ql;
+    for (int m = 0; m < gn; ++m) {
+      const BdptBuf& B = pp.bb[m];
+      const BdptBuf::Sq& Q = B.sq[slot & 1];
+      ql.add(rq(Q.o, Q.d, B.cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut), A[m].n * (kVMax + 2));
+      if (light)
+        ql.add(rq(B.q_o[b & 1], B.q_d[b & 1], B.P, &pp.sc[m].ext[b], B.q_t[b & 1], B.q_prim[b & 1]), A[m].n);
+      if (more)
+        ql.add(rq(B.qc_o[slot & 1], B.qc_d[slot & 1], B.P, &pp.sc[m].ext[slot], B.qc_t[slot & 1], B.qc_prim[slot & 1]),
+               A[m].n);
+    }
+    trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE, false, nullptr,
+                 gn);
+    LateArgs L{};
+    if (light) hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA, b, L, 0);
+    const int nres = shade_grid(c, G.nmax * (kVMax + 2));
+    hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, G.GC, slot, nres,
+                       more ? 1 : 0, L, 0);
+    tm.mark(WR_K_SHADE);
+    return WR_OK;
+  };
   auto issue = [&](GroupIssue& G, int step) -> int {
+    if (overlap) return issue_overlap(G, step);
     Pipe& pp = *G.pp;
     const hipStream_t sm = pp.stream;
     Timer tm(c, &pp);
@@ -2204,6 +2275,8 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
         a.iter = static_cast<uint32_t>(prm->iter_begin + pc.iter);
         a.base = pc.base;
         a.n = pc.n;
+        G.GC.a[m] = a;
+        G.GC.a[m].B = camera_view(a.B);
         G.nmax = std::max(G.nmax, pc.n);
       }
       live += G.gn > 0;
@@ -2660,7 +2733,7 @@ static int reserve_one(wr_context* c, int kind, int W, int H) {
   }
   if (fit < 1) return WR_E_HIP;  // message set by the allocation
   const size_t cap_sq = size_t(c->pipes[0].bb[0].cap_sq);
-  const size_t per = kGroup * (std::max(cap_sq, size_t(cap)) + size_t(cap));
+  const size_t per = kGroup * (std::max(cap_sq, size_t(cap)) + 2 * size_t(cap));
   for (int i = 0; i < fit; ++i)
     if (int rc = ensure_t2(c, c->pipes[i], per)) return rc;
   if (kind == WR_INTEGRATOR_BDPT && c->fast_on && !c->stamps && defer_enabled(c, fit))

@@ -225,8 +225,10 @@ __device__ __forceinline__ float occl_cut(V3 o, V3 tgt, float dist) {
 // The queues of one traversal launch, fetched in order (the shadow / aux queue
 // of an iteration first: its long rays start early and overlap the extension
 // rays instead of forming a tail of their own).
+// (6: the overlapped BDPT schedule traces, per group member, the shadow / aux
+// queue and both passes' extension queues in one launch)
 #ifndef WR_MAX_QUEUES
-#define WR_MAX_QUEUES 4
+#define WR_MAX_QUEUES 6
 #endif
 constexpr int kMaxQueues = WR_MAX_QUEUES;
 struct TraceQueues {
