@@ -689,22 +689,26 @@ __device__ WR_HARD_CALL void kd_first_leaves(const DevScene& S, const FastScene&
         }
         continue;
       }
-      // leaf: which wanted primitives does it hold?
+      // leaf: which wanted primitives does it hold?  Its own reference list
+      // (ref_c.y: the primitive, in the leaf's order) read 8 entries per
+      // round trip -- one for the usual leaf -- instead of a binary search of
+      // each candidate's ascending leaf list (~12 dependent loads per
+      // candidate on the 1M-triangle tree); a primitive listed twice keeps its
+      // first position, as prim_leaf_pos does
       ++visit;
-      const int off = F.node_path[node];
-      for (int c = 0; c < kTie; ++c) {
-        if (!((want >> c) & 1u)) continue;
-        int a = F.prim_leaf_off[cp[c]], b = F.prim_leaf_off[cp[c] + 1];
-        while (a < b) {
-          const int mid = (a + b) >> 1;
-          if (F.prim_leaf[mid] < off) a = mid + 1;
-          else b = mid;
-        }
-        if (a < F.prim_leaf_off[cp[c] + 1] && F.prim_leaf[a] == off) {
-          vis[c] = visit;
-          pos[c] = F.prim_leaf_pos[a];
-          want &= ~(1u << c);
-        }
+      const uint32_t first = w.x, cnt = w.y >> 2;
+      for (uint32_t j0 = 0; j0 < cnt && want; j0 += 8) {
+        int pr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pr[u] = j0 + u < cnt ? __float_as_int(S.ref_c[first + j0 + u].y) : -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          for (int c = 0; c < kTie; ++c)
+            if (((want >> c) & 1u) && pr[u] == cp[c]) {
+              vis[c] = visit;
+              pos[c] = static_cast<int>(j0) + u;
+              want &= ~(1u << c);
+            }
       }
       if (!want) return;
       pop = true;
