@@ -10,6 +10,7 @@
 // Build: g++ -O2 -std=c++17 -I winmad-s-raytracer-v1.0_amd/csrc -I include
 //   scripts/bvh_cost.cpp winmad-s-raytracer-v1.0_amd/csrc/{wr_scene,wr_bvh}.cpp -lpthread
 // Usage: bvh_cost scene [rays]
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -108,6 +109,117 @@ void walk(const wrf::FastHost& F, V o, V d, Cost& c) {
     if (cur == 0x7fffffff) return;
   }
 }
+// W-wide trees collapsed from the binary one (as wr_bvh.cpp's Collapse does
+// for W = 4: open the inner child of largest area until W children), walked
+// the same way: children hit sorted by entry t, nearest next, the rest pushed
+struct Wide {
+  struct Node {
+    float b[8][6];
+    int c[8];
+    int n;
+  };
+  std::vector<Node> nodes;
+  int W;
+  const wrf::FastHost& F;
+  Wide(const wrf::FastHost& f, int w) : W(w), F(f) { build(0); }
+  static double area(const float* b) {
+    if (!(b[0] <= b[3])) return 0.0;
+    const double x = b[3] - b[0], y = b[4] - b[1], z = b[5] - b[2];
+    return 2.0 * (x * y + x * z + y * z);
+  }
+  int build(int n2) {
+    struct K {
+      float b[6];
+      int link;
+    };
+    std::vector<K> ks;
+    auto kid = [&](int n, int side) {
+      K k;
+      std::memcpy(k.b, F.nodes[static_cast<size_t>(n)].b + 6 * side, sizeof k.b);
+      k.link = F.nodes[static_cast<size_t>(n)].c[side];
+      return k;
+    };
+    ks.push_back(kid(n2, 0));
+    ks.push_back(kid(n2, 1));
+    while (static_cast<int>(ks.size()) < W) {
+      int best = -1;
+      double ba = -1;
+      for (size_t i = 0; i < ks.size(); ++i)
+        if (ks[i].link >= 0 && area(ks[i].b) > ba) {
+          ba = area(ks[i].b);
+          best = static_cast<int>(i);
+        }
+      if (best < 0) break;
+      const int open = ks[static_cast<size_t>(best)].link;
+      ks[static_cast<size_t>(best)] = kid(open, 0);
+      ks.push_back(kid(open, 1));
+    }
+    const int at = static_cast<int>(nodes.size());
+    nodes.emplace_back();
+    std::vector<int> links;
+    for (const K& k : ks) links.push_back(k.link >= 0 ? build(k.link) : k.link);
+    Node& d = nodes[static_cast<size_t>(at)];
+    d.n = static_cast<int>(ks.size());
+    for (int i = 0; i < d.n; ++i) {
+      std::memcpy(d.b[i], ks[static_cast<size_t>(i)].b, sizeof d.b[i]);
+      d.c[i] = links[static_cast<size_t>(i)];
+    }
+    return at;
+  }
+  void walk(V o, V d, Cost& c, double& leaves) const {
+    const V inv{1.f / d.x, 1.f / d.y, 1.f / d.z};
+    float t1 = INFINITY;
+    struct E {
+      int link;
+      float t;
+    } st[512];
+    int sp = 0, cur = 0;
+    auto hi = [&]() { return t1 + 2.f * kEps; };
+    auto slab = [&](const float* b, float& tn) {
+      const float x0 = (b[0] - o.x) * inv.x, x1 = (b[3] - o.x) * inv.x;
+      const float y0 = (b[1] - o.y) * inv.y, y1 = (b[4] - o.y) * inv.y;
+      const float z0 = (b[2] - o.z) * inv.z, z1 = (b[5] - o.z) * inv.z;
+      tn = std::fmax(std::fmax(std::fmin(x0, x1), std::fmin(y0, y1)), std::fmax(std::fmin(z0, z1), 0.f));
+      const float tf = std::fmin(std::fmin(std::fmax(x0, x1), std::fmax(y0, y1)), std::fmin(std::fmax(z0, z1), hi()));
+      return tn <= tf;
+    };
+    for (;;) {
+      if (cur >= 0) {
+        c.nodes += 1;
+        const Node& n = nodes[static_cast<size_t>(cur)];
+        E hit[8];
+        int nh = 0;
+        for (int i = 0; i < n.n; ++i) {
+          float t;
+          if (slab(n.b[i], t)) hit[nh++] = {n.c[i], t};
+        }
+        std::sort(hit, hit + nh, [](const E& a, const E& b) { return a.t < b.t; });
+        if (nh > 0) {
+          for (int i = nh - 1; i >= 1; --i) st[sp++] = hit[i];
+          cur = hit[0].link;
+          continue;
+        }
+      } else {
+        leaves += 1;
+        const int l = ~cur, first = l >> 3, cnt = (l & 7) + 1;
+        for (int j = 0; j < cnt; ++j) {
+          c.tests += 1;
+          float t;
+          if (tri(F.tris[static_cast<size_t>(first + j)], o, d, t) && t < t1) t1 = t;
+        }
+      }
+      cur = 0x7fffffff;
+      while (sp > 0) {
+        --sp;
+        if (st[sp].t <= hi()) {
+          cur = st[sp].link;
+          break;
+        }
+      }
+      if (cur == 0x7fffffff) return;
+    }
+  }
+};
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -161,13 +273,19 @@ int main(int argc, char** argv) {
     cdf[i] = acc;
   }
   Cost cam, sec;
+  std::vector<Wide> wides;
+  for (int w : {4, 8}) wides.emplace_back(F, w);
+  std::vector<Cost> wcam(wides.size()), wsec(wides.size());
+  std::vector<double> wlv(wides.size(), 0.0);
   const V cpos = f3(s.cam.pos), cfwd = norm(f3(s.cam.fwd)), cup = norm(f3(s.cam.up));
   const V cright = norm(cross(cfwd, cup));
   const float th = std::tan(s.cam.fov * 0.5f * 3.14159265f / 180.f);
   for (int i = 0; i < nrays; ++i) {
     // camera ray: a random point of the image plane (same FOV scale on both axes)
     const float a = (2.f * U(rng) - 1.f) * th, b = (2.f * U(rng) - 1.f) * th * s.cam.yres / s.cam.xres;
-    walk(F, cpos, norm(add(cfwd, add(mul(cright, a), mul(cup, b)))), cam);
+    const V cd = norm(add(cfwd, add(mul(cright, a), mul(cup, b))));
+    walk(F, cpos, cd, cam);
+    for (size_t w = 0; w < wides.size(); ++w) wides[w].walk(cpos, cd, wcam[w], wlv[w]);
     // secondary ray: random surface point, cosine direction about a random side's normal
     const double x = U(rng) * acc;
     const size_t k = static_cast<size_t>(std::lower_bound(cdf.begin(), cdf.end(), x) - cdf.begin());
@@ -185,7 +303,12 @@ int main(int argc, char** argv) {
     const V dir = norm(add(mul(n, std::sqrt(1.f - r1)), add(mul(t1, rr * std::cos(ph)), mul(t2, rr * std::sin(ph)))));
     const V org = add(add(add(f3(p.p0), mul(e1, u)), mul(e2, v)), mul(dir, kEps));
     walk(F, org, dir, sec);
+    for (size_t w = 0; w < wides.size(); ++w) wides[w].walk(org, dir, wsec[w], wlv[w]);
   }
+  for (size_t w = 0; w < wides.size(); ++w)
+    std::printf("%d-wide: nodes %zu | mix(1:3) %.2f nodes %.2f tests %.2f leaves\n", wides[w].W, wides[w].nodes.size(),
+                (wcam[w].nodes + 3 * wsec[w].nodes) / (4.0 * nrays), (wcam[w].tests + 3 * wsec[w].tests) / (4.0 * nrays),
+                wlv[w] / (2.0 * nrays));
   std::printf("nodes %zu leaves %d depth %d sah %.2f | camera %.2f nodes %.2f tests | secondary %.2f nodes %.2f tests"
               " | mix(1:3) %.2f nodes %.2f tests\n",
               F.nodes.size(), F.leaves, F.depth, sah, cam.nodes / nrays, cam.tests / nrays, sec.nodes / nrays,
