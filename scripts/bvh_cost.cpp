@@ -166,7 +166,14 @@ struct Wide {
     }
     return at;
   }
+  mutable std::vector<long> sp_hist = std::vector<long>(64, 0);  // rays by their deepest stack
   void walk(V o, V d, Cost& c, double& leaves) const {
+    int spmax = 0;
+    struct Rec {
+      std::vector<long>& h;
+      int& m;
+      ~Rec() { ++h[static_cast<size_t>(std::min(m, 63))]; }
+    } rec{sp_hist, spmax};
     const V inv{1.f / d.x, 1.f / d.y, 1.f / d.z};
     float t1 = INFINITY;
     struct E {
@@ -196,6 +203,7 @@ struct Wide {
         std::sort(hit, hit + nh, [](const E& a, const E& b) { return a.t < b.t; });
         if (nh > 0) {
           for (int i = nh - 1; i >= 1; --i) st[sp++] = hit[i];
+          spmax = std::max(spmax, sp);
           cur = hit[0].link;
           continue;
         }
@@ -305,10 +313,19 @@ int main(int argc, char** argv) {
     walk(F, org, dir, sec);
     for (size_t w = 0; w < wides.size(); ++w) wides[w].walk(org, dir, wsec[w], wlv[w]);
   }
-  for (size_t w = 0; w < wides.size(); ++w)
-    std::printf("%d-wide: nodes %zu | mix(1:3) %.2f nodes %.2f tests %.2f leaves\n", wides[w].W, wides[w].nodes.size(),
-                (wcam[w].nodes + 3 * wsec[w].nodes) / (4.0 * nrays), (wcam[w].tests + 3 * wsec[w].tests) / (4.0 * nrays),
-                wlv[w] / (2.0 * nrays));
+  for (size_t w = 0; w < wides.size(); ++w) {
+    std::printf("%d-wide: nodes %zu | mix(1:3) %.2f nodes %.2f tests %.2f leaves | rays whose stack exceeds",
+                wides[w].W, wides[w].nodes.size(), (wcam[w].nodes + 3 * wsec[w].nodes) / (4.0 * nrays),
+                (wcam[w].tests + 3 * wsec[w].tests) / (4.0 * nrays), wlv[w] / (2.0 * nrays));
+    long tot = 0, above[4] = {0, 0, 0, 0};
+    const int lim[4] = {8, 12, 16, 24};
+    for (int k = 0; k < 64; ++k) {
+      tot += wides[w].sp_hist[static_cast<size_t>(k)];
+      for (int j = 0; j < 4; ++j) above[j] += k > lim[j] ? wides[w].sp_hist[static_cast<size_t>(k)] : 0;
+    }
+    for (int j = 0; j < 4; ++j) std::printf(" %d: %.2e", lim[j], double(above[j]) / double(tot));
+    std::printf("\n");
+  }
   std::printf("nodes %zu leaves %d depth %d sah %.2f | camera %.2f nodes %.2f tests | secondary %.2f nodes %.2f tests"
               " | mix(1:3) %.2f nodes %.2f tests\n",
               F.nodes.size(), F.leaves, F.depth, sah, cam.nodes / nrays, cam.tests / nrays, sec.nodes / nrays,

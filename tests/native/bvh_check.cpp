@@ -11,6 +11,9 @@
 #include "wr_bvh.h"
 #include "wr_scene.h"
 
+// an empty child slot: a point box far outside every scene (wr_bvh.cpp) or an inverted box
+static bool empty_slot(float lo0, float hi0) { return !(lo0 <= hi0) || (lo0 == 3e38f && hi0 == 3e38f); }
+
 static int fail(const std::string& m) {
   std::printf("FAIL %s\n", m.c_str());
   return 1;
@@ -56,7 +59,7 @@ int main(int argc, char** argv) {
   for (int c = 0; c < 2; ++c) {
     const wrf::BNode& n = f.nodes[0];
     It it{n.c[c], 1, {n.b[6 * c], n.b[6 * c + 1], n.b[6 * c + 2]}, {n.b[6 * c + 3], n.b[6 * c + 4], n.b[6 * c + 5]}};
-    if (it.lo[0] <= it.hi[0]) st.push_back(it);
+    if (!empty_slot(it.lo[0], it.hi[0])) st.push_back(it);
   }
   while (!st.empty()) {
     const It it = st.back();
@@ -102,7 +105,7 @@ int main(int argc, char** argv) {
     while (!s2.empty()) {
       const It it = s2.back();
       s2.pop_back();
-      if (!(it.lo[0] <= it.hi[0])) continue;  // empty slot
+      if (empty_slot(it.lo[0], it.hi[0])) continue;
       if (it.link >= 0) {
         const wrf::BNode& n = f.nodes[static_cast<size_t>(it.link)];
         for (int c = 0; c < 2; ++c)
@@ -126,7 +129,7 @@ int main(int argc, char** argv) {
       const wrf::BNode4& n = f.nodes4[static_cast<size_t>(it.node)];
       for (int k = 0; k < 4; ++k) {
         const float lo[3] = {n.lo[0][k], n.lo[1][k], n.lo[2][k]}, hi[3] = {n.hi[0][k], n.hi[1][k], n.hi[2][k]};
-        if (!(lo[0] <= hi[0])) continue;  // empty slot
+        if (empty_slot(lo[0], hi[0])) continue;
         for (int a = 0; a < 3; ++a)
           if (lo[a] < it.lo[a] || hi[a] > it.hi[a]) return fail("4-wide child box outside its parent's");
         if (n.c[k] >= 0) {

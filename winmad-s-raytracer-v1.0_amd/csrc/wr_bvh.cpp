@@ -486,9 +486,13 @@ struct Collapse {
     for (int i = 0; i < 4; ++i) links[i] = i < n && ks[i].link >= 0 ? node(ks[i].link, depth + 1) : (i < n ? ks[i].link : ~0);
     BNode4& d = out.nodes4[static_cast<size_t>(at)];
     for (int i = 0; i < 4; ++i) {
+      // an empty slot is a point far outside every scene: its slab interval is
+      // empty for every direction (an inverted [inf, -inf] box is not: its
+      // min / max per axis span the whole line, and the slot's link -1 would
+      // then test triangle 0 as a leaf)
       for (int a = 0; a < 3; ++a) {
-        d.lo[a][i] = i < n ? ks[i].lo[a] : INFINITY;
-        d.hi[a][i] = i < n ? ks[i].hi[a] : -INFINITY;
+        d.lo[a][i] = i < n ? ks[i].lo[a] : 3e38f;
+        d.hi[a][i] = i < n ? ks[i].hi[a] : 3e38f;
       }
       d.c[i] = links[i];
       d.pad[i] = 0;
@@ -567,8 +571,8 @@ void build_fast(const wr::Scene& s, FastHost& out) {
     for (int k = 0; k < 3; ++k) {
       nd.b[k] = all.lo[k];
       nd.b[3 + k] = all.hi[k];
-      nd.b[6 + k] = INFINITY;
-      nd.b[9 + k] = -INFINITY;
+      nd.b[6 + k] = 3e38f;  // a point far outside the scene: never hit (see Collapse)
+      nd.b[9 + k] = 3e38f;
     }
     nd.c[0] = l;
     nd.c[1] = ~0;  // never reached: empty box
