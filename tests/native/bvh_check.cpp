@@ -2,6 +2,9 @@
 // built and run by tests/test_bvh_host.py.  Prints "OK <stats>" or the first
 // violated property and exits non-zero.
 #include <algorithm>
+#include <map>
+#include <functional>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -147,6 +150,112 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < want.size(); ++i)
       if (want[i].first != got[i].first || std::memcmp(want[i].second.data(), got[i].second.data(), 24) != 0)
         return fail("4-wide tree leaves differ from the binary tree's");
+  }
+  // 2c. the 8-wide tree (built with -DWR_BVH_WIDE=8 only): the same leaves,
+  //     each once, every decoded child box fmaf(q, scale, org) CONTAINING the
+  //     binary tree's box of that child (the search's boxes only grow), inner
+  //     nodes' boxes holding their children's decoded boxes, depth <= depth8
+  if (!f.nodes8.empty()) {
+    std::vector<std::pair<int, std::vector<float>>> want, got;
+    std::vector<It> s2;
+    for (int c = 0; c < 2; ++c) {
+      const wrf::BNode& n = f.nodes[0];
+      s2.push_back(It{n.c[c], 1, {n.b[6 * c], n.b[6 * c + 1], n.b[6 * c + 2]}, {n.b[6 * c + 3], n.b[6 * c + 4], n.b[6 * c + 5]}});
+    }
+    while (!s2.empty()) {
+      const It it = s2.back();
+      s2.pop_back();
+      if (empty_slot(it.lo[0], it.hi[0])) continue;
+      if (it.link >= 0) {
+        const wrf::BNode& n = f.nodes[static_cast<size_t>(it.link)];
+        for (int c = 0; c < 2; ++c)
+          s2.push_back(It{n.c[c], 0, {n.b[6 * c], n.b[6 * c + 1], n.b[6 * c + 2]}, {n.b[6 * c + 3], n.b[6 * c + 4], n.b[6 * c + 5]}});
+      } else {
+        want.push_back({it.link, {it.lo[0], it.lo[1], it.lo[2], it.hi[0], it.hi[1], it.hi[2]}});
+      }
+    }
+    // every binary inner node's box by link, to check the decoded inner boxes too
+    std::vector<std::vector<float>> bin_box(f.nodes.size());
+    for (size_t i = 0; i < f.nodes.size(); ++i)
+      for (int c = 0; c < 2; ++c)
+        if (f.nodes[i].c[c] >= 0)
+          bin_box[static_cast<size_t>(f.nodes[i].c[c])] = {f.nodes[i].b[6 * c], f.nodes[i].b[6 * c + 1], f.nodes[i].b[6 * c + 2],
+                                                           f.nodes[i].b[6 * c + 3], f.nodes[i].b[6 * c + 4], f.nodes[i].b[6 * c + 5]};
+    struct It8 {
+      int node, depth;
+      float lo[3], hi[3];
+    };
+    std::vector<It8> s8{{0, 1, {-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}}};
+    int maxd8 = 0;
+    size_t visits = 0;
+    std::vector<std::pair<int, std::vector<float>>> leaf_dec;  // leaf link -> decoded box
+    bool bad_inner = false;
+    while (!s8.empty()) {
+      const It8 it = s8.back();
+      s8.pop_back();
+      if (++visits > f.nodes8.size()) return fail("8-wide tree has a cycle");
+      maxd8 = std::max(maxd8, it.depth);
+      const wrf::BNode8& n = f.nodes8[static_cast<size_t>(it.node)];
+      if (n.n < 1 || n.n > 8) return fail("8-wide child count");
+      for (int k = 0; k < n.n; ++k) {
+        float lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+          if (!(n.scale[a] > 0.f)) return fail("8-wide scale");
+          lo[a] = std::fma(static_cast<float>(n.qlo[a][k]), n.scale[a], n.org[a]);
+          hi[a] = std::fma(static_cast<float>(n.qhi[a][k]), n.scale[a], n.org[a]);
+          if (lo[a] > hi[a]) return fail("8-wide decoded box inverted");
+        }
+        (void)it;
+        if (n.c[k] >= 0) {
+          if (static_cast<size_t>(n.c[k]) >= f.nodes8.size()) return fail("8-wide link out of range");
+          s8.push_back(It8{n.c[k], it.depth + 1, {lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}});
+        } else {
+          got.push_back({n.c[k], {}});
+          leaf_dec.push_back({n.c[k], {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]}});
+        }
+      }
+    }
+    if (maxd8 > f.depth8) return fail("8-wide depth bound");
+    std::sort(want.begin(), want.end());
+    std::sort(leaf_dec.begin(), leaf_dec.end());
+    if (want.size() != leaf_dec.size()) return fail("8-wide tree leaf count");
+    for (size_t i = 0; i < want.size(); ++i) {
+      if (want[i].first != leaf_dec[i].first) return fail("8-wide tree leaves differ from the binary tree's");
+      for (int a = 0; a < 3; ++a)
+        if (leaf_dec[i].second[a] > want[i].second[a] || leaf_dec[i].second[3 + a] < want[i].second[3 + a])
+          return fail("8-wide decoded leaf box does not contain the binary box");
+    }
+    // inner children: each decoded box contains every binary leaf box beneath
+    // it (the union of its subtree's geometry); decoded boxes need not nest
+    std::map<int, std::vector<float>> leaf_box(want.begin(), want.end());
+    std::vector<std::array<float, 6>> sub(f.nodes8.size());
+    std::vector<char> done(f.nodes8.size(), 0);
+    std::function<std::array<float, 6>(int)> uni = [&](int nd) -> std::array<float, 6> {
+      if (done[static_cast<size_t>(nd)]) return sub[static_cast<size_t>(nd)];
+      std::array<float, 6> u{INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      const wrf::BNode8& n = f.nodes8[static_cast<size_t>(nd)];
+      for (int k = 0; k < n.n; ++k) {
+        std::array<float, 6> c;
+        if (n.c[k] >= 0) {
+          c = uni(n.c[k]);
+        } else {
+          const std::vector<float>& b = leaf_box[n.c[k]];
+          for (int a = 0; a < 6; ++a) c[static_cast<size_t>(a)] = b[static_cast<size_t>(a)];
+        }
+        for (int a = 0; a < 3; ++a) {
+          const float lo = std::fma(static_cast<float>(n.qlo[a][k]), n.scale[a], n.org[a]);
+          const float hi = std::fma(static_cast<float>(n.qhi[a][k]), n.scale[a], n.org[a]);
+          if (lo > c[static_cast<size_t>(a)] || hi < c[static_cast<size_t>(3 + a)]) bad_inner = true;
+          u[static_cast<size_t>(a)] = std::min(u[static_cast<size_t>(a)], c[static_cast<size_t>(a)]);
+          u[static_cast<size_t>(3 + a)] = std::max(u[static_cast<size_t>(3 + a)], c[static_cast<size_t>(3 + a)]);
+        }
+      }
+      done[static_cast<size_t>(nd)] = 1;
+      return sub[static_cast<size_t>(nd)] = u;
+    };
+    uni(0);
+    if (bad_inner) return fail("8-wide decoded box does not contain its subtree's leaf boxes");
+    (void)bin_box;
   }
   // 3. KD membership: each primitive's leaves (ascending), its position in
   //    each, and the leaf paths lead from the root to that leaf

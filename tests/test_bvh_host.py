@@ -18,7 +18,7 @@ _bin = {}
 
 
 def checker(wide=None):
-    """The checker built from the product's sources; wide=4 builds the 4-wide
+    """The checker built from the product's sources; wide=4 / 8 builds the 4- / 8-wide
     search tree (WR_BVH_WIDE=4) as well and checks it against the binary one."""
     key = wide or "default"
     if key not in _bin:
@@ -70,4 +70,14 @@ def test_bvh_parallel_build_equals_serial():
 
 def test_bvh_wide_tree_structure():
     r = subprocess.run([checker(4), _scenes.torus(64, 64)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("maker", [lambda: _scenes.torus(64, 64), lambda: _scenes.cbox(64, 48), small_torus],
+                         ids=["torus", "cbox_dragon", "synthetic_torus_40k"])
+def test_bvh_8wide_quantised_tree_structure(maker):
+    """The 8-wide search tree (WR_BVH_WIDE=8): the binary tree's leaves, each
+    once, every byte-quantised child box decoded with the device's formula
+    containing the binary box, children inside their parents."""
+    r = subprocess.run([checker(8), maker()], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr

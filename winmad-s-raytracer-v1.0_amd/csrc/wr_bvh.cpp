@@ -501,6 +501,100 @@ struct Collapse {
   }
 };
 
+// The 8-wide tree: as Collapse, up to eight children, their boxes quantised
+// outward to bytes on a per-node power-of-two grid (BNode8).
+struct Collapse8 {
+  FastHost& out;
+  struct Kid {
+    float lo[3], hi[3];
+    int link;
+    double area() const {
+      if (!(lo[0] <= hi[0])) return 0.0;
+      const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+      return 2.0 * (x * y + x * z + y * z);
+    }
+  };
+  Kid kid(int n2, int side) const {
+    const BNode& b = out.nodes[static_cast<size_t>(n2)];
+    Kid k;
+    for (int a = 0; a < 3; ++a) {
+      k.lo[a] = b.b[6 * side + a];
+      k.hi[a] = b.b[6 * side + 3 + a];
+    }
+    k.link = b.c[side];
+    return k;
+  }
+  static bool empty(const Kid& k) { return !(k.lo[0] <= k.hi[0]) || (k.lo[0] == 3e38f && k.hi[0] == 3e38f); }
+  // one axis of a node: the grid (org, scale) and each child's bytes, with the
+  // decoded faces fmaf(q, scale, org) holding the child's [lo, hi]
+  static void quantise(const Kid* ks, int n, int a, BNode8& d) {
+    float lo = INFINITY, hi = -INFINITY;
+    for (int i = 0; i < n; ++i) {
+      lo = std::min(lo, ks[i].lo[a]);
+      hi = std::max(hi, ks[i].hi[a]);
+    }
+    // the smallest power of two with (hi - lo) / scale <= 254 (one step spare
+    // for the outward corrections below)
+    int e = -126;
+    const double ext = static_cast<double>(hi) - static_cast<double>(lo);
+    while (std::ldexp(254.0, e) < ext) ++e;
+    for (;; ++e) {
+      const float sc = std::ldexp(1.f, e);
+      bool ok = true;
+      for (int i = 0; i < n && ok; ++i) {
+        double ql = std::floor((static_cast<double>(ks[i].lo[a]) - lo) / sc);
+        double qh = std::ceil((static_cast<double>(ks[i].hi[a]) - lo) / sc);
+        ql = std::max(0.0, ql);
+        while (ql > 0 && std::fma(static_cast<float>(ql), sc, lo) > ks[i].lo[a]) ql -= 1;
+        while (qh <= 255 && std::fma(static_cast<float>(qh), sc, lo) < ks[i].hi[a]) qh += 1;
+        if (std::fma(static_cast<float>(ql), sc, lo) > ks[i].lo[a] || qh > 255) {
+          ok = false;
+          break;
+        }
+        d.qlo[a][i] = static_cast<uint8_t>(ql);
+        d.qhi[a][i] = static_cast<uint8_t>(qh);
+      }
+      if (ok) {
+        d.org[a] = lo;
+        d.scale[a] = sc;
+        return;
+      }
+    }
+  }
+  int node(int n2, int depth) {
+    out.depth8 = std::max(out.depth8, depth);
+    Kid ks[8] = {kid(n2, 0), kid(n2, 1)};
+    int n = 2;
+    while (n < 8) {
+      int best = -1;
+      double ba = -1.0;
+      for (int i = 0; i < n; ++i)
+        if (ks[i].link >= 0 && ks[i].area() > ba) {
+          ba = ks[i].area();
+          best = i;
+        }
+      if (best < 0) break;
+      const int open = ks[best].link;
+      ks[best] = kid(open, 0);
+      ks[n++] = kid(open, 1);
+    }
+    int m = 0;  // drop empty children (the binary root of a tiny scene)
+    for (int i = 0; i < n; ++i)
+      if (!empty(ks[i])) ks[m++] = ks[i];
+    n = m;
+    const int at = static_cast<int>(out.nodes8.size());
+    out.nodes8.emplace_back();
+    int links[8];
+    for (int i = 0; i < n; ++i) links[i] = ks[i].link >= 0 ? node(ks[i].link, depth + 1) : ks[i].link;
+    BNode8& d = out.nodes8[static_cast<size_t>(at)];
+    std::memset(&d, 0, sizeof d);
+    d.n = n;
+    for (int i = 0; i < 8; ++i) d.c[i] = i < n ? links[i] : 0;
+    for (int a = 0; a < 3; ++a) quantise(ks, n, a, d);
+    return at;
+  }
+};
+
 }  // namespace
 
 void build_fast(const wr::Scene& s, FastHost& out) {
@@ -587,6 +681,10 @@ void build_fast(const wr::Scene& s, FastHost& out) {
   if (out.ok && WR_BVH_WIDE == 4) {
     out.nodes4.reserve(out.nodes.size() / 2 + 4);
     Collapse{out}.node(0, 1);
+  }
+  if (out.ok && WR_BVH_WIDE == 8) {
+    out.nodes8.reserve(out.nodes.size() / 4 + 4);
+    Collapse8{out}.node(0, 1);
   }
 }
 

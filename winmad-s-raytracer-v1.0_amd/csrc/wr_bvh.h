@@ -57,6 +57,28 @@ struct BNode4 {
 };
 static_assert(sizeof(BNode4) == 128, "4-wide BVH node is 128 bytes");
 
+// 128 bytes (one cache line): an 8-wide node of the search, collapsed from the
+// binary BVH (same leaves), with child boxes quantised to bytes on a per-node
+// grid.  Child k's face on axis a is decoded as fmaf(q, scale[a], org[a]) (one
+// correctly rounded operation, the same on the host and the device); the build
+// picks each q so that the decoded box CONTAINS the binary tree's box, bit for
+// bit checked, so the search's boxes only grow and every argument about its
+// margins holds unchanged.  Layout (float4 words):
+//   [0] org.xyz, scale.x   [1] scale.y, scale.z, n (children), 0
+//   [2] c[0..3]            [3] c[4..7]          (links as in BNode; slots >= n unused)
+//   [4] qlo.x[0..7], qlo.y[0..7]   [5] qlo.z[0..7], qhi.x[0..7]
+//   [6] qhi.y[0..7], qhi.z[0..7]   [7] unused
+struct BNode8 {
+  float org[3];
+  float scale[3];
+  int32_t n, pad0;
+  int32_t c[8];
+  uint8_t qlo[3][8];
+  uint8_t qhi[3][8];
+  uint8_t pad1[16];
+};
+static_assert(sizeof(BNode8) == 128, "8-wide BVH node is 128 bytes");
+
 // 48 bytes per triangle, in BVH leaf order, laid out as the KD refs
 // (wr_traverse.h): (p0.xyz, A), (B, C, D, E), (F, prim, lb, ln) with A..F =
 // p0 - p1, p0 - p2 exactly as Triangle::hit forms them and [lb, lb + ln) the
@@ -85,7 +107,7 @@ struct PrimRec {
 static_assert(sizeof(PrimRec) == 128, "primitive membership record is 128 bytes");
 
 #ifndef WR_BVH_WIDE
-#define WR_BVH_WIDE 2  // the search's tree: 2 = BNode (measured faster), 4 = BNode4
+#define WR_BVH_WIDE 2  // the search's tree: 2 = BNode, 4 = BNode4, 8 = BNode8
 #endif
 #ifndef WR_BVH_LEAF
 // 2: the search keeps 2 instead of 4 triangle records in flight per leaf
@@ -120,6 +142,8 @@ struct FastHost {
   std::vector<BNode> nodes;
   std::vector<BNode4> nodes4;  // the search's tree (root 0)
   int depth4 = 0;              // deepest 4-wide node chain
+  std::vector<BNode8> nodes8;  // WR_BVH_WIDE 8: the search's tree (root 0)
+  int depth8 = 0;              // deepest 8-wide node chain
   std::vector<TriRec> tris;
   std::vector<int32_t> prim_leaf_off, prim_leaf, prim_leaf_pos;
   std::vector<int32_t> node_path;  // KD leaf node -> its path record offset (-1: inner node)

@@ -38,6 +38,7 @@ namespace wrd {
 struct FastScene {
   const float4* nodes;  // 4 per wrf::BNode (tie resolution's collection)
   const float4* nodes4;  // 8 per wrf::BNode4 (the search, WR_BVH_WIDE 4)
+  const float4* nodes8;  // 8 per wrf::BNode8 (the search, WR_BVH_WIDE 8)
   const float4* tris;   // 3 per wrf::TriRec
   const int* prim_leaf_off;
   const int* prim_leaf;
@@ -77,7 +78,10 @@ __host__ __device__ constexpr size_t fast_lds_bytes(int depth) { return size_t(d
 // global spill area, so that the 4-wide tree's worst case (3 entries per
 // level) does not set the LDS size and with it the waves per CU.
 #ifndef WR_BVH_LDS_STACK
-#define WR_BVH_LDS_STACK 64  // the binary tree never spills; the 4-wide one ran with 12
+// the binary tree never spills; the 4-wide one ran with 12; the 8-wide one
+// keeps 16 (a ray's stack outgrows 12 entries for 2e-4 of torus rays, 16 for
+// none in 10^5: scripts/bvh_cost.cpp)
+#define WR_BVH_LDS_STACK (WR_BVH_WIDE == 8 ? 16 : 64)
 #endif
 constexpr int kLdsStack = WR_BVH_LDS_STACK;
 __host__ __device__ constexpr size_t search_lds_bytes(int depth) {
@@ -91,7 +95,9 @@ __host__ __device__ constexpr size_t search_spill_entries(int depth) {
 // (kMaxBvhDepth + 1 entries fit), so its push / pop carry no spill branch: a
 // generic pointer select between LDS and the spill area made the compiler emit
 // flat loads (vmcnt + lgkmcnt waits) on every pop.
-constexpr bool kSearchSpills = (WR_BVH_WIDE == 4 ? 3 * wrf::kMaxBvhDepth + 1 : wrf::kMaxBvhDepth + 1) > kLdsStack;
+constexpr bool kSearchSpills =
+    (WR_BVH_WIDE == 8 ? 7 * wrf::kMaxBvhDepth + 1 : WR_BVH_WIDE == 4 ? 3 * wrf::kMaxBvhDepth + 1 : wrf::kMaxBvhDepth + 1) >
+    kLdsStack;
 // Speculative leaves (Aila & Laine 2009): a lane that has found its leaf keeps
 // descending inner nodes while other lanes still look for theirs, and the
 // leaf is tested (postponed) with theirs.  Extra nodes visited under a stale
@@ -1102,6 +1108,65 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           if (nh > 2) push(l2, k2);
           if (nh > 1) push(l1, k1);
           cur = l0;
+        }
+#elif WR_BVH_WIDE == 8
+        // an 8-wide node (wrf::BNode8, one 128-byte line): the eight child
+        // boxes decoded from bytes, fmaf(q, scale, org) -- the build made each
+        // contain the binary tree's box, bit for bit checked -- and tested as
+        // above; the children hit, nearest first: the nearest is visited next,
+        // the others pushed farthest first
+        const float4* np = F.nodes8 + 8 * static_cast<size_t>(cur);
+        const float4 h0 = np[0], h1 = np[1];
+        const int4 la = *reinterpret_cast<const int4*>(np + 2), lb = *reinterpret_cast<const int4*>(np + 3);
+        const uint4 q0 = *reinterpret_cast<const uint4*>(np + 4), q1 = *reinterpret_cast<const uint4*>(np + 5),
+                    q2 = *reinterpret_cast<const uint4*>(np + 6);
+        const int nch = __float_as_int(h1.z);
+        const float inf = __int_as_float(0x7f800000);
+        float tk[8];
+        int lk8[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int sh = 8 * (i & 3);
+          auto dq = [&](uint32_t w, float sc, float org) {
+            return fmaf(static_cast<float>((w >> sh) & 255u), sc, org);
+          };
+          const float lx = dq(i < 4 ? q0.x : q0.y, h0.w, h0.x), ly = dq(i < 4 ? q0.z : q0.w, h1.x, h0.y),
+                      lz = dq(i < 4 ? q1.x : q1.y, h1.y, h0.z);
+          const float hx = dq(i < 4 ? q1.z : q1.w, h0.w, h0.x), hy = dq(i < 4 ? q2.x : q2.y, h1.x, h0.y),
+                      hz = dq(i < 4 ? q2.z : q2.w, h1.y, h0.z);
+          const float x0 = fmaf(lx, binv.x, cl.x), x1 = fmaf(hx, binv.x, ch.x);
+          const float y0 = fmaf(ly, binv.y, cl.y), y1 = fmaf(hy, binv.y, ch.y);
+          const float z0 = fmaf(lz, binv.z, cl.z), z1 = fmaf(hz, binv.z, ch.z);
+          const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), lo_t));
+          const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), hi_t));
+          tk[i] = (tn <= tf && i < nch) ? tn : inf;  // miss: +inf (a hit's tn <= hi_t is finite)
+        }
+        auto cswap = [&](int a, int b) {
+          const bool s = tk[b] < tk[a];
+          const float t = s ? tk[b] : tk[a];
+          tk[b] = s ? tk[a] : tk[b];
+          tk[a] = t;
+          const int l = s ? lk8[b] : lk8[a];
+          lk8[b] = s ? lk8[a] : lk8[b];
+          lk8[a] = l;
+        };
+        // 19-comparator sorting network for 8 keys
+        cswap(0, 2); cswap(1, 3); cswap(4, 6); cswap(5, 7);
+        cswap(0, 4); cswap(1, 5); cswap(2, 6); cswap(3, 7);
+        cswap(0, 1); cswap(2, 3); cswap(4, 5); cswap(6, 7);
+        cswap(2, 4); cswap(3, 5);
+        cswap(1, 4); cswap(3, 6);
+        cswap(1, 2); cswap(3, 4); cswap(5, 6);
+        int nh = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) nh += tk[i] < inf ? 1 : 0;
+        if (nh == 0) {
+          pop();
+        } else {
+#pragma unroll
+          for (int i = 7; i >= 1; --i)
+            if (i < nh) push(lk8[i], tk[i]);
+          cur = lk8[0];
         }
 #else
         const float4* np = F.nodes + 4 * static_cast<size_t>(cur);

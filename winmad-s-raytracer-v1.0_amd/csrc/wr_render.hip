@@ -1698,6 +1698,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
         a.take<wrf::BNode>(fbn); a.take<wrf::TriRec>(ftr); a.take<int>(fpo); a.take<int>(fpl); a.take<int>(fpl);
         a.take<uint2>(fpa); a.take<int>(fnp); a.take<float4>(2 * fnp); a.take<wrf::PrimRec>(fh.prim_rec.size());
         a.take<wrf::BNode4>(fh.nodes4.size());
+        a.take<wrf::BNode8>(fh.nodes8.size());
       });
       if (int rc = c->fast_mem.reserve(fbytes)) {
         wr_destroy(c);
@@ -1714,6 +1715,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       float4* dnc = F.take<float4>(2 * fnp);
       auto* dpr = F.take<wrf::PrimRec>(fh.prim_rec.size());
       auto* dn4 = F.take<wrf::BNode4>(fh.nodes4.size());
+      auto* dn8 = F.take<wrf::BNode8>(fh.nodes8.size());
       hipError_t fe = hipSuccess;
       for (hipError_t x : {hipMemcpy(dno, fh.nodes.data(), fbn * sizeof(wrf::BNode), hipMemcpyHostToDevice),
                            hipMemcpy(dtr, fh.tris.data(), ftr * sizeof(wrf::TriRec), hipMemcpyHostToDevice),
@@ -1727,6 +1729,8 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                            hipMemcpy(dpr, fh.prim_rec.data(), fh.prim_rec.size() * sizeof(wrf::PrimRec),
                                      hipMemcpyHostToDevice),
                            hipMemcpy(dn4, fh.nodes4.data(), fh.nodes4.size() * sizeof(wrf::BNode4),
+                                     hipMemcpyHostToDevice),
+                           hipMemcpy(dn8, fh.nodes8.data(), fh.nodes8.size() * sizeof(wrf::BNode8),
                                      hipMemcpyHostToDevice)})
         if (x != hipSuccess) fe = x;
       if (fe != hipSuccess) {
@@ -1744,6 +1748,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       fs.node_cell = dnc;
       fs.prim_rec = reinterpret_cast<const float4*>(dpr);
       fs.nodes4 = reinterpret_cast<const float4*>(dn4);
+      fs.nodes8 = reinterpret_cast<const float4*>(dn8);
       float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
       for (int k = 0; k < 3; ++k) {
         lo[k] = std::min(fh.nodes[0].b[k], fh.nodes[0].b[6 + k]);
@@ -1753,7 +1758,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       fs.hi = v3(hi[0], hi[1], hi[2]);
       // the search's stack holds BVH entries only; the hard rays' kernel walks
       // both trees
-      fs.sdepth = WR_BVH_WIDE == 4 ? 3 * fh.depth4 + 1 : fh.depth + 1;
+      fs.sdepth = WR_BVH_WIDE == 8 ? 7 * fh.depth8 + 1 : WR_BVH_WIDE == 4 ? 3 * fh.depth4 + 1 : fh.depth + 1;
       fs.depth = std::max(fh.depth + 1, d.max_stack + 1);
       c->fast_ok = true;
       int per_cu = 0;
