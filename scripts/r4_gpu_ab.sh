@@ -24,6 +24,21 @@ done
 for v in ${VARIANTS:-}; do
   WR_LIB=winmad-s-raytracer-v1.0_amd/variants/$v.so run var_${v}_20 150 $B --steps 20
 done
+if [ "${EM:-0}" = 1 ]; then  # INTEGRATION.md 1's main() (example_main) alone at the headline config
+  mkdir -p gpurun_out/em/src
+  python3 -c "import sys; sys.path.insert(0, 'winmad-s-raytracer-v1.0_amd'); from winmad_rt import scenes; scenes.write('gpurun_out/em/torus.scene', scenes.torus_scene(1920, 1080)); open('gpurun_out/em/src/parameters.para', 'w').write('7\n1\n8\n4\n1920\n1080\n5\n400\n')"
+  for it in 256 20 1; do
+    (cd gpurun_out/em && timeout -k 10 120 ../../winmad-s-raytracer-v1.0_amd/example_main torus.scene o.ppm -bpt $it \
+      > ../r4_em_$it.out 2> ../r4_em_$it.err); rc=$?
+    echo "em_$it rc=$rc $(tail -1 gpurun_out/r4_em_$it.out)"; [ $rc -eq 0 ] || exit $rc
+  done
+fi
+if [ "${TL:-0}" = 1 ]; then  # kernel timeline of one overlapped iteration
+  export TMPDIR=/tmp
+  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl1 -o run -- \
+    python3 bench.py --steps 1 --warmup 3 --no-cpu --no-count --no-compare > gpurun_out/r4_tl1.out 2>&1
+  rc=$?; echo "tl1 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
 if [ "${SUITE:-1}" = 1 ]; then
   run suite 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 fi

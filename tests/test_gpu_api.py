@@ -206,7 +206,11 @@ def test_reference_main_with_the_mirror_runs_at_the_bench_rate(tmp_path):
                         "--no-compare"], cwd=root, capture_output=True, text=True, timeout=300, env=env)
     assert b.returncode == 0, b.stderr[-2000:]
     bench_rate = json.loads([ln for ln in b.stdout.splitlines() if ln.startswith("{")][-1])["value"]
-    print(f"example_main {main_rate:.1f} Mrays/s ({pipes} pipelines) vs bench.py {bench_rate:.1f}: "
-          f"{main_rate / bench_rate:.3f}")
-    assert pipes == 16
+    bench_pipes = json.loads([ln for ln in b.stdout.splitlines() if ln.startswith("{")][-1])["config"]["pipelines"]
+    print(f"example_main {main_rate:.1f} Mrays/s ({pipes} pipelines) vs bench.py {bench_rate:.1f} "
+          f"({bench_pipes} pipelines): {main_rate / bench_rate:.3f}")
+    # the library's load-time set-up gave the program bench.py's queues: the same
+    # pipeline count (16 on an idle GPU; fewer when this test process still
+    # holds device memory, as both size their pipelines by the free memory)
+    assert pipes == bench_pipes, (pipes, bench_pipes)
     assert main_rate >= 0.8 * bench_rate, (main_rate, bench_rate)

@@ -120,12 +120,12 @@ struct BdptBuf {
   float *ls, *cs;  // light / camera subpath state, PS_WORDS floats per path
   float* vs;       // stored light vertices, VS_WORDS floats per slot k * P + p (k < kVMax)
   float* cv;       // overlapped schedule: stored camera vertices, CV_WORDS floats per slot j * P + p (j < kCvMax)
-  // extension-ray queues (double buffered).  The overlapped schedule gives the
-  // camera pass its own pair (qc_*); its kernels see them as q_* (camera_view)
+  // extension-ray queues (double buffered, SoA with stride qs).  Overlapped
+  // schedule: qs = 2P, the light pass's rays of a bounce first (count
+  // ext[b]), the camera pass's behind them (count ext[kCamSlot + b])
+  int qs = 0;
   float *q_o[2], *q_d[2], *q_t[2];
   int *q_path[2], *q_prim[2];
-  float *qc_o[2], *qc_d[2], *qc_t[2];
-  int *qc_path[2], *qc_prim[2];
   // shadow + aux closest-hit queue (splat / connection / NEE / DI-BSDF)
   // shadow / aux queue and DI records, two each: the ones of step `slot` are
   // [slot & 1], so a step's resolve and the next step's vertex shading (which
@@ -153,17 +153,11 @@ struct BdptArgs {
   int ctl, maxlen, faithful;
   int overlap = 0;  // 1: the overlapped schedule (light splats into the step's sq, CV store, light-side connections)
 };
-// The camera kernels of the overlapped schedule read and write the camera
-// pass's own extension queues under the q_* names
-__host__ __device__ inline BdptBuf camera_view(BdptBuf B) {
-  for (int q = 0; q < 2; ++q) {
-    B.q_o[q] = B.qc_o[q];
-    B.q_d[q] = B.qc_d[q];
-    B.q_t[q] = B.qc_t[q];
-    B.q_path[q] = B.qc_path[q];
-    B.q_prim[q] = B.qc_prim[q];
-  }
-  return B;
+// First queue index of the camera pass's extension rays of step `slot`
+// (kCamSlot + bounce): overlapped, behind the light pass's rays of the same
+// bounce, whose count is final once the step's light kernel has run
+__device__ __forceinline__ int cam_ext_base(const BdptArgs& A, int slot) {
+  return A.overlap ? A.sc->ext[slot - kCamSlot] : 0;
 }
 struct BdptGroup {
   BdptArgs a[kGroup];
@@ -189,7 +183,7 @@ __device__ __forceinline__ bool len_ok(int ctl, int L) { return ctl <= 0 || L ==
 __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_light_gen(BdptGroup G_) {
   const BdptArgs& A = G_.a[blockIdx.y];
   const BdptBuf& B = A.B;
-  const int P = B.P;  // buffer stride
+  // (queues use the stride B.qs)
   const float lpp = 1.f / static_cast<float>(A.S.nlights);
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < A.n; p += gridDim.x * blockDim.x) {
     // local index p, global light path A.base + p (the RNG key pairs it with
@@ -221,8 +215,8 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_light_gen(BdptGro
     psu(B.ls, p, PS_CTR) = rng.ctr;
     psi(B.ls, p, PS_VCOUNT) = 0;
     // Ray(origin + dir * EPS, dir) (:79-80)
-    st3(B.q_o[0], P, p, pos + dir * WR_EPS);
-    st3(B.q_d[0], P, p, normalize(dir));
+    st3(B.q_o[0], B.qs, p, pos + dir * WR_EPS);
+    st3(B.q_d[0], B.qs, p, normalize(dir));
     B.q_path[0][p] = p;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[0] = A.n;
@@ -442,8 +436,8 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
   }
   const int ei = wave_append(&A.sc->ext[oslot], ext);
   if (ext) {
-    st3(B.q_o[nxt], P, ei, e_o);
-    st3(B.q_d[nxt], P, ei, e_d);
+    st3(B.q_o[nxt], B.qs, ei, e_o);
+    st3(B.q_d[nxt], B.qs, ei, e_d);
     B.q_path[nxt][ei] = p;
   }
   // sequential schedule: traced with the camera primaries; overlapped: with
@@ -505,7 +499,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
     return;
   }
   const BdptBuf& B = A.B;
-  const int P = B.P, cur = slot & 1;
+  const int cur = slot & 1;
   const int n = A.sc->ext[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = nmain * blockDim.x;
@@ -519,15 +513,15 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
       prim = B.q_prim[cur][j];
 #ifdef WR_DEBUG_PATH
       if (A.base + p == WR_DEBUG_PATH && A.iter == WR_DEBUG_ITER) {
-        const V3 o = ld3(B.q_o[cur], P, j), d = ld3(B.q_d[cur], P, j);
+        const V3 o = ld3(B.q_o[cur], B.qs, j), d = ld3(B.q_d[cur], B.qs, j);
         printf("[dbg gpu] light step %d ray o %a %a %a d %a %a %a prim %d t %a\n", slot, o.x, o.y, o.z, d.x, d.y, d.z, prim,
                B.q_t[cur][j]);
       }
 #endif
       if (prim >= 0) {
         t = B.q_t[cur][j];
-        o = ld3(B.q_o[cur], P, j);
-        d = ld3(B.q_d[cur], P, j);
+        o = ld3(B.q_o[cur], B.qs, j);
+        d = ld3(B.q_d[cur], B.qs, j);
       }
     }
     light_vertex(A, p, prim, t, o, d, slot + 1);
@@ -540,7 +534,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
 __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
   const BdptBuf& B = A.B;
   const DCam& cam = A.S.cam;
-  const int P = B.P;  // buffer stride
+  // (queues use the stride B.qs)
   // queue order: 8x8 raster tiles per wave (coherent primary rays); the
   // path <-> pixel mapping stays the reference's (x = p / W, y = p % W, :422-423).
   // A tiled piece is whole 8-row bands (base and n multiples of 8 W), so the
@@ -574,9 +568,10 @@ __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
   psu(B.cs, l, PS_CTR) = rng.ctr;
   psi(B.cs, l, PS_PIX) = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
   psi(B.cs, l, PS_CVCOUNT) = 0;  // (BDPT only: VertexCM's camera gen sets PS_DVM here after this)
-  st3(B.q_o[0], P, s, cam.pos + d * WR_EPS);
-  st3(B.q_d[0], P, s, normalize(d));
-  B.q_path[0][s] = l;
+  const int e = cam_ext_base(A, kCamSlot) + s;  // overlapped: behind the light pass's first rays
+  st3(B.q_o[0], B.qs, e, cam.pos + d * WR_EPS);
+  st3(B.q_d[0], B.qs, e, normalize(d));
+  B.q_path[0][e] = l;
   return l;
 }
 __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGroup G_) {
@@ -794,18 +789,18 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
       psi(B.cs, p, PS_LEN) = len + 1;
     }
   }
-  const int ei = wave_append(&A.sc->ext[oslot], ext);
+  const int ei = wave_append(&A.sc->ext[oslot], ext) + cam_ext_base(A, oslot);
   if (ext) {
-    st3(B.q_o[nxt], P, ei, e_o);
-    st3(B.q_d[nxt], P, ei, e_d);
+    st3(B.q_o[nxt], B.qs, ei, e_o);
+    st3(B.q_d[nxt], B.qs, ei, e_d);
     B.q_path[nxt][ei] = p;
   }
 }
 
 __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, int bid, int nblk) {
   const BdptBuf& B = A.B;
-  const int P = B.P, cur = slot & 1;  // P: buffer stride
-  const int n = A.sc->ext[slot];
+  const int cur = slot & 1;
+  const int n = A.sc->ext[slot], e0 = cam_ext_base(A, slot);
   if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
@@ -814,12 +809,13 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
     float t = 0.f;
     V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 0.f);
     if (j < n) {
-      p = B.q_path[cur][j];
-      prim = B.q_prim[cur][j];
+      const int e = e0 + j;
+      p = B.q_path[cur][e];
+      prim = B.q_prim[cur][e];
       if (prim >= 0) {
-        t = B.q_t[cur][j];
-        o = ld3(B.q_o[cur], P, j);
-        d = ld3(B.q_d[cur], P, j);
+        t = B.q_t[cur][e];
+        o = ld3(B.q_o[cur], B.qs, e);
+        d = ld3(B.q_d[cur], B.qs, e);
       }
     }
     camera_vertex(A, p, prim, t, o, d, slot + 1);

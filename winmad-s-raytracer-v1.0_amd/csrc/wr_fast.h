@@ -875,7 +875,7 @@ struct QueueIndex {
     int acc = 0;
 #pragma unroll
     for (int i = 0; i < kMaxQueues; ++i) {
-      if (i < Q.n && Q.q[i].count) acc += *Q.q[i].count;
+      if (i < Q.n && Q.q[i].count) acc += *Q.q[i].count + (Q.q[i].count2 ? *Q.q[i].count2 : 0);
       qend[i] = acc;
     }
     n = acc;

@@ -642,20 +642,16 @@ void layout_bdpt(Arena& a, BdptBuf& B, int P, bool overlapped) {
   B.cs = a.take<float>(PS_WORDS * sP);
   B.vs = a.take<float>(VS_WORDS * sV);
   B.cv = overlapped ? a.take<float>(CV_WORDS * size_t(kCvMax) * P) : nullptr;
-  for (int q = 0; q < 2; ++q) {
-    B.qc_o[q] = overlapped ? a.take<float>(3 * sP) : nullptr;
-    B.qc_d[q] = overlapped ? a.take<float>(3 * sP) : nullptr;
-    B.qc_t[q] = overlapped ? a.take<float>(sP) : nullptr;
-    B.qc_path[q] = overlapped ? a.take<int>(sP) : nullptr;
-    B.qc_prim[q] = overlapped ? a.take<int>(sP) : nullptr;
-  }
+  // overlapped: an extension queue holds both passes' rays (light, then camera)
+  B.qs = overlapped ? 2 * P : P;
+  const size_t sE = B.qs;
 
   for (int q = 0; q < 2; ++q) {
-    B.q_o[q] = a.take<float>(3 * sP);
-    B.q_d[q] = a.take<float>(3 * sP);
-    B.q_t[q] = a.take<float>(sP);
-    B.q_path[q] = a.take<int>(sP);
-    B.q_prim[q] = a.take<int>(sP);
+    B.q_o[q] = a.take<float>(3 * sE);
+    B.q_d[q] = a.take<float>(3 * sE);
+    B.q_t[q] = a.take<float>(sE);
+    B.q_path[q] = a.take<int>(sE);
+    B.q_prim[q] = a.take<int>(sE);
   }
   for (int k = 0; k < 2; ++k) {
     BdptBuf::Sq& q = B.sq[k];
@@ -825,14 +821,25 @@ struct Timer {
 
 RayQueue rq(const float* o3, const float* d3, int cap, const int* cnt, float* t, int* prim,
             const float* tmin = nullptr, const float* tmax = nullptr, const float* cut = nullptr,
-            const LateList* late = nullptr, int* late_n = nullptr, int late_bit = 0) {
-  return RayQueue{o3, d3, cap, cnt, tmin, tmax, t, prim, cut, late, late_n, late_bit};
+            const LateList* late = nullptr, int* late_n = nullptr, int late_bit = 0, const int* cnt2 = nullptr) {
+  return RayQueue{o3, d3, cap, cnt, tmin, tmax, t, prim, cut, late, late_n, late_bit, cnt2};
+}
+// a queue's ray count read back to the host (diagnostics only: synchronous)
+int host_count(const RayQueue& q) {
+  int k = 0, k2 = 0;
+  if (q.count) (void)hipMemcpy(&k, q.count, sizeof(int), hipMemcpyDeviceToHost);
+  if (q.count2) (void)hipMemcpy(&k2, q.count2, sizeof(int), hipMemcpyDeviceToHost);
+  return k + k2;
 }
 // queues of one launch (empty `count` pointers are skipped)
 struct QueueList {
   TraceQueues Q{};
   int max_rays = 0;
   void add(const RayQueue& q, int cap) {
+    if (Q.n >= kMaxQueues) {  // a schedule asking for more queues than a launch takes: a build error
+      std::fprintf(stderr, "winmad_rt: more than %d queues in one traversal launch\n", kMaxQueues);
+      std::abort();
+    }
     Q.q[Q.n++] = q;
     max_rays += cap;
   }
@@ -1023,11 +1030,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
       (void)hipEventRecord(f1, stream);
       (void)hipEventSynchronize(f1);
       int tot = 0;
-      for (int i = 0; i < Q.n; ++i) {
-        int k = 0;
-        if (Q.q[i].count) (void)hipMemcpy(&k, Q.q[i].count, sizeof(int), hipMemcpyDeviceToHost);
-        tot += k;
-      }
+      for (int i = 0; i < Q.n; ++i) tot += host_count(Q.q[i]);
       float ms = 0.f, ma = 0.f, mb = 0.f;
       int nhs[2] = {0, 0};
       (void)hipMemcpy(nhs, ts.hard_n, 2 * sizeof(int), hipMemcpyDeviceToHost);
@@ -1061,11 +1064,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     (void)hipEventRecord(e1, stream);
     (void)hipEventSynchronize(e1);
     int tot = 0;
-    for (int i = 0; i < Q.n; ++i) {
-      int k = 0;
-      if (Q.q[i].count) (void)hipMemcpy(&k, Q.q[i].count, sizeof(int), hipMemcpyDeviceToHost);
-      tot += k;
-    }
+    for (int i = 0; i < Q.n; ++i) tot += host_count(Q.q[i]);
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, e0, e1);
     std::fprintf(stderr, "[wr trace] %d queues, %d rays  %.1f us  grid %d\n", Q.n, tot, ms * 1e3f, grid);
@@ -2089,7 +2088,7 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   // bounce step, the camera pass extension rays at its last step).
   // The overlapped schedule (wr_bdpt.h; WR_BDPT_OVERLAP=0: the sequential one,
   // which the deferred hard rays need)
-  const bool overlap = c->bdpt_overlap && !(c->fast_on && !c->stamps && defer_enabled(c, np));
+  const bool overlap = c->bdpt_overlap && kMaxQueues >= 2 * kGroup && !(c->fast_on && !c->stamps && defer_enabled(c, np));
   const bool defer = !overlap && c->fast_on && !c->stamps && defer_enabled(c, np);
   if (defer)
     for (int i = 0; i < fit; ++i)
@@ -2118,7 +2117,6 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   struct GroupIssue {
     Pipe* pp = nullptr;
     BdptGroup GA;
-    BdptGroup GC;  // overlapped: the camera kernels' view (camera_view: their own extension queues)
     int gn = 0, nmax = 0;
     bool late[kSlots] = {};  // late work issued at step slot
   };
@@ -2129,10 +2127,15 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   // The overlapped schedule: step 0 starts both subpaths of every path; step
   // b + 1 traces, per group member, the shadow / aux rays queued by the
   // vertices of bounce b - 1 (sq slot kCamSlot + b: light splats and
-  // connections, camera DI rays and connections), the light pass's extension
-  // rays of bounce b (b <= maxlen - 2) and the camera pass's (b < maxlen),
-  // then shades the light vertices of bounce b and after them (same stream)
-  // resolves the step's shadow / aux rays and shades its camera vertices.
+  // connections, camera DI rays and connections) and the extension queue of
+  // bounce b: the light pass's rays (count ext[b]; b <= maxlen - 2) followed
+  // by the camera pass's (count ext[kCamSlot + b]; b < maxlen) -- one queue,
+  // so that a launch takes at most 2 x kGroup queues (more queues cost the
+  // traversal kernels registers: WR_MAX_QUEUES 6 took k_trace_fast from 79 to
+  // 95 VGPRs, 6 to 5 waves per SIMD).  Then it shades the light vertices of
+  // bounce b and after them (same stream) resolves the step's shadow / aux
+  // rays and shades its camera vertices, which append their extension rays
+  // behind the light pass's final count.
   auto issue_overlap = [&](GroupIssue& G, int step) -> int {
     Pipe& pp = *G.pp;
     const hipStream_t sm = pp.stream;
@@ -2143,7 +2146,7 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
     if (step == 0) {
       HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
       hipLaunchKernelGGL(k_light_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA);
-      hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GC);
+      hipLaunchKernelGGL(k_camera_gen, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA);
       tm.mark(WR_K_GEN);
       return WR_OK;
     }
@@ -2154,18 +2157,17 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
       const BdptBuf& B = pp.bb[m];
       const BdptBuf::Sq& Q = B.sq[slot & 1];
       ql.add(rq(Q.o, Q.d, B.cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut), A[m].n * (kVMax + 2));
-      if (light)
-        ql.add(rq(B.q_o[b & 1], B.q_d[b & 1], B.P, &pp.sc[m].ext[b], B.q_t[b & 1], B.q_prim[b & 1]), A[m].n);
-      if (more)
-        ql.add(rq(B.qc_o[slot & 1], B.qc_d[slot & 1], B.P, &pp.sc[m].ext[slot], B.qc_t[slot & 1], B.qc_prim[slot & 1]),
-               A[m].n);
+      if (light || more)
+        ql.add(rq(B.q_o[b & 1], B.q_d[b & 1], B.qs, &pp.sc[m].ext[b], B.q_t[b & 1], B.q_prim[b & 1], nullptr, nullptr,
+                  nullptr, nullptr, nullptr, 0, &pp.sc[m].ext[slot]),
+               2 * A[m].n);
     }
     trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE, false, nullptr,
                  gn);
     LateArgs L{};
     if (light) hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA, b, L, 0);
     const int nres = shade_grid(c, G.nmax * (kVMax + 2));
-    hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, G.GC, slot, nres,
+    hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, G.GA, slot, nres,
                        more ? 1 : 0, L, 0);
     tm.mark(WR_K_SHADE);
     return WR_OK;
@@ -2185,8 +2187,8 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
     auto ext = [&](int m, int slot, int bit) {
       const BdptBuf& B = pp.bb[m];
       const int q = slot & 1;
-      if (!bit) return rq(B.q_o[q], B.q_d[q], B.P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
-      return rq(B.q_o[q], B.q_d[q], B.P, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q], nullptr, nullptr, nullptr,
+      if (!bit) return rq(B.q_o[q], B.q_d[q], B.qs, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q]);
+      return rq(B.q_o[q], B.q_d[q], B.qs, &pp.sc[m].ext[slot], B.q_t[q], B.q_prim[q], nullptr, nullptr, nullptr,
                 pp.late_d + 2 * m + q, pp.sc[m].late[slot], bit);
     };
     // the late lists of step slot - 1 (when it deferred): settled by extra
@@ -2280,8 +2282,6 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
         a.iter = static_cast<uint32_t>(prm->iter_begin + pc.iter);
         a.base = pc.base;
         a.n = pc.n;
-        G.GC.a[m] = a;
-        G.GC.a[m].B = camera_view(a.B);
         G.nmax = std::max(G.nmax, pc.n);
       }
       live += G.gn > 0;

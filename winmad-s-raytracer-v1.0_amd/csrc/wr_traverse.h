@@ -205,6 +205,9 @@ struct RayQueue {
   const LateList* late;
   int* late_n;   // [2] this step's late-list counts
   int late_bit;  // the pass's bit of LateList::delayed
+  // a second count (nullptr: none): the queue holds *count + *count2 rays (the
+  // overlapped BDPT schedule: the light pass's rays, then the camera pass's)
+  const int* count2;
 };
 
 // Scene::occluded(p1, dir, p2) answers "unoccluded" iff the closest hit is
@@ -225,10 +228,8 @@ __device__ __forceinline__ float occl_cut(V3 o, V3 tgt, float dist) {
 // The queues of one traversal launch, fetched in order (the shadow / aux queue
 // of an iteration first: its long rays start early and overlap the extension
 // rays instead of forming a tail of their own).
-// (6: the overlapped BDPT schedule traces, per group member, the shadow / aux
-// queue and both passes' extension queues in one launch)
 #ifndef WR_MAX_QUEUES
-#define WR_MAX_QUEUES 6
+#define WR_MAX_QUEUES 4
 #endif
 constexpr int kMaxQueues = WR_MAX_QUEUES;
 struct TraceQueues {
@@ -429,7 +430,7 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
     int acc = 0;
 #pragma unroll
     for (int i = 0; i < kMaxQueues; ++i) {
-      if (i < Q.n && Q.q[i].count) acc += *Q.q[i].count;
+      if (i < Q.n && Q.q[i].count) acc += *Q.q[i].count + (Q.q[i].count2 ? *Q.q[i].count2 : 0);
       qend[i] = acc;
     }
   }
