@@ -531,7 +531,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
 // generateCameraSample (:418-452) + first extension ray, for queue entry s of
 // the piece; returns the path's local index.  (VertexCM::generateCameraSample,
 // vertexcm.cpp:446-479, is the same plus dVM = 0.)
-__device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
+__device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s, int ebase = 0) {
   const BdptBuf& B = A.B;
   const DCam& cam = A.S.cam;
   // (queues use the stride B.qs)
@@ -568,7 +568,7 @@ __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
   psu(B.cs, l, PS_CTR) = rng.ctr;
   psi(B.cs, l, PS_PIX) = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
   psi(B.cs, l, PS_CVCOUNT) = 0;  // (BDPT only: VertexCM's camera gen sets PS_DVM here after this)
-  const int e = cam_ext_base(A, kCamSlot) + s;  // overlapped: behind the light pass's first rays
+  const int e = ebase + s;  // overlapped: behind the light pass's first rays (cam_ext_base)
   st3(B.q_o[0], B.qs, e, cam.pos + d * WR_EPS);
   st3(B.q_d[0], B.qs, e, normalize(d));
   B.q_path[0][e] = l;
@@ -576,7 +576,8 @@ __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s) {
 }
 __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGroup G_) {
   const BdptArgs& A = G_.a[blockIdx.y];
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < A.n; s += gridDim.x * blockDim.x) camera_gen_one(A, s);
+  const int eb = cam_ext_base(A, kCamSlot);
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < A.n; s += gridDim.x * blockDim.x) camera_gen_one(A, s, eb);
   if (blockIdx.x == 0 && threadIdx.x == 0) A.sc->ext[kCamSlot] = A.n;
 }
 
@@ -586,7 +587,10 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_camera_gen(BdptGr
 // wave calls it.  oslot: the step whose queues (shadow / aux, DI records,
 // extension) get this vertex's rays -- slot + 1, or slot + 2 for a deferred
 // vertex (k_late_camera).
-__device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim, float t, V3 o, V3 d, int oslot) {
+// ebase: the queue index of the camera pass's first extension ray of step
+// oslot (cam_ext_base, read once by the caller)
+__device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim, float t, V3 o, V3 d, int oslot,
+                                              int ebase = 0) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   const int P = B.P, nxt = oslot & 1, cap = B.cap_sq;  // P: buffer stride
@@ -789,7 +793,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
       psi(B.cs, p, PS_LEN) = len + 1;
     }
   }
-  const int ei = wave_append(&A.sc->ext[oslot], ext) + cam_ext_base(A, oslot);
+  const int ei = wave_append(&A.sc->ext[oslot], ext) + ebase;
   if (ext) {
     st3(B.q_o[nxt], B.qs, ei, e_o);
     st3(B.q_d[nxt], B.qs, ei, e_d);
@@ -800,7 +804,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
 __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, int bid, int nblk) {
   const BdptBuf& B = A.B;
   const int cur = slot & 1;
-  const int n = A.sc->ext[slot], e0 = cam_ext_base(A, slot);
+  const int n = A.sc->ext[slot], e0 = cam_ext_base(A, slot), eb = cam_ext_base(A, slot + 1);
   if (bid == 0 && threadIdx.x == 0) atomicAdd(&A.ctr->closest, (unsigned long long)n);
   const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
@@ -818,7 +822,7 @@ __device__ __forceinline__ void camera_shade_body(const BdptArgs& A, int slot, i
         d = ld3(B.q_d[cur], B.qs, e);
       }
     }
-    camera_vertex(A, p, prim, t, o, d, slot + 1);
+    camera_vertex(A, p, prim, t, o, d, slot + 1, eb);
   }
 }
 

@@ -609,8 +609,8 @@ void build_fast(const wr::Scene& s, FastHost& out) {
     return;
   }
   const size_t n = s.prims.size();
-  if (n >= (size_t(1) << 30)) {  // the search marks near-ties in bit 30 of a primitive index (wr_fast.h)
-    out.why = "2^30 primitives or more";
+  if (n >= (size_t(1) << 29)) {  // the search marks near-ties and grazing rays in bits 30, 29 of a primitive (wr_fast.h)
+    out.why = "2^29 primitives or more";
     return;
   }
   std::vector<Box> box(n);

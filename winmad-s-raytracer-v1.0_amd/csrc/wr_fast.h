@@ -904,7 +904,34 @@ __device__ __forceinline__ auto qfield(const TraceQueues& Q, int q, Fn field) {
 // the search's near-tie mark on a hit primitive (queue out_prim, between the
 // search and k_fast_resolve, which clears it; scenes have < 2^30 primitives)
 constexpr int kTieMark = 1 << 30;
-__device__ __forceinline__ int unmark(int p) { return p >= 0 ? (p & ~kTieMark) : p; }
+// ... and its grazing mark: the ray runs nearly in the plane of a triangle the
+// search tested (tri_grazes), on a hit primitive, or kGrazeMiss for a ray
+// without a hit (scenes have < 2^29 primitives)
+constexpr int kGrazeMark = 1 << 29;
+constexpr int kGrazeMiss = -3;
+__device__ __forceinline__ int unmark(int p) {
+  return p >= 0 ? (p & ~(kTieMark | kGrazeMark)) : (p == kGrazeMiss ? -1 : p);
+}
+__device__ __forceinline__ bool graze_marked(int p) { return p >= 0 ? (p & kGrazeMark) != 0 : p == kGrazeMiss; }
+// Is Triangle::hit's denominator (triangle.cpp:43-44) for direction d within
+// kGrazeRel of the magnitude of its products: does the ray run nearly in the
+// triangle's plane?  There Cramer's rule works in its rounding noise: the
+// reference can accept such a triangle at a noise t although the ray passes
+// outside its grown box -- one the search never visits (the
+// near-grazing case).  A ray that grazes ANY triangle the search tests lies
+// in that plane near its origin or its path, so a coplanar neighbour in a KD
+// leaf the reference crosses is grazed as well: such rays take the KD walk.
+// (A, B, C, D, E, F) = a.w, b.xyzw, f as in tri_test.
+constexpr float kGrazeRel = 1e-5f;
+__device__ __forceinline__ bool tri_grazes(float4 a, float4 b, float f, V3 dir) {
+  const float A = a.w, B = b.x, C = b.y, D = b.z, E = b.w, F = f;
+  const float G = dir.x, H = dir.y, I = dir.z;
+  const float EIHF = E * I - H * F, GFDI = G * F - D * I, DHEG = D * H - E * G;
+  const float den = A * EIHF + B * GFDI + C * DHEG;
+  const float mag = fabsf(A) * (fabsf(E * I) + fabsf(H * F)) + fabsf(B) * (fabsf(G * F) + fabsf(D * I)) +
+                    fabsf(C) * (fabsf(D * H) + fabsf(E * G));
+  return fabsf(den) <= kGrazeRel * mag;
+}
 
 template <bool COUNT>
 __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, int* fetch,
@@ -935,6 +962,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   float rtmin = 0.f, rtmax = WR_INF, t1 = WR_INF, t2 = WR_INF, tcap = 0.f, dlen = 1.f, olen = 0.f;
   float lo_t = 0.f, hi_t = 0.f;
   int p1 = -1, sp = 0;
+  bool gz = false;          // the ray grazes a tested triangle's plane (tri_grazes)
   uint32_t rn = 0, rt = 0;  // COUNT: this ray's node visits / tests
   int cur = 0;  // >= 0 inner node to visit; < 0 leaf link to test; kDone when finished
   int pl = 0;   // WR_BVH_SPEC: parked leaf link (< 0), or 0
@@ -1027,6 +1055,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           t1 = WR_INF;
           t2 = WR_INF;
           p1 = -1;
+          gz = false;
           sp = 0;
           cur = 0;
           rn = rt = 0;
@@ -1224,6 +1253,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           ++rt;
         }
         float t;
+        gz |= tri_grazes(ta[j], tb[j], tc[j].x, d);
         // screen against t1 + 3 EPS: every hit with t <= t1 + 2 EPS survives
         if (tri_test(ta[j], tb[j], tc[j].x, o, d, rtmin, rtmax, t1 + 3.f * WR_EPS, t)) {
           if (t < t1) {
@@ -1255,6 +1285,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
       int po = p1;
       if (F.diag) t2buf[lidx] = t2;
       else if (p1 >= 0 && !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0)) po = p1 | kTieMark;
+      if (gz) po = po >= 0 ? (po | kGrazeMark) : kGrazeMiss;
       qfield(Q, qi, [](const RayQueue& x) { return x.out_t; })[r] = p1 >= 0 ? t1 : WR_INF;
       qfield(Q, qi, [](const RayQueue& x) { return x.out_prim; })[r] = po;
       r = -1;
@@ -1262,27 +1293,8 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   }
 }
 
-// Is Triangle::hit's denominator (triangle.cpp:43-44) for this direction
-// within 1e-5 of the magnitude of its products, i.e. does the ray run nearly in
-// the triangle's plane?  There the computed (beta, gamma, t) approach their
-// rounding noise, and a coplanar neighbour outside the search window could be
-// accepted by the reference at a noise t; such rays take the KD walk.  The
-// noise level is ~4 ulp (2.4e-7), so 1e-5 leaves a factor 40.
-constexpr float kGrazeRel = 1e-5f;
 // tie-list entries: launch index, | kWalkEntry for a ray the KD walk settles
 constexpr int kWalkEntry = 1 << 30;
-__device__ __forceinline__ bool grazing_test(const DevScene& S, int prim, V3 dir) {
-  const float4 g = S.prim_rec[2 * static_cast<size_t>(prim)], g2 = S.prim_rec[2 * static_cast<size_t>(prim) + 1];
-  if (__float_as_int(g2.w) != 0) return false;  // a sphere
-  const float A = g.x, B = g.y, C = g.z, D = g.w, E = g2.x, F = g2.y;
-  const float G = dir.x, H = dir.y, I = dir.z;
-  const float EIHF = E * I - H * F, GFDI = G * F - D * I, DHEG = D * H - E * G;
-  const float den = A * EIHF + B * GFDI + C * DHEG;
-  const float mag = fabsf(A) * (fabsf(E * I) + fabsf(H * F)) + fabsf(B) * (fabsf(G * F) + fabsf(D * I)) +
-                    fabsf(C) * (fabsf(D * H) + fabsf(E * G));
-  return fabsf(den) <= kGrazeRel * mag;
-}
-
 // one atomic per wave: this lane's slot in a list (or -1 if !want)
 __device__ __forceinline__ int fast_append(int* counter, bool want) {
   const unsigned long long m = __ballot(want);
@@ -1330,10 +1342,11 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
       // p1's membership record: one line with its first four leaves' cells
       const float4* pr = F.prim_rec + 8 * static_cast<size_t>(max(p1, 0));
       const float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3], c4 = pr[4], c5 = pr[5];
-      if (p1 >= 0 && grazing_test(S, p1, d)) {
-        // the ray runs within ~1e-5 (relative) of the winner's plane: Cramer's
-        // rule is near its rounding noise there, beyond the search margins'
-        // reach (margins) -- the KD walk settles it
+      if (graze_marked(pm)) {
+        // the ray runs within ~1e-5 (relative) of the plane of a triangle the
+        // search tested (the winner among them): Cramer's rule is near its
+        // rounding noise there, beyond the search margins' reach (DESIGN.md
+        // 4b, margins) -- the KD walk settles it
         need = true;
         walk = true;
       } else if (p1 >= 0) {  // (no hit anywhere: a miss for the reference too)
