@@ -913,24 +913,39 @@ __device__ __forceinline__ int unmark(int p) {
   return p >= 0 ? (p & ~(kTieMark | kGrazeMark)) : (p == kGrazeMiss ? -1 : p);
 }
 __device__ __forceinline__ bool graze_marked(int p) { return p >= 0 ? (p & kGrazeMark) != 0 : p == kGrazeMiss; }
-// Is Triangle::hit's denominator (triangle.cpp:43-44) for direction d within
-// kGrazeRel of the magnitude of its products: does the ray run nearly in the
-// triangle's plane?  There Cramer's rule works in its rounding noise: the
-// reference can accept such a triangle at a noise t although the ray passes
+// Does the ray run inside the triangle's plane?  Triangle::hit's denominator
+// (triangle.cpp:43-44) within kGrazeRel of the magnitude of its products (the
+// direction nearly parallel to the plane) AND its t numerator within
+// kGrazePlaneRel of its products' (the origin nearly on the plane).  There
+// Cramer's rule divides rounding noise by rounding noise: the reference can
+// accept a triangle of that plane at a noise t although the ray passes
 // outside its grown box -- one the search never visits (the
-// near-grazing case).  A ray that grazes ANY triangle the search tests lies
-// in that plane near its origin or its path, so a coplanar neighbour in a KD
-// leaf the reference crosses is grazed as well: such rays take the KD walk.
-// (A, B, C, D, E, F) = a.w, b.xyzw, f as in tri_test.
-constexpr float kGrazeRel = 1e-5f;
-__device__ __forceinline__ bool tri_grazes(float4 a, float4 b, float f, V3 dir) {
+// near-grazing case; the probe in tests/test_gpu_bvh.py found such rays only
+// with the origin on the plane: a ray parallel to a plane but off it gets a
+// t far beyond any other hit).  A ray inside a plane runs through the
+// triangles of that plane near its origin, so the search tests one of them
+// (the one the origin lies on) and the ray takes the KD walk.  A..F as in
+// tri_test, p0 = a.xyz.
+#ifndef WR_GRAZE_REL
+#define WR_GRAZE_REL 1e-5f
+#endif
+#ifndef WR_GRAZE_PLANE_REL
+#define WR_GRAZE_PLANE_REL 1e-4f
+#endif
+constexpr float kGrazeRel = WR_GRAZE_REL, kGrazePlaneRel = WR_GRAZE_PLANE_REL;
+__device__ __forceinline__ bool tri_grazes(float4 a, float4 b, float f, V3 o, V3 dir) {
   const float A = a.w, B = b.x, C = b.y, D = b.z, E = b.w, F = f;
   const float G = dir.x, H = dir.y, I = dir.z;
+  const float J = a.x - o.x, K = a.y - o.y, L = a.z - o.z;
   const float EIHF = E * I - H * F, GFDI = G * F - D * I, DHEG = D * H - E * G;
   const float den = A * EIHF + B * GFDI + C * DHEG;
   const float mag = fabsf(A) * (fabsf(E * I) + fabsf(H * F)) + fabsf(B) * (fabsf(G * F) + fabsf(D * I)) +
                     fabsf(C) * (fabsf(D * H) + fabsf(E * G));
-  return fabsf(den) <= kGrazeRel * mag;
+  const float AKJB = A * K - J * B, JCAL = J * C - A * L, BLKC = B * L - K * C;
+  const float tnum = F * AKJB + E * JCAL + D * BLKC;
+  const float tmag = fabsf(F) * (fabsf(A * K) + fabsf(J * B)) + fabsf(E) * (fabsf(J * C) + fabsf(A * L)) +
+                     fabsf(D) * (fabsf(B * L) + fabsf(K * C));
+  return fabsf(den) <= kGrazeRel * mag && fabsf(tnum) <= kGrazePlaneRel * tmag;
 }
 
 template <bool COUNT>
@@ -1253,7 +1268,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           ++rt;
         }
         float t;
-        gz |= tri_grazes(ta[j], tb[j], tc[j].x, d);
+        gz |= tri_grazes(ta[j], tb[j], tc[j].x, o, d);
         // screen against t1 + 3 EPS: every hit with t <= t1 + 2 EPS survives
         if (tri_test(ta[j], tb[j], tc[j].x, o, d, rtmin, rtmax, t1 + 3.f * WR_EPS, t)) {
           if (t < t1) {
