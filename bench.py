@@ -423,9 +423,10 @@ def main():
         }
         if trace == "bvh":
             out["trace_note"] = ("verified BVH traversal: every ray gets the reference KD walk's (t, primitive) "
-                                 "answer, bit for bit (argument in DESIGN.md 4b, one near-grazing case open; 0 mismatches over "
-                                 "2.2e10 rays of the bench workloads, profiles/r3/bvh_verify*.json); the same rays are "
-                                 "traced and counted")
+                                 "answer, bit for bit (argument in DESIGN.md 4b; rays running inside the plane of a "
+                                 "triangle the search tests take the KD walk; 0 mismatches on the plane-grazing probe, "
+                                 "tests/test_gpu_bvh.py, and on the bench workloads, profiles/r4/bvh_verify*.json); the "
+                                 "same rays are traced and counted")
         if other:
             out["other_trace"] = other
         if cfg["integrator"] in ("pt", "vcm"):

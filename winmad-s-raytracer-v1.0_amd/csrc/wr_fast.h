@@ -930,7 +930,7 @@ __device__ __forceinline__ bool graze_marked(int p) { return p >= 0 ? (p & kGraz
 #define WR_GRAZE_REL 1e-5f
 #endif
 #ifndef WR_GRAZE_PLANE_REL
-#define WR_GRAZE_PLANE_REL 1e-4f
+#define WR_GRAZE_PLANE_REL 1e-3f
 #endif
 constexpr float kGrazeRel = WR_GRAZE_REL, kGrazePlaneRel = WR_GRAZE_PLANE_REL;
 __device__ __forceinline__ bool tri_grazes(float4 a, float4 b, float f, V3 o, V3 dir) {
