@@ -535,22 +535,38 @@ __device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3
 // The first leaf of primitive p that the reference's traversal visits, as its
 // visit key (kd_reaches) and p's position in that leaf's list; key = ~0: p is
 // not visited.  (pos < 256, so (key, pos) orders the visits of one ray.)
+// The leaves are taken four at a time: their path offsets, then their headers
+// (cells) in flight together -- a candidate's leaves mostly fail the cell
+// test, and one at a time each cost two dependent round trips.
 __device__ WR_HARD_CALL void first_leaf(const FastScene& F, int p, V3 o, V3 d, V3 inv, float tmin0, float tmax0,
                                         float rtmax, unsigned long long& key, int& pos, uint32_t& steps) {
+  constexpr int U = 4;
   key = ~0ull;
   pos = 0;
   const int lb = F.prim_leaf_off[p], le = F.prim_leaf_off[p + 1];
-  for (int k = lb; k < le; ++k) {
-    unsigned long long kk;
-    const uint2* rec = F.path + F.prim_leaf[k];
-    // a leaf whose cell the ray's line misses is never reached: no replay
-    if (!cell_may_be_reached(*reinterpret_cast<const uint4*>(rec), *reinterpret_cast<const uint4*>(rec + 2), o, d))
-      continue;
-    if (!kd_reaches(rec, o, d, inv, tmin0, tmax0, rtmax, steps, kk)) continue;
-    const int pk = F.prim_leaf_pos[k];
-    if (kk < key || (kk == key && pk < pos)) {
-      key = kk;
-      pos = pk;
+  for (int k0 = lb; k0 < le; k0 += U) {
+    int off[U];
+    uint4 h0[U], h1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) off[u] = k0 + u < le ? F.prim_leaf[k0 + u] : F.prim_leaf[k0];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint2* rec = F.path + off[u];
+      h0[u] = *reinterpret_cast<const uint4*>(rec);
+      h1[u] = *reinterpret_cast<const uint4*>(rec + 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (k0 + u >= le) break;
+      // a leaf whose cell the ray's line misses is never reached: no replay
+      if (!cell_may_be_reached(h0[u], h1[u], o, d)) continue;
+      unsigned long long kk;
+      if (!kd_reaches(F.path + off[u], o, d, inv, tmin0, tmax0, rtmax, steps, kk)) continue;
+      const int pk = F.prim_leaf_pos[k0 + u];
+      if (kk < key || (kk == key && pk < pos)) {
+        key = kk;
+        pos = pk;
+      }
     }
   }
 }
