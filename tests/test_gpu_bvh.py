@@ -195,6 +195,44 @@ def test_bvh_verify_every_ray_against_the_kd_walk(name, maker, kind, monkeypatch
     assert st.verify_mismatches == 0, (st.verify_mismatches, st.verify_rays)
 
 
+@pytest.mark.parametrize("name,maker,n", [("torus", lambda: _scenes.torus(256, 256), 200_000),
+                                          ("cbox", lambda: _scenes.cbox(256, 192), 200_000),
+                                          ("torus1m", lambda: big_torus(64, 64), 60_000)])
+def test_wave_kd_walk_matches_reference_mode(name, maker, n, monkeypatch):
+    """WR_BVH_DIAG=256 sends every ray to k_fast_hard's KD walk: the API calls
+    walk them one ray per wave (kd_walk_wave: the wave expands the crossed
+    nodes together and replays the reference's first-found rule over the hits
+    in walk order).  Same (t, primitive) as the reference mode, bit for bit."""
+    ref, _ = pair(maker())
+    monkeypatch.setenv("WR_BVH_DIAG", "256")
+    s = native.Scene(maker())
+    walk = native.Context(s, 0, trace=native.TRACE_BVH)
+    rays, (p, sd, q) = _corpus(ref, n, 77)
+    a = ref.trace_closest(rays)
+    b = walk.trace_closest(rays)
+    ok = _same_hits(a, b)
+    assert ok.all(), (name, int((~ok).sum()), rays.shape[0], np.nonzero(~ok)[0][:8])
+    r8 = native.rays_from_arrays(p, sd)
+    assert np.array_equal(ref.occluded(r8, q), walk.occluded(r8, q))
+
+
+@pytest.mark.parametrize("name,maker", [("torus", lambda: _scenes.torus(128, 128)),
+                                        ("torus1m", lambda: big_torus(96, 54))])
+def test_wave_kd_walk_in_pipelines_verified(name, maker, monkeypatch):
+    """Every ray of a BDPT render to the KD walk (WR_BVH_DIAG=256): the
+    pipelines' k_fast_hard takes them one per lane and each lane hands its walk
+    to its wave; WR_BVH_VERIFY checks every answer against the serial walk."""
+    monkeypatch.setenv("WR_BVH_DIAG", "256")
+    monkeypatch.setenv("WR_BVH_VERIFY", "1")
+    s = native.Scene(maker())
+    c = native.Context(s, 0, trace=native.TRACE_BVH)
+    W, H = (128, 128) if name == "torus" else (96, 54)
+    _, st = c.render_bdpt(W, H, iterations=1, seed=9, count_work=True)
+    assert st.verify_rays == st.closest_rays + st.shadow_rays > 0
+    assert st.verify_mismatches == 0, (st.verify_mismatches, st.verify_rays)
+    assert st.fallback_rays >= 0.5 * st.closest_rays, (st.fallback_rays, st.closest_rays)  # walked
+
+
 @pytest.mark.parametrize("name,maker,W,H,its", [("torus", lambda: _scenes.torus(256, 256), 256, 256, 3),
                                                 ("cbox", lambda: _scenes.cbox(96, 72, "bdpt"), 96, 72, 3),
                                                 ("torus1m", lambda: big_torus(192, 108), 192, 108, 1)])

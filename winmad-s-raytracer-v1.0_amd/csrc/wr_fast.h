@@ -50,9 +50,10 @@ struct FastScene {
   V3 lo, hi;  // union of the (grown) triangle boxes
   int depth;   // stack entries of the KD walks and tie resolution (k_fast_hard, k_fast_verify)
   int sdepth;  // stack entries of the BVH search (k_trace_fast): the BVH's depth + 1
+  int walk_wave;  // 1: the one-ray-per-wave resolutions walk the KD tree with the whole wave (kd_walk_wave)
   int diag;   // WR_BVH_DIAG (measurement only): 1 = skip the KD walks, 8 = skip the replays, 16 = skip k_fast_resolve,
               // 32 = skip k_fast_hard, 64 its scan list, 128 its tie list (all wrong answers);
-              // 2 = KD walk for every tie
+              // 2 = KD walk for every tie, 256 = every ray to k_fast_hard's KD walk (exact: a test of the walks)
 };
 
 struct FastCounters {  // algorithmic work (count_work)
@@ -390,6 +391,227 @@ __device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtm
     tmax = sp > 0 ? stk_tmin[(sp - 1) * 64] : root_tmax;
     if (rtmax < tmin) return;  // :323
   }
+}
+
+// kd_walk for one ray by a whole wave (every lane holds the ray; all lanes
+// return the same answer).  The reference's walk has no early exit, so the
+// leaves it reaches are fixed by the root clip, the near / far rule and the
+// :323 stop, never by its hits; a node's (tmin, tmax) is a function of its
+// root path (near child (tmin, t) or (tmin, tmax), far child (t, tmax): the
+// popped todo entry's tmax is the entry below it, which is the parent's tmax);
+// and the :323 stop at a popped far child ends the walk only after every entry
+// below it would fail it too (their tmin are >= its own).  So the wave expands
+// the crossed nodes up to 64 at a time from a work stack in LDS, each reached
+// leaf's references are tested by the lane that reached it, and every hit is
+// kept with its place in the walk's order: the leaf's key (kd_reaches' bits,
+// far child at depth k = bit 63 - k; the walk visits smaller keys first) and
+// the reference's index.  The reference's `cmp(t - best) < 0` (first found
+// wins) is then replayed over the hits in that order.  A ray whose walk takes
+// ~10^2-10^3 dependent loads on one lane takes ~ its tree depth in rounds here.
+// `lds`: the wave's `words` 32-bit words (the hard kernels' stack columns).
+// Returns false, nothing written, when the work stack or the hit list outgrows
+// them: the caller walks the ray the serial way.  Node indices < 2^26 (the
+// depth shares their word; the host checks, FastScene::walk_wave).
+constexpr int kWalkHits = 128;  // hits kept for the replay
+__device__ __forceinline__ uint32_t wave_add32(uint32_t v) {
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) v += __shfl_xor(v, sh);
+  return v;
+}
+template <bool COUNT>
+__device__ __forceinline__ bool kd_walk_wave(const DevScene& S, V3 o, V3 d, float rtmin, float rtmax, uint32_t* lds,
+                                             int words, float& t_best, int& best, FastCounters& ctr) {
+  const int lane = __lane_id();
+  t_best = WR_INF;
+  best = -1;
+  float tmin0, tmax0;
+  if (!box_hit(S.root_l, S.root_r, o, d, tmin0, tmax0) || rtmax < tmin0) return true;  // :312-313, :323
+  const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+  // LDS: hit count, the hit list (5 columns), then the work stack (5 columns)
+  uint32_t* hn = lds;
+  uint32_t* h_khi = lds + 1;
+  uint32_t* h_klo = h_khi + kWalkHits;
+  uint32_t* h_ref = h_klo + kWalkHits;
+  float* h_t = reinterpret_cast<float*>(h_ref + kWalkHits);
+  int* h_prim = reinterpret_cast<int*>(h_t + kWalkHits);
+  const int cap = (words - 1 - 5 * kWalkHits) / 5;
+  if (cap < 128) return false;
+  uint32_t* s_node = reinterpret_cast<uint32_t*>(h_prim + kWalkHits);
+  float* s_tmin = reinterpret_cast<float*>(s_node + cap);
+  float* s_tmax = s_tmin + cap;
+  uint32_t* s_khi = reinterpret_cast<uint32_t*>(s_tmax + cap);
+  uint32_t* s_klo = s_khi + cap;
+  if (lane == 0) {
+    *hn = 0u;
+    s_node[0] = 0u;
+    s_tmin[0] = tmin0;
+    s_tmax[0] = tmax0;
+    s_khi[0] = 0u;
+    s_klo[0] = 0u;
+  }
+  __syncthreads();  // one wave per block: orders the LDS writes for the other lanes
+  int sp = 1;  // wave-uniform
+  bool over = false;
+  uint32_t ninner = 0, nleaves = 0, nrefs = 0;
+  while (sp > 0) {
+    const int take = min(sp, 64), base = sp - take;
+    const bool act = lane < take;
+    uint32_t nd = 0, khi = 0, klo = 0;
+    float tmin = 0.f, tmax = 0.f;
+    if (act) {
+      nd = s_node[base + lane];
+      tmin = s_tmin[base + lane];
+      tmax = s_tmax[base + lane];
+      khi = s_khi[base + lane];
+      klo = s_klo[base + lane];
+    }
+    __syncthreads();  // the entries are read before this round's pushes overwrite them
+    const uint32_t node = nd & 0x03ffffffu, depth = nd >> 26;
+    const uint4 w = act ? S.nrec[node] : make_uint4(0u, 0u, 0u, 0u);
+    const bool leaf = act && (w.y & 3u) == 3u;
+    // inner (:325-358): the children this node's walk goes on to
+    int nc = 0;
+    uint32_t c0 = 0, c1 = 0;
+    float c0min = 0.f, c0max = 0.f, c1min = 0.f, c1max = 0.f;
+    uint32_t c0hi = khi, c0lo = klo, c1hi = khi, c1lo = klo;
+    if (act && !leaf) {
+      if (COUNT) ++ninner;
+      const uint32_t axis = w.y & 3u;
+      const float split = __uint_as_float(w.x);
+      const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+      const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+      const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
+      const float t = (split - oa) * ia;
+      const bool below = (oa < split) | ((oa == split) & (da <= 0));
+      const uint32_t left = node + 1, right = w.y >> 2;
+      const uint32_t nearc = below ? left : right, farc = below ? right : left;
+      // the far child's key bit at this depth (a one-child step sets it or
+      // not alike for every leaf below: only the order of two visited
+      // children matters)
+      const uint32_t fhi = depth < 32 ? (0x80000000u >> depth) : 0u, flo = depth < 32 ? 0u : (0x80000000u >> (depth - 32));
+      const uint32_t cd = (depth + 1) << 26;
+      if ((t > tmax) | (t <= 0)) {
+        nc = 1;
+        c0 = nearc | cd;
+        c0min = tmin;
+        c0max = tmax;
+      } else if (t < tmin) {
+        nc = 1;
+        c0 = farc | cd;
+        c0min = tmin;
+        c0max = tmax;
+        c0hi |= fhi;
+        c0lo |= flo;
+      } else {
+        nc = 1;
+        c0 = nearc | cd;
+        c0min = tmin;
+        c0max = t;
+        if (!(rtmax < t)) {  // the far entry's :323 test at its pop
+          nc = 2;
+          c1 = farc | cd;
+          c1min = t;
+          c1max = tmax;
+          c1hi |= fhi;
+          c1lo |= flo;
+        }
+      }
+    }
+    // pushes: one or two entries per lane, packed by prefix counts
+    const unsigned long long m1 = __ballot(nc >= 1), m2 = __ballot(nc == 2);
+    const int pre = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m1 >> 32),
+                                              __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m1), 0)) +
+                    __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m2 >> 32),
+                                              __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m2), 0));
+    const int pushed = __popcll(m1) + __popcll(m2);
+    if (base + pushed > cap) {
+      over = true;
+      break;
+    }
+    if (nc >= 1) {
+      const int i = base + pre;
+      s_node[i] = c0;
+      s_tmin[i] = c0min;
+      s_tmax[i] = c0max;
+      s_khi[i] = c0hi;
+      s_klo[i] = c0lo;
+    }
+    if (nc == 2) {
+      const int i = base + pre + 1;
+      s_node[i] = c1;
+      s_tmin[i] = c1min;
+      s_tmax[i] = c1max;
+      s_khi[i] = c1hi;
+      s_klo[i] = c1lo;
+    }
+    // leaf (:359-373): its references, four records in flight; every hit kept
+    if (leaf) {
+      const uint32_t first = w.x, cnt = w.y >> 2;
+      if (COUNT) {
+        ++nleaves;
+        nrefs += cnt;
+      }
+      for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
+        float4 ra[4], rb[4];
+        float2 rc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t ref = first + min(k0 + u, cnt - 1);
+          ra[u] = S.ref_a[ref];
+          rb[u] = S.ref_b[ref];
+          rc[u] = S.ref_c[ref];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (k0 + u >= cnt) break;
+          float t;
+          // t_best WR_INF: the exact Triangle::hit outcome (the screen drops
+          // only what it proves rejected); the replay applies the rule
+          if (tri_test(ra[u], rb[u], rc[u].x, o, d, rtmin, rtmax, WR_INF, t) && cmpf(t - WR_INF) < 0) {
+            const uint32_t j = atomicAdd(hn, 1u);
+            if (j < static_cast<uint32_t>(kWalkHits)) {
+              h_khi[j] = khi;
+              h_klo[j] = klo;
+              h_ref[j] = first + k0 + u;
+              h_t[j] = t;
+              h_prim[j] = __float_as_int(rc[u].y);
+            }
+          }
+        }
+      }
+    }
+    sp = base + pushed;
+    __syncthreads();  // this round's pushes and hits before the next round's reads
+  }
+  if (COUNT) {
+    ctr.kinner += wave_add32(ninner);
+    ctr.kleaves += wave_add32(nleaves);
+    ctr.krefs += wave_add32(nrefs);
+  }
+  __syncthreads();
+  const int nh = static_cast<int>(*hn);
+  if (over || nh > kWalkHits) return false;
+  // the hits in walk order: each lane ranks its hits among all, then writes
+  // them sorted into the (finished) work stack's columns
+  for (int i = lane; i < nh; i += 64) {
+    const uint32_t ah = h_khi[i], al = h_klo[i], ar = h_ref[i];
+    int rank = 0;
+    for (int j = 0; j < nh; ++j) {
+      const uint32_t bh = h_khi[j], bl = h_klo[j], br = h_ref[j];
+      rank += (bh < ah || (bh == ah && (bl < al || (bl == al && br < ar)))) ? 1 : 0;
+    }
+    s_tmin[rank] = h_t[i];
+    s_node[rank] = static_cast<uint32_t>(h_prim[i]);
+  }
+  __syncthreads();
+  for (int j = 0; j < nh; ++j) {  // wave-uniform: the reference's leaf loop, hit by hit
+    const float t = s_tmin[j];
+    if (cmpf(t - t_best) < 0) {
+      t_best = t;
+      best = static_cast<int>(s_node[j]);
+    }
+  }
+  return true;
 }
 
 // The kTie smallest triangle hits (Triangle::hit) with t <= cap of the ray over
@@ -1373,7 +1595,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
       // p1's membership record: one line with its first four leaves' cells
       const float4* pr = F.prim_rec + 8 * static_cast<size_t>(max(p1, 0));
       const float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3], c4 = pr[4], c5 = pr[5];
-      if (graze_marked(pm)) {
+      if (graze_marked(pm) || (F.diag & 256)) {  // (diag 256: every ray, a test of the walks)
         // the ray runs within ~1e-5 (relative) of the plane of a triangle the
         // search tested (the winner among them): Cramer's rule is near its
         // rounding noise there, beyond the search margins' reach (DESIGN.md
@@ -1468,12 +1690,15 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
 // the pipelines keep WAVE = false.
 // One listed ray's general resolution: the reference's rule over the visited
 // hits near the smallest (resolve_tie), or failing that its KD walk.
-// Returns false only when the one-lane form hands the ray back (kTieDeferred:
-// nothing written; hard_fast resolves it with the whole wave).
+// Returns false only when the one-lane form hands the ray back (kTieDeferred,
+// or a KD walk when walk_wave: *hand_walk set; nothing written; hard_rays
+// resolves it with the whole wave).  The callers' stack columns start at
+// lds + lane: kd_walk_wave takes the wave's whole region.
 template <bool COUNT, bool WAVE>
 __device__ __forceinline__ bool settle_ray(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin, float rtmax,
                                            float t1, int* stk_node, float* stk_tmin, float* outt, int* outp, int r,
-                                           bool lead, FastCounters& ctr, bool walk = false) {
+                                           bool lead, FastCounters& ctr, bool walk = false,
+                                           bool* hand_walk = nullptr) {
   float tb;
   int pb;
   if (!(F.diag & 2) && !walk) {
@@ -1510,11 +1735,18 @@ __device__ __forceinline__ bool settle_ray(const DevScene& S, const FastScene& F
     }
   }
   // unresolved (a crowd of hits near m, or visited hits in the band): the walk decides
+  if (!WAVE && F.walk_wave && hand_walk) {  // by the lane's whole wave, afterwards
+    *hand_walk = true;
+    return false;
+  }
   if (COUNT && lead) ++ctr.fallback;
   if (F.diag & 1) return true;
   const uint64_t c1 = COUNT ? wall_clock64() : 0;
   const uint32_t ki = ctr.kinner, kl = ctr.kleaves, kr = ctr.krefs;
-  kd_walk<COUNT>(S, o, d, rtmin, rtmax, stk_node, stk_tmin, tb, pb, ctr);
+  const bool waved = WAVE && F.walk_wave &&
+                     kd_walk_wave<COUNT>(S, o, d, rtmin, rtmax, reinterpret_cast<uint32_t*>(stk_node - __lane_id()),
+                                         F.depth * 128, tb, pb, ctr);
+  if (!waved) kd_walk<COUNT>(S, o, d, rtmin, rtmax, stk_node, stk_tmin, tb, pb, ctr);
   if (COUNT) {
     if (!lead) {  // the wave walked one ray: counted once
       ctr.kinner = ki;
@@ -1586,11 +1818,11 @@ __device__ __forceinline__ void hard_rays(const DevScene& S, const FastScene& F,
   for (int base = bid * 64; base < nh; base += nb * 64) {  // wave-uniform
     const int i = base + lane;
     ListedRay L{};
-    bool back = false;
+    bool back = false, hw = false;
     if (i < nh) {
       L = get(i);
       back = !settle_ray<COUNT, false>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r,
-                                       true, ctr, L.walk);
+                                       true, ctr, L.walk, &hw);
     }
     for (unsigned long long m = __ballot(back); m != 0ull; m &= m - 1ull) {
       const int src = __ffsll(static_cast<unsigned long long>(m)) - 1;
@@ -1603,7 +1835,7 @@ __device__ __forceinline__ void hard_rays(const DevScene& S, const FastScene& F,
       };
       settle_ray<COUNT, true>(S, F, v3(bf(L.o.x), bf(L.o.y), bf(L.o.z)), v3(bf(L.d.x), bf(L.d.y), bf(L.d.z)),
                               bf(L.rtmin), bf(L.rtmax), bf(L.t1), stk_node, stk_tmin, bp(L.outt), bp(L.outp), bi(L.r),
-                              lane == 0, ctr);
+                              lane == 0, ctr, bi(hw ? 1 : 0) != 0);
     }
   }
 }

@@ -540,8 +540,12 @@ struct wr_context {
   int piece_cap = 1 << 21;
   int piece_min = 655360;
   // pipelines' k_fast_hard: launches with at most this many ties resolve them
-  // one per wave (env WR_TIE_WAVE_MAX; 0: always one per lane)
-  int tie_wave_max = 512;
+  // one per wave (env WR_TIE_WAVE_MAX; 0: always one per lane).  Measured
+  // (C2, profiles/r4/tie_wave_max): 512 -> 4096 lifts 1 iteration from
+  // 1,182 to 1,328 Mrays/s and keeps 20 (2,766 -> 2,788); every tie one per
+  // wave loses at 20 (2,432)
+  int tie_wave_max = 4096;
+  int scan_waves = 256;  // k_fast_hard's scan-list waves (WR_SCAN_WAVES)
   // host threads issuing a render's launches (env WR_ISSUE_THREADS): the
   // pipelines are dealt out to them, each thread issues its pipelines' steps
   int issue_threads = 1;
@@ -1013,10 +1017,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     const int lgrid = std::max(1, std::min(256, blocks));
     const int hgrid = hard_wave ? std::max(1, std::min(2048, max_rays))
                                 : std::max(lgrid, std::min(c->tie_wave_max, max_rays));
-#ifndef WR_SCAN_WAVES
-#define WR_SCAN_WAVES 256
-#endif
-    const int sgrid = std::max(1, std::min(WR_SCAN_WAVES, max_rays));  // scan waves
+    const int sgrid = std::max(1, std::min(c->scan_waves, max_rays));  // scan waves
     auto hk = hard_wave ? (count ? k_fast_hard<true, true> : k_fast_hard<false, true>)
                         : (count ? k_fast_hard<true, false> : k_fast_hard<false, false>);
     hipLaunchKernelGGL(hk, dim3(hgrid + sgrid),
@@ -1459,6 +1460,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   if (const char* e = std::getenv("WR_PIECE_CAP")) c->piece_cap = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("WR_PIECE_MIN")) c->piece_min = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("WR_TIE_WAVE_MAX")) c->tie_wave_max = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("WR_SCAN_WAVES")) c->scan_waves = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("WR_ISSUE_THREADS")) c->issue_threads = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   if (const char* e = std::getenv("WR_DEFER")) c->defer = std::atoi(e) != 0 ? 1 : 0;
   if (const char* e = std::getenv("WR_BDPT_OVERLAP")) c->bdpt_overlap = std::atoi(e) != 0;
@@ -1759,6 +1761,9 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       // both trees
       fs.sdepth = WR_BVH_WIDE == 8 ? 7 * fh.depth8 + 1 : WR_BVH_WIDE == 4 ? 3 * fh.depth4 + 1 : fh.depth + 1;
       fs.depth = std::max(fh.depth + 1, d.max_stack + 1);
+      // kd_walk_wave: node index and depth share a word, the leaf key 64 bits
+      fs.walk_wave = s.nodes.size() < (size_t(1) << 26) && s.dep_max < 64 ? 1 : 0;
+      if (const char* e = std::getenv("WR_WALK_WAVE")) fs.walk_wave = fs.walk_wave && std::atoi(e) != 0;
       c->fast_ok = true;
       int per_cu = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_fast<false, false>, kTraceBlock,
