@@ -235,6 +235,37 @@ __device__ __forceinline__ bool box_crossed_with_margin(float lx, float ly, floa
   return cell_crossed_with_margin(h0, h1, o, d, binv, rtmax);
 }
 
+// Can the reference's walk reach the KD leaf whose cell is (h0.zw, h1) (the
+// header of its path record)?  False only when the ray's LINE misses the cell
+// grown by delta_a = 1e-5 x (|lo_a| + |hi_a| + 2 |o_a|) on every axis.  A leaf is
+// reached only if its walk interval [tmin, tmax] stays non-empty (each near /
+// far step of :331-357 keeps tmin <= tmax), and the interval's ends are float
+// crossings of the cell's own faces (the root box and the splits on its path),
+// each within 3 ulp of the exact crossing; missing the grown cell leaves a gap
+// between the exact crossings far wider than that.  Rays with a near-zero
+// direction component are never pruned.
+__device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3 d) {
+  if (!(fabsf(d.x) > 1e-20f && fabsf(d.y) > 1e-20f && fabsf(d.z) > 1e-20f)) return true;
+  const float lx = __uint_as_float(h0.z), ly = __uint_as_float(h0.w), lz = __uint_as_float(h1.x);
+  const float hx = __uint_as_float(h1.y), hy = __uint_as_float(h1.z), hz = __uint_as_float(h1.w);
+  const float mx = 1e-5f * (fabsf(lx) + fabsf(hx) + 2.f * fabsf(o.x)) + 1e-30f;
+  const float my = 1e-5f * (fabsf(ly) + fabsf(hy) + 2.f * fabsf(o.y)) + 1e-30f;
+  const float mz = 1e-5f * (fabsf(lz) + fabsf(hz) + 2.f * fabsf(o.z)) + 1e-30f;
+  const float ix = 1.f / d.x, iy = 1.f / d.y, iz = 1.f / d.z;
+  const float x0 = (lx - mx - o.x) * ix, x1 = (hx + mx - o.x) * ix;
+  const float y0 = (ly - my - o.y) * iy, y1 = (hy + my - o.y) * iy;
+  const float z0 = (lz - mz - o.z) * iz, z1 = (hz + mz - o.z) * iz;
+  const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+  return !(tn > tf);  // NaN: kept
+}
+
+// WR_SCAN_CELL_FILTER=1: the membership replays (kd_member, scan_rays) skip
+// leaves whose cell the ray's line misses, as the tie resolution does.  Off:
+// 2 mismatches in 600 K plane-grazing Cornell-box rays with it on (round 4).
+#ifndef WR_SCAN_CELL_FILTER
+#define WR_SCAN_CELL_FILTER 0
+#endif
 // Is the primitive whose KD leaves are prim_leaf[lb, lb + ln) tested by the
 // reference's traversal of this ray?  kMember / kNotMember, or kScan: a
 // many-leaf primitive whose located leaf proves nothing, left to the scan
@@ -309,7 +340,9 @@ __device__ __forceinline__ int kd_member(const DevScene& S, const FastScene& F, 
       const bool in = p.x >= __uint_as_float(h0.z) && p.y >= __uint_as_float(h0.w) && p.z >= __uint_as_float(h1.x) &&
                       p.x <= __uint_as_float(h1.y) && p.y <= __uint_as_float(h1.z) && p.z <= __uint_as_float(h1.w);
       if (pass == 0 && ln > 4 && cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return kMember;
-      if (in == (pass == 0) && kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key)) return kMember;
+      if (in == (pass == 0) && (!WR_SCAN_CELL_FILTER || cell_may_be_reached(h0, h1, o, d)) &&
+          kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key))
+        return kMember;
     }
   }
   return kNotMember;
@@ -727,31 +760,6 @@ __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float
     }
     if (cur == 0x7fffffff) return found;
   }
-}
-
-// Can the reference's walk reach the KD leaf whose cell is (h0.zw, h1) (the
-// header of its path record)?  False only when the ray's LINE misses the cell
-// grown by delta_a = 1e-5 x (|lo_a| + |hi_a| + 2 |o_a|) on every axis.  A leaf is
-// reached only if its walk interval [tmin, tmax] stays non-empty (each near /
-// far step of :331-357 keeps tmin <= tmax), and the interval's ends are float
-// crossings of the cell's own faces (the root box and the splits on its path),
-// each within 3 ulp of the exact crossing; missing the grown cell leaves a gap
-// between the exact crossings far wider than that.  Rays with a near-zero
-// direction component are never pruned.
-__device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3 d) {
-  if (!(fabsf(d.x) > 1e-20f && fabsf(d.y) > 1e-20f && fabsf(d.z) > 1e-20f)) return true;
-  const float lx = __uint_as_float(h0.z), ly = __uint_as_float(h0.w), lz = __uint_as_float(h1.x);
-  const float hx = __uint_as_float(h1.y), hy = __uint_as_float(h1.z), hz = __uint_as_float(h1.w);
-  const float mx = 1e-5f * (fabsf(lx) + fabsf(hx) + 2.f * fabsf(o.x)) + 1e-30f;
-  const float my = 1e-5f * (fabsf(ly) + fabsf(hy) + 2.f * fabsf(o.y)) + 1e-30f;
-  const float mz = 1e-5f * (fabsf(lz) + fabsf(hz) + 2.f * fabsf(o.z)) + 1e-30f;
-  const float ix = 1.f / d.x, iy = 1.f / d.y, iz = 1.f / d.z;
-  const float x0 = (lx - mx - o.x) * ix, x1 = (hx + mx - o.x) * ix;
-  const float y0 = (ly - my - o.y) * iy, y1 = (hy + my - o.y) * iy;
-  const float z0 = (lz - mz - o.z) * iz, z1 = (hz + mz - o.z) * iz;
-  const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-  return !(tn > tf);  // NaN: kept
 }
 
 // The first leaf of primitive p that the reference's traversal visits, as its
@@ -1874,16 +1882,32 @@ __device__ __forceinline__ void scan_rays(const DevScene& S, const FastScene& F,
       const V3 inv = v3(1.f / L.d.x, 1.f / L.d.y, 1.f / L.d.z);
       const V3 binv = v3(clamp_inv(L.d.x), clamp_inv(L.d.y), clamp_inv(L.d.z));
       const int lb = F.prim_leaf_off[L.p1], ln = F.prim_leaf_off[L.p1 + 1] - lb;
-      for (int base = 0; base < ln && !member; base += 64) {  // wave-uniform
-        const int k = base + lane;
+      // four leaves per lane and round, their loads in flight together; a
+      // leaf whose cell the ray's line misses is not replayed
+      // (cell_may_be_reached: floors and walls sit in hundreds of leaves)
+      constexpr int U = 4;
+      for (int base = 0; base < ln && !member; base += 64 * U) {  // wave-uniform
+        int po[U];
+        uint4 h0[U], h1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int k = base + u * 64 + lane;
+          po[u] = k < ln ? F.prim_leaf[lb + k] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint2* rec = F.path + max(po[u], 0);
+          h0[u] = *reinterpret_cast<const uint4*>(rec);
+          h1[u] = *reinterpret_cast<const uint4*>(rec + 2);
+        }
         bool ok = false;
-        if (k < ln) {
-          const uint2* rec = F.path + F.prim_leaf[lb + k];
-          const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
-          const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (ok || po[u] < 0) continue;
           unsigned long long key;
-          ok = cell_crossed_with_margin(h0, h1, L.o, L.d, binv, L.rtmax) ||
-               kd_reaches(rec, L.o, L.d, inv, tmin, tmax, L.rtmax, steps, key);
+          ok = cell_crossed_with_margin(h0[u], h1[u], L.o, L.d, binv, L.rtmax) ||
+               ((!WR_SCAN_CELL_FILTER || cell_may_be_reached(h0[u], h1[u], L.o, L.d)) &&
+                kd_reaches(F.path + po[u], L.o, L.d, inv, tmin, tmax, L.rtmax, steps, key));
         }
         member = __ballot(ok) != 0ull;
       }
