@@ -9,7 +9,8 @@
 // would drop.  Built and run by tests/test_cell_filter.py; CPU only.
 //
 //   cell_filter_check SCENE NRAYS SEED
-//   cell_filter_check SCENE --rays RAYS.f32
+//   cell_filter_check SCENE --rays RAYS.f32 [--list]
+// Exit status 1 if any reached leaf would be dropped.
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
@@ -47,8 +48,9 @@ bool box_hit(V l, V r, V o, V d, float& t1, float& t2) {
   return true;
 }
 
-// wr_fast.h cell_may_be_reached, on a cell (lo, hi)
-bool cell_may_be_reached(V lo, V hi, V o, V d) {
+// wr_fast.h cell_may_be_reached, on a cell (lo, hi); tmax0: the root interval's end
+bool cell_may_be_reached(V lo, V hi, V o, V d, float tmax0) {
+  if (!(tmax0 > 0.f)) return true;
   if (!(std::fabs(d.x) > 1e-20f && std::fabs(d.y) > 1e-20f && std::fabs(d.z) > 1e-20f)) return true;
   const float mx = 1e-5f * (std::fabs(lo.x) + std::fabs(hi.x) + 2.f * std::fabs(o.x)) + 1e-30f;
   const float my = 1e-5f * (std::fabs(lo.y) + std::fabs(hi.y) + 2.f * std::fabs(o.y)) + 1e-30f;
@@ -87,10 +89,11 @@ struct Entry {
 
 // the walk; calls leaf(node, lo, hi, tmin, tmax) for every leaf reached
 template <class F>
-void walk(const wr::Scene& s, V o, V d, float rtmax, F leaf) {
+void walk(const wr::Scene& s, V o, V d, float rtmax, float& root_tmax, F leaf) {
   const V rl{s.root_l.x, s.root_l.y, s.root_l.z}, rr{s.root_r.x, s.root_r.y, s.root_r.z};
   float tmin, tmax;
   if (!box_hit(rl, rr, o, d, tmin, tmax) || rtmax < tmin) return;
+  root_tmax = tmax;
   const V inv{1.f / d.x, 1.f / d.y, 1.f / d.z};
   std::vector<Entry> stk;
   Entry cur{0, tmin, tmax, rl, rr};
@@ -159,6 +162,7 @@ int main(int argc, char** argv) {
     while (std::fread(buf, sizeof(float), 8, f) == 8) file_rays.insert(file_rays.end(), buf, buf + 8);
     std::fclose(f);
   }
+  const bool list = argc > 4 && std::string(argv[4]) == "--list";
   const long n = file_rays.empty() ? std::atol(argv[2]) : static_cast<long>(file_rays.size() / 8);
   std::mt19937_64 rng(file_rays.empty() ? static_cast<uint64_t>(std::atoll(argv[3])) : 1u);
   std::uniform_real_distribution<double> U(0.0, 1.0);
@@ -205,28 +209,25 @@ int main(int argc, char** argv) {
     }
     if (!std::isfinite(d.x) || !std::isfinite(d.y) || !std::isfinite(d.z)) continue;
     bool rb = false;
-    walk(s, o, d, 1e7f, [&](const Entry& e) {
+    float root_tmax = 0.f;
+    walk(s, o, d, 1e7f, root_tmax, [&](const Entry& e) {
       ++leaves;
-      // a leaf reached with an all-negative interval (an origin outside the
-      // root box, the ray pointing away): counted apart, and only when one of
-      // its triangles is hit (the walk tests them like any other leaf's)
       if (!(e.tmax > 0.f)) {
-        if (cell_may_be_reached(e.lo, e.hi, o, d)) return;
+        // a leaf reached with an all-negative interval (an origin outside the
+        // root box, the ray pointing away): counted when one of its triangles
+        // is hit at t > EPS all the same (the walk tests it like any leaf)
         const wr::KdNode& nd = s.nodes[static_cast<size_t>(e.node)];
         for (int r = 0; r < nd.count; ++r) {
           float t;
           const wr::Prim& p = s.prims[static_cast<size_t>(s.refs[static_cast<size_t>(nd.first + r)])];
           if (p.type == wr::kTri && tri_hit(p, o, d, t)) {
             ++neg_hit;
-            if (neg_hit <= 5)
-              std::printf("NEG-INTERVAL HIT o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) t=%.9g interval [%.9g %.9g]\n", o.x,
-                          o.y, o.z, d.x, d.y, d.z, t, e.tmin, e.tmax);
+            if (list) std::printf("NEG %ld\n", k);
             break;
           }
         }
-        return;
       }
-      if (!cell_may_be_reached(e.lo, e.hi, o, d)) {
+      if (!cell_may_be_reached(e.lo, e.hi, o, d, root_tmax)) {
         ++bad;
         if (!rb && bad_rays < 20)
           std::printf("DROP ray %ld o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) leaf %d cell (%.9g %.9g %.9g)-(%.9g %.9g %.9g) "
@@ -238,7 +239,7 @@ int main(int argc, char** argv) {
     });
     bad_rays += rb ? 1 : 0;
   }
-  std::printf("rays %ld (grazing %ld) leaves %ld dropped %ld rays_with_drops %ld; dropped all-negative leaves "
-              "with a hit %ld\n", n, grazing, leaves, bad, bad_rays, neg_hit);
-  return 0;
+  std::printf("rays %ld (grazing %ld) leaves %ld dropped %ld rays_with_drops %ld; hits in all-negative leaves %ld\n",
+              n, grazing, leaves, bad, bad_rays, neg_hit);
+  return bad == 0 ? 0 : 1;
 }

@@ -243,8 +243,16 @@ __device__ __forceinline__ bool box_crossed_with_margin(float lx, float ly, floa
 // crossings of the cell's own faces (the root box and the splits on its path),
 // each within 3 ulp of the exact crossing; missing the grown cell leaves a gap
 // between the exact crossings far wider than that.  Rays with a near-zero
-// direction component are never pruned.
-__device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3 d) {
+// direction component are never pruned.  Nor are rays whose root interval
+// (tmax0) is not positive: an origin outside the root box, the ray pointing
+// away.  The walk still runs for them (only `ray.tmax < tmin` stops it), every
+// split crossing is then behind the origin (t <= 0: the near child only, the
+// interval unchanged), so it ends in leaves whose cells the line need not
+// meet -- and Triangle::hit's EPS-fattened test can still hit a triangle there
+// at t > 0 (a wall met just outside the box; 20 of 600 K plane-grazing
+// Cornell-box rays, tests/native/cell_filter_check.cpp).
+__device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3 d, float tmax0) {
+  if (!(tmax0 > 0.f)) return true;
   if (!(fabsf(d.x) > 1e-20f && fabsf(d.y) > 1e-20f && fabsf(d.z) > 1e-20f)) return true;
   const float lx = __uint_as_float(h0.z), ly = __uint_as_float(h0.w), lz = __uint_as_float(h1.x);
   const float hx = __uint_as_float(h1.y), hy = __uint_as_float(h1.z), hz = __uint_as_float(h1.w);
@@ -260,11 +268,10 @@ __device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3
   return !(tn > tf);  // NaN: kept
 }
 
-// WR_SCAN_CELL_FILTER=1: the membership replays (kd_member, scan_rays) skip
-// leaves whose cell the ray's line misses, as the tie resolution does.  Off:
-// 2 mismatches in 600 K plane-grazing Cornell-box rays with it on (round 4).
+// The membership replays (kd_member, scan_rays) skip leaves whose cell the
+// ray's line misses, as the tie resolution does (WR_SCAN_CELL_FILTER=0: off).
 #ifndef WR_SCAN_CELL_FILTER
-#define WR_SCAN_CELL_FILTER 0
+#define WR_SCAN_CELL_FILTER 1
 #endif
 // Is the primitive whose KD leaves are prim_leaf[lb, lb + ln) tested by the
 // reference's traversal of this ray?  kMember / kNotMember, or kScan: a
@@ -340,7 +347,7 @@ __device__ __forceinline__ int kd_member(const DevScene& S, const FastScene& F, 
       const bool in = p.x >= __uint_as_float(h0.z) && p.y >= __uint_as_float(h0.w) && p.z >= __uint_as_float(h1.x) &&
                       p.x <= __uint_as_float(h1.y) && p.y <= __uint_as_float(h1.z) && p.z <= __uint_as_float(h1.w);
       if (pass == 0 && ln > 4 && cell_crossed_with_margin(h0, h1, o, d, binv, rtmax)) return kMember;
-      if (in == (pass == 0) && (!WR_SCAN_CELL_FILTER || cell_may_be_reached(h0, h1, o, d)) &&
+      if (in == (pass == 0) && (!WR_SCAN_CELL_FILTER || cell_may_be_reached(h0, h1, o, d, tmax)) &&
           kd_reaches(rec, o, d, inv, tmin, tmax, rtmax, steps, key))
         return kMember;
     }
@@ -789,7 +796,7 @@ __device__ WR_HARD_CALL void first_leaf(const FastScene& F, int p, V3 o, V3 d, V
     for (int u = 0; u < U; ++u) {
       if (k0 + u >= le) break;
       // a leaf whose cell the ray's line misses is never reached: no replay
-      if (!cell_may_be_reached(h0[u], h1[u], o, d)) continue;
+      if (!cell_may_be_reached(h0[u], h1[u], o, d, tmax0)) continue;
       unsigned long long kk;
       if (!kd_reaches(F.path + off[u], o, d, inv, tmin0, tmax0, rtmax, steps, kk)) continue;
       const int pk = F.prim_leaf_pos[k0 + u];
@@ -855,7 +862,7 @@ __device__ __forceinline__ void first_leaves_wave(const FastScene& F, const int 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       unsigned long long t;
-      if (mine[u] >= 0 && cell_may_be_reached(h0[u], h1[u], o, d) &&
+      if (mine[u] >= 0 && cell_may_be_reached(h0[u], h1[u], o, d, tmax0) &&
           kd_reaches(F.path + po[u], o, d, inv, tmin0, tmax0, rtmax, steps, t)) {
         const int pk = F.prim_leaf_pos[k[u]];
 #pragma unroll
@@ -1906,7 +1913,7 @@ __device__ __forceinline__ void scan_rays(const DevScene& S, const FastScene& F,
           if (ok || po[u] < 0) continue;
           unsigned long long key;
           ok = cell_crossed_with_margin(h0[u], h1[u], L.o, L.d, binv, L.rtmax) ||
-               ((!WR_SCAN_CELL_FILTER || cell_may_be_reached(h0[u], h1[u], L.o, L.d)) &&
+               ((!WR_SCAN_CELL_FILTER || cell_may_be_reached(h0[u], h1[u], L.o, L.d, tmax)) &&
                 kd_reaches(F.path + po[u], L.o, L.d, inv, tmin, tmax, L.rtmax, steps, key));
         }
         member = __ballot(ok) != 0ull;
