@@ -494,7 +494,11 @@ __device__ __forceinline__ bool kd_walk_wave(const DevScene& S, V3 o, V3 d, floa
   bool over = false;
   uint32_t ninner = 0, nleaves = 0, nrefs = 0;
   while (sp > 0) {
-    const int take = min(sp, 64), base = sp - take;
+    // an entry taken pushes at most two: taking no more than the free room
+    // keeps the stack within its columns (a long walk -- C4's reach 10^3-10^4
+    // nodes -- then narrows to the room it has instead of failing over to the
+    // serial walk)
+    const int take = max(1, min(min(sp, 64), cap - sp)), base = sp - take;
     const bool act = lane < take;
     uint32_t nd = 0, khi = 0, klo = 0;
     float tmin = 0.f, tmax = 0.f;
