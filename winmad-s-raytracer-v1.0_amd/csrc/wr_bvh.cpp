@@ -597,7 +597,7 @@ struct Collapse8 {
 
 }  // namespace
 
-void build_fast(const wr::Scene& s, FastHost& out) {
+void build_fast(const wr::Scene& s, FastHost& out, int wide) {
   out = FastHost();
   for (const auto& p : s.prims)
     if (p.type != wr::kTri) {
@@ -678,11 +678,11 @@ void build_fast(const wr::Scene& s, FastHost& out) {
     if (m < 0) m = nn / 2;
     B.inner(0, nn, m, 1);
   }
-  if (out.ok && WR_BVH_WIDE == 4) {
+  if (out.ok && wide == 4) {
     out.nodes4.reserve(out.nodes.size() / 2 + 4);
     Collapse{out}.node(0, 1);
   }
-  if (out.ok && WR_BVH_WIDE == 8) {
+  if (out.ok && wide == 8) {
     out.nodes8.reserve(out.nodes.size() / 4 + 4);
     Collapse8{out}.node(0, 1);
   }

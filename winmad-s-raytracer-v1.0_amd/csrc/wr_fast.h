@@ -37,8 +37,9 @@ namespace wrd {
 
 struct FastScene {
   const float4* nodes;  // 4 per wrf::BNode (tie resolution's collection)
-  const float4* nodes4;  // 8 per wrf::BNode4 (the search, WR_BVH_WIDE 4)
-  const float4* nodes8;  // 8 per wrf::BNode8 (the search, WR_BVH_WIDE 8)
+  const float4* nodes4;  // 8 per wrf::BNode4 (the search when wide == 4)
+  const float4* nodes8;  // 8 per wrf::BNode8 (the search when wide == 8)
+  int wide;              // the search tree's width: 2 (nodes), 4 (nodes4) or 8 (nodes8)
   const float4* tris;   // 3 per wrf::TriRec
   const int* prim_leaf_off;
   const int* prim_leaf;
@@ -66,6 +67,9 @@ struct FastCounters {  // algorithmic work (count_work)
   // k_fast_hard tie resolution and KD walk -- max and sum per ray -- and the
   // rays whose membership test scanned a many-leaf primitive's whole list
   uint32_t mem_max, mem_sum, tie_max, tie_sum, walk_max, walk_sum, scans;
+  // kd_walk_wave (count_work): walks, their rounds and nodes, and fall-backs
+  // to the serial walk (work stack or hit list outgrown)
+  uint32_t ww_walks, ww_rounds, ww_nodes, ww_over;
 };
 
 // Per wave: the stack columns, 8 bytes per entry and lane (BVH: link + entry t;
@@ -79,26 +83,35 @@ __host__ __device__ constexpr size_t fast_lds_bytes(int depth) { return size_t(d
 // global spill area, so that the 4-wide tree's worst case (3 entries per
 // level) does not set the LDS size and with it the waves per CU.
 #ifndef WR_BVH_LDS_STACK
-// the binary tree never spills; the 4-wide one ran with 12; the 8-wide one
-// keeps 16 (a ray's stack outgrows 12 entries for 2e-4 of torus rays, 16 for
-// none in 10^5: scripts/bvh_cost.cpp)
-#define WR_BVH_LDS_STACK (WR_BVH_WIDE == 8 ? 16 : 64)
+#define WR_BVH_LDS_STACK 64  // the binary tree: never spills
 #endif
-constexpr int kLdsStack = WR_BVH_LDS_STACK;
-__host__ __device__ constexpr size_t search_lds_bytes(int depth) {
-  return size_t(depth < kLdsStack ? depth : kLdsStack) * 64 * 6;
+#ifndef WR_BVH4_LDS_STACK
+#define WR_BVH4_LDS_STACK 12  // the 4-wide tree (12 / 16 / 24 measured alike)
+#endif
+// The search tree's width is chosen per scene (FastScene::wide: the 4-wide
+// tree for scenes whose nodes outgrow the L2, wrf::kWide4MinTris); the
+// stack's LDS part per width.  Can it outgrow the LDS columns?  Not for the
+// binary tree (kMaxBvhDepth + 1 entries fit), so its push / pop carry no
+// spill branch: a generic pointer select between LDS and the spill area made
+// the compiler emit flat loads (vmcnt + lgkmcnt waits) on every pop.
+template <int W>
+struct SearchStack {
+  // the 8-wide tree keeps 16 (a ray's stack outgrows 12 entries for 2e-4 of
+  // torus rays, 16 for none in 10^5: scripts/bvh_cost.cpp)
+  static constexpr int lds = W == 4 ? WR_BVH4_LDS_STACK : W == 8 ? 16 : WR_BVH_LDS_STACK;
+  static constexpr bool spills =
+      (W == 8 ? 7 * wrf::kMaxBvhDepth + 1 : W == 4 ? 3 * wrf::kMaxBvhDepth + 1 : wrf::kMaxBvhDepth + 1) > lds;
+};
+__host__ __device__ constexpr int search_lds_stack(int wide) {
+  return wide == 4 ? SearchStack<4>::lds : wide == 8 ? SearchStack<8>::lds : SearchStack<2>::lds;
+}
+__host__ __device__ constexpr size_t search_lds_bytes(int depth, int wide) {
+  return size_t(depth < search_lds_stack(wide) ? depth : search_lds_stack(wide)) * 64 * 6;
 }
 // spill entries per lane for a search stack of `depth` entries
-__host__ __device__ constexpr size_t search_spill_entries(int depth) {
-  return depth > kLdsStack ? size_t(depth - kLdsStack) : 0;
+__host__ __device__ constexpr size_t search_spill_entries(int depth, int wide) {
+  return depth > search_lds_stack(wide) ? size_t(depth - search_lds_stack(wide)) : 0;
 }
-// Can the search's stack outgrow the LDS columns?  Not for the binary tree
-// (kMaxBvhDepth + 1 entries fit), so its push / pop carry no spill branch: a
-// generic pointer select between LDS and the spill area made the compiler emit
-// flat loads (vmcnt + lgkmcnt waits) on every pop.
-constexpr bool kSearchSpills =
-    (WR_BVH_WIDE == 8 ? 7 * wrf::kMaxBvhDepth + 1 : WR_BVH_WIDE == 4 ? 3 * wrf::kMaxBvhDepth + 1 : wrf::kMaxBvhDepth + 1) >
-    kLdsStack;
 // Speculative leaves (Aila & Laine 2009): a lane that has found its leaf keeps
 // descending inner nodes while other lanes still look for theirs, and the
 // leaf is tested (postponed) with theirs.  Extra nodes visited under a stale
@@ -441,18 +454,24 @@ __device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtm
 // popped todo entry's tmax is the entry below it, which is the parent's tmax);
 // and the :323 stop at a popped far child ends the walk only after every entry
 // below it would fail it too (their tmin are >= its own).  So the wave expands
-// the crossed nodes up to 64 at a time from a work stack in LDS, each reached
-// leaf's references are tested by the lane that reached it, and every hit is
-// kept with its place in the walk's order: the leaf's key (kd_reaches' bits,
-// far child at depth k = bit 63 - k; the walk visits smaller keys first) and
-// the reference's index.  The reference's `cmp(t - best) < 0` (first found
-// wins) is then replayed over the hits in that order.  A ray whose walk takes
-// ~10^2-10^3 dependent loads on one lane takes ~ its tree depth in rounds here.
+// the crossed nodes up to 64 at a time from a work stack in LDS, and each
+// reached leaf's references are tested by the lane that reached it.  A hit's
+// place in the walk's order is its leaf's key (kd_reaches' bits, far child at
+// depth k = bit 63 - k; the walk visits smaller keys first) with its position
+// in the leaf in the key's free low bits.  Only each primitive's first hit in
+// that order can matter -- the same ray and triangle give the same t, so a
+// later repeat fails `cmp(t - best) < 0` whether the first was taken or not --
+// and a floor or wall sits in hundreds of the leaves a ray crosses: the hits
+// go to a hash table in LDS keyed by primitive, keeping the smallest order
+// (atomicMin).  The reference's rule, first found wins, is then replayed over
+// the primitives sorted by that order: kd_walk's answer.  A ray whose walk
+// takes ~10^3 dependent loads on one lane takes ~ its tree depth plus its
+// nodes / 64 in rounds here (C4: 40 rounds for 1,640 nodes).
 // `lds`: the wave's `words` 32-bit words (the hard kernels' stack columns).
-// Returns false, nothing written, when the work stack or the hit list outgrows
+// Returns false, nothing written, when the work stack or the table outgrows
 // them: the caller walks the ray the serial way.  Node indices < 2^26 (the
-// depth shares their word; the host checks, FastScene::walk_wave).
-constexpr int kWalkHits = 128;  // hits kept for the replay
+// depth shares their word) and KD depth <= 43 (the position's bits): the host
+// checks, FastScene::walk_wave.
 __device__ __forceinline__ uint32_t wave_add32(uint32_t v) {
 #pragma unroll
   for (int sh = 32; sh >= 1; sh >>= 1) v += __shfl_xor(v, sh);
@@ -467,22 +486,25 @@ __device__ __forceinline__ bool kd_walk_wave(const DevScene& S, V3 o, V3 d, floa
   float tmin0, tmax0;
   if (!box_hit(S.root_l, S.root_r, o, d, tmin0, tmax0) || rtmax < tmin0) return true;  // :312-313, :323
   const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-  // LDS: hit count, the hit list (5 columns), then the work stack (5 columns)
-  uint32_t* hn = lds;
-  uint32_t* h_khi = lds + 1;
-  uint32_t* h_klo = h_khi + kWalkHits;
-  uint32_t* h_ref = h_klo + kWalkHits;
-  float* h_t = reinterpret_cast<float*>(h_ref + kWalkHits);
-  int* h_prim = reinterpret_cast<int*>(h_t + kWalkHits);
-  const int cap = (words - 1 - 5 * kWalkHits) / 5;
-  if (cap < 128) return false;
-  uint32_t* s_node = reinterpret_cast<uint32_t*>(h_prim + kWalkHits);
+  // LDS: the table (order u64, primitive, t: 4 words a slot), then the work
+  // stack (5 columns, at least as many entries as the table has slots: the
+  // replay's sorted primitives go to its first two columns)
+  const int lg = words >= 2048 ? 8 : 7, T = 1 << lg;
+  const int cap = (words - 4 * T) / 5;
+  if (cap < T || cap < 128) return false;
+  unsigned long long* h_ord = reinterpret_cast<unsigned long long*>(lds);
+  int* h_prim = reinterpret_cast<int*>(h_ord + T);
+  float* h_t = reinterpret_cast<float*>(h_prim + T);
+  uint32_t* s_node = reinterpret_cast<uint32_t*>(h_t + T);
   float* s_tmin = reinterpret_cast<float*>(s_node + cap);
   float* s_tmax = s_tmin + cap;
   uint32_t* s_khi = reinterpret_cast<uint32_t*>(s_tmax + cap);
   uint32_t* s_klo = s_khi + cap;
+  for (int i = lane; i < T; i += 64) {
+    h_ord[i] = ~0ull;
+    h_prim[i] = -1;
+  }
   if (lane == 0) {
-    *hn = 0u;
     s_node[0] = 0u;
     s_tmin[0] = tmin0;
     s_tmax[0] = tmax0;
@@ -491,14 +513,15 @@ __device__ __forceinline__ bool kd_walk_wave(const DevScene& S, V3 o, V3 d, floa
   }
   __syncthreads();  // one wave per block: orders the LDS writes for the other lanes
   int sp = 1;  // wave-uniform
-  bool over = false;
+  bool over = false, full = false;
+  uint32_t rounds = 0;
   uint32_t ninner = 0, nleaves = 0, nrefs = 0;
   while (sp > 0) {
     // an entry taken pushes at most two: taking no more than the free room
-    // keeps the stack within its columns (a long walk -- C4's reach 10^3-10^4
-    // nodes -- then narrows to the room it has instead of failing over to the
-    // serial walk)
+    // keeps the stack within its columns (a long walk then narrows to the
+    // room it has instead of failing over to the serial walk)
     const int take = max(1, min(min(sp, 64), cap - sp)), base = sp - take;
+    ++rounds;
     const bool act = lane < take;
     uint32_t nd = 0, khi = 0, klo = 0;
     float tmin = 0.f, tmax = 0.f;
@@ -588,13 +611,15 @@ __device__ __forceinline__ bool kd_walk_wave(const DevScene& S, V3 o, V3 d, floa
       s_khi[i] = c1hi;
       s_klo[i] = c1lo;
     }
-    // leaf (:359-373): its references, four records in flight; every hit kept
+    // leaf (:359-373): its references, four records in flight; each hit into
+    // the table under its primitive, the smallest order kept
     if (leaf) {
       const uint32_t first = w.x, cnt = w.y >> 2;
       if (COUNT) {
         ++nleaves;
         nrefs += cnt;
       }
+      const unsigned long long key = (static_cast<unsigned long long>(khi) << 32) | klo;
       for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
         float4 ra[4], rb[4];
         float2 rc[4];
@@ -612,14 +637,19 @@ __device__ __forceinline__ bool kd_walk_wave(const DevScene& S, V3 o, V3 d, floa
           // t_best WR_INF: the exact Triangle::hit outcome (the screen drops
           // only what it proves rejected); the replay applies the rule
           if (tri_test(ra[u], rb[u], rc[u].x, o, d, rtmin, rtmax, WR_INF, t) && cmpf(t - WR_INF) < 0) {
-            const uint32_t j = atomicAdd(hn, 1u);
-            if (j < static_cast<uint32_t>(kWalkHits)) {
-              h_khi[j] = khi;
-              h_klo[j] = klo;
-              h_ref[j] = first + k0 + u;
-              h_t[j] = t;
-              h_prim[j] = __float_as_int(rc[u].y);
+            const int prim = __float_as_int(rc[u].y);
+            uint32_t h = (static_cast<uint32_t>(prim) * 2654435761u) >> (32 - lg);
+            bool put = false;
+            for (int probe = 0; probe < T && !put; ++probe) {
+              const int was = atomicCAS(&h_prim[h], -1, prim);
+              if (was == -1 || was == prim) {
+                atomicMin(&h_ord[h], key | (k0 + u));
+                h_t[h] = t;  // (every repeat writes the same t)
+                put = true;
+              }
+              h = (h + 1) & static_cast<uint32_t>(T - 1);
             }
+            full |= !put;
           }
         }
       }
@@ -627,28 +657,37 @@ __device__ __forceinline__ bool kd_walk_wave(const DevScene& S, V3 o, V3 d, floa
     sp = base + pushed;
     __syncthreads();  // this round's pushes and hits before the next round's reads
   }
-  if (COUNT) {
-    ctr.kinner += wave_add32(ninner);
-    ctr.kleaves += wave_add32(nleaves);
-    ctr.krefs += wave_add32(nrefs);
-  }
   __syncthreads();
-  const int nh = static_cast<int>(*hn);
-  if (over || nh > kWalkHits) return false;
-  // the hits in walk order: each lane ranks its hits among all, then writes
-  // them sorted into the (finished) work stack's columns
-  for (int i = lane; i < nh; i += 64) {
-    const uint32_t ah = h_khi[i], al = h_klo[i], ar = h_ref[i];
-    int rank = 0;
-    for (int j = 0; j < nh; ++j) {
-      const uint32_t bh = h_khi[j], bl = h_klo[j], br = h_ref[j];
-      rank += (bh < ah || (bh == ah && (bl < al || (bl == al && br < ar)))) ? 1 : 0;
+  full = __ballot(full) != 0ull;
+  // the primitives hit, in walk order: each lane ranks its slots' entries
+  // among all (orders are distinct: one primitive per leaf position), then
+  // writes them sorted into the (finished) work stack's columns
+  int nh = 0;
+  if (!over && !full) {
+    for (int i = lane; i < T; i += 64) {
+      if (h_prim[i] < 0) continue;
+      const unsigned long long a = h_ord[i];
+      int rank = 0;
+      for (int j = 0; j < T; ++j) rank += (h_prim[j] >= 0 && h_ord[j] < a) ? 1 : 0;
+      s_tmin[rank] = h_t[i];
+      s_node[rank] = static_cast<uint32_t>(h_prim[i]);
+      ++nh;
     }
-    s_tmin[rank] = h_t[i];
-    s_node[rank] = static_cast<uint32_t>(h_prim[i]);
+    nh = static_cast<int>(wave_add32(static_cast<uint32_t>(nh)));
   }
+  if (COUNT) {
+    const uint32_t a = wave_add32(ninner), b = wave_add32(nleaves);
+    ctr.kinner += a;
+    ctr.kleaves += b;
+    ctr.krefs += wave_add32(nrefs);
+    ctr.ww_walks += 1;
+    ctr.ww_rounds += rounds;
+    ctr.ww_nodes += a + b;
+    ctr.ww_over += (over ? 1000u : 0u) + (full ? 1u : 0u);  // (stack x 1000 + table)
+  }
+  if (over || full) return false;
   __syncthreads();
-  for (int j = 0; j < nh; ++j) {  // wave-uniform: the reference's leaf loop, hit by hit
+  for (int j = 0; j < nh; ++j) {  // wave-uniform: the reference's leaf loop, primitive by primitive
     const float t = s_tmin[j];
     if (cmpf(t - t_best) < 0) {
       t_best = t;
@@ -1205,10 +1244,12 @@ __device__ __forceinline__ bool tri_grazes(float4 a, float4 b, float f, V3 o, V3
   return fabsf(den) <= kGrazeRel * mag && fabsf(tnum) <= kGrazePlaneRel * tmag;
 }
 
-template <bool COUNT>
+template <bool COUNT, int W>
 __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, int* fetch,
                                            float* t2buf, int2* spill, uint32_t* lds, FastCounters& ctr,
                                            int bid, int nblk) {  // this block's index among the launch's nblk search blocks
+  constexpr int kLdsStack = SearchStack<W>::lds;
+  constexpr bool kSearchSpills = SearchStack<W>::spills;
   const int lane = __lane_id();
   int* stk_link = reinterpret_cast<int*>(lds) + lane;
   uint16_t* stk_t = reinterpret_cast<uint16_t*>(reinterpret_cast<int*>(lds) + min(F.sdepth, kLdsStack) * 64) + lane;
@@ -1367,7 +1408,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           ++ctr.nodes;
           ++rn;
         }
-#if WR_BVH_WIDE == 4
+        if constexpr (W == 4) {
         // a 4-wide node: the four boxes, then the hit children nearest first
         // (the nearest is visited next, the others pushed farthest first)
         const float4* np = F.nodes4 + 8 * static_cast<size_t>(cur);
@@ -1410,7 +1451,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           if (nh > 1) push(l1, k1);
           cur = l0;
         }
-#elif WR_BVH_WIDE == 8
+        } else if constexpr (W == 8) {
         // an 8-wide node (wrf::BNode8, one 128-byte line): the eight child
         // boxes decoded from bytes, fmaf(q, scale, org) -- the build made each
         // contain the binary tree's box, bit for bit checked -- and tested as
@@ -1469,7 +1510,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
             if (i < nh) push(lk8[i], tk[i]);
           cur = lk8[0];
         }
-#else
+        } else {
         const float4* np = F.nodes + 4 * static_cast<size_t>(cur);
         const float4 n0 = np[0], n1 = np[1], n2 = np[2];
         const int4 lk = *reinterpret_cast<const int4*>(np + 3);
@@ -1495,7 +1536,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         } else {
           pop();
         }
-#endif
+        }
       }
     }
     // ---- leaf: test its triangles (Triangle::hit), keep (t1, p1) and t2

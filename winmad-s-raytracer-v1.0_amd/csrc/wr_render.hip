@@ -150,6 +150,7 @@ struct DevCounters {
   unsigned long long verify_rays, verify_bad;                   // WR_BVH_VERIFY
   unsigned long long deferred;  // BDPT rays settled off the critical path (late lists)
   unsigned long long lat[7];  // WR_TRACE_BVH latency tail (FastCounters mem_max .. scans; max or sum)
+  unsigned long long ww[4];   // kd_walk_wave: walks, rounds, nodes, serial fall-backs
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -263,6 +264,11 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
     if (k % 2 == 0 && k < 6) atomicMax(&ctr->lat[k], static_cast<unsigned long long>(lat[k]));
     else atomicAdd(&ctr->lat[k], static_cast<unsigned long long>(lat[k]));
   }
+  if (lane_id() == 0) {  // (wave-uniform: counted by the walking wave's lane 0 only)
+    const uint32_t ww[4] = {fc.ww_walks, fc.ww_rounds, fc.ww_nodes, fc.ww_over};
+    for (int k = 0; k < 4; ++k)
+      if (ww[k]) atomicAdd(&ctr->ww[k], static_cast<unsigned long long>(ww[k]));
+  }
 }
 #ifndef WR_FAST_WAVES
 #define WR_FAST_WAVES 4  // minimum waves per SIMD the search's registers must allow
@@ -270,7 +276,8 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
 // LATE: blocks [0, lblocks) settle the previous step's deferred hard rays
 // (its late lists, late_hard) beside this step's search; they come first so
 // that they are dispatched with the search's persistent blocks, not after them
-template <bool COUNT, bool LATE>
+// W: the search tree's width (FastScene::wide)
+template <bool COUNT, bool LATE, int W>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WR_FAST_WAVES, 8))) WR_NO_PK_FP32
 k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* spill,
              LateArgs L, int lblocks, int gn, int hblocks, int lane_blocks, int wave_max) {
@@ -285,10 +292,21 @@ k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetc
       atomicAdd(&ctr->deferred, static_cast<unsigned long long>(min(L.n[m][0], half) + min(L.n[m][1], half)));
     }
   } else {
-    trace_fast<COUNT>(S, F, Q, fetch, t2buf, spill, smem, fc, b - (LATE ? lblocks : 0),
-                      static_cast<int>(gridDim.x) - (LATE ? lblocks : 0));
+    trace_fast<COUNT, W>(S, F, Q, fetch, t2buf, spill, smem, fc, b - (LATE ? lblocks : 0),
+                         static_cast<int>(gridDim.x) - (LATE ? lblocks : 0));
   }
   if (COUNT) fast_counts<COUNT>(ctr, fc);
+}
+// the search kernel for a tree width (instantiated for 2 and 4; 8 when the
+// library is built with WR_BVH_WIDE=8)
+using TraceFastKernel = void (*)(DevScene, FastScene, TraceQueues, DevCounters*, int*, float*, int2*, LateArgs, int, int,
+                                 int, int, int);
+template <bool COUNT, bool LATE>
+TraceFastKernel trace_fast_kernel(int wide) {
+#if WR_BVH_WIDE == 8
+  if (wide == 8) return k_trace_fast<COUNT, LATE, 8>;
+#endif
+  return wide == 4 ? k_trace_fast<COUNT, LATE, 4> : k_trace_fast<COUNT, LATE, 2>;
 }
 template <bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
@@ -909,8 +927,9 @@ TraceSlot tslot(Pipe& p, int slot) {
 // t2 scratch + hard-ray list of a pipeline for launches of up to `rays` rays
 int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
   if (!c->fast_on) return WR_OK;
-  if (!p.spill && search_spill_entries(c->fs.sdepth) > 0)
-    HIPCHK(hipMalloc(&p.spill, search_spill_entries(c->fs.sdepth) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
+  if (!p.spill && search_spill_entries(c->fs.sdepth, c->fs.wide) > 0)
+    HIPCHK(hipMalloc(&p.spill,
+                     search_spill_entries(c->fs.sdepth, c->fs.wide) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
   if (p.t2_cap >= rays) return WR_OK;
   if (p.t2buf) (void)hipFree(p.t2buf);
   p.t2buf = nullptr;
@@ -980,7 +999,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
   if (c->fast_on && !c->stamps && ts.t2 && static_cast<size_t>(max_rays) <= ts.t2_cap) {
     const int blocks = (max_rays + kTraceBlock - 1) / kTraceBlock;
     const int fgrid = std::max(1, std::min(c->fast_blocks, blocks));
-    const size_t lds = fast_lds_bytes(c->fs.depth), slds = search_lds_bytes(c->fs.sdepth);
+    const size_t lds = fast_lds_bytes(c->fs.depth), slds = search_lds_bytes(c->fs.sdepth, c->fs.wide);
     hipEvent_t f0 = nullptr, f1 = nullptr, fa = nullptr, fb = nullptr;
     if (c->trace_log) {
       (void)hipEventCreate(&f0);
@@ -991,7 +1010,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     }
     if (late_prev) {  // + the previous step's deferred hard rays, beside the search
       const int lblocks = late_gn * (kLateTieBlocks + kLateScanBlocks);
-      auto kf = count ? k_trace_fast<true, true> : k_trace_fast<false, true>;
+      auto kf = count ? trace_fast_kernel<true, true>(c->fs.wide) : trace_fast_kernel<false, true>(c->fs.wide);
       hipLaunchKernelGGL(kf, dim3(lblocks + fgrid),
                          dim3(kTraceBlock), std::max(slds, lds), stream, c->ds, c->fs, Q, ctr, fetch, ts.t2, ts.spill,
                          *late_prev, lblocks, late_gn, kLateTieBlocks, kLateLaneBlocks, kLateTieBlocks);
@@ -999,7 +1018,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
         hipLaunchKernelGGL(k_late_verify, dim3(64, late_gn), dim3(kTraceBlock), lds, stream, c->ds, c->fs, *late_prev,
                            ctr);
     } else {
-      auto kf = count ? k_trace_fast<true, false> : k_trace_fast<false, false>;
+      auto kf = count ? trace_fast_kernel<true, false>(c->fs.wide) : trace_fast_kernel<false, false>(c->fs.wide);
       hipLaunchKernelGGL(kf, dim3(fgrid),
                          dim3(kTraceBlock), slds, stream, c->ds, c->fs, Q, ctr, fetch, ts.t2, ts.spill, LateArgs{}, 0,
                          1, 0, 0, 0);
@@ -1267,6 +1286,14 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
                  lat[0] * 0.01, lat[1] * 0.01, lat[2] * 0.01, lat[3] * 0.01, lat[4] * 0.01, lat[5] * 0.01, lat[6]);
     std::fprintf(stderr, "[wr bvh walks] many-leaf %llu, no visited hit %llu, crowd %llu, band %llu\n", why[0], why[1],
                  why[2], why[3]);
+    unsigned long long ww[4] = {0, 0, 0, 0};
+    for (int i = 0; i < n; ++i) {
+      DevCounters h;
+      HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
+      for (int k = 0; k < 4; ++k) ww[k] += h.ww[k];
+    }
+    std::fprintf(stderr, "[wr bvh wave walks] %llu walks, %.1f rounds and %.1f nodes per walk, %llu serial fall-backs\n",
+                 ww[0], ww[0] ? double(ww[1]) / ww[0] : 0.0, ww[0] ? double(ww[2]) / ww[0] : 0.0, ww[3]);
     std::fprintf(stderr, "[wr bvh tail] max nodes/ray %llu, max tests/ray %llu, rays > 256 nodes %llu, ties resolved by visit order %llu\n",
                  mx[0], mx[1], mx[2], ties);
   }
@@ -1689,8 +1716,22 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   // ---- verified-BVH traversal data (wr_bvh.h): BVH nodes, triangle records
   // in leaf order, and the KD root paths of every primitive's leaves
   {
+    // the search tree's width: 4-wide for scenes whose binary tree outgrows
+    // the L2 (its nodes then come from the Infinity Cache / HBM, and one
+    // 128-byte node holds two of the binary tree's levels: C4 +5-8 %, while
+    // L2-resident scenes lose 1-4 %: DESIGN.md 4b); WR_BVH_WIDE=2|4 forces
+    int wide = WR_BVH_WIDE;
+    if (wide == 2) {
+      size_t tris = 0;
+      for (const wr::Prim& p : s.prims) tris += p.type == wr::kTri ? 1 : 0;
+      if (tris >= wrf::kWide4MinTris) wide = 4;
+    }
+    if (const char* e = std::getenv("WR_BVH_WIDE")) {
+      const int w = std::atoi(e);
+      if (w == 2 || w == 4 || (w == 8 && WR_BVH_WIDE == 8)) wide = w;
+    }
     wrf::FastHost fh;
-    wrf::build_fast(s, fh);
+    wrf::build_fast(s, fh, wide);
     if (fh.ok) {
       const size_t fbn = fh.nodes.size(), ftr = fh.tris.size(), fpo = fh.prim_leaf_off.size(),
                    fpl = std::max<size_t>(1, fh.prim_leaf.size()), fpa = fh.path.size() / 2;
@@ -1759,15 +1800,17 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       fs.hi = v3(hi[0], hi[1], hi[2]);
       // the search's stack holds BVH entries only; the hard rays' kernel walks
       // both trees
-      fs.sdepth = WR_BVH_WIDE == 8 ? 7 * fh.depth8 + 1 : WR_BVH_WIDE == 4 ? 3 * fh.depth4 + 1 : fh.depth + 1;
+      fs.wide = wide;
+      fs.sdepth = wide == 8 ? 7 * fh.depth8 + 1 : wide == 4 ? 3 * fh.depth4 + 1 : fh.depth + 1;
       fs.depth = std::max(fh.depth + 1, d.max_stack + 1);
-      // kd_walk_wave: node index and depth share a word, the leaf key 64 bits
-      fs.walk_wave = s.nodes.size() < (size_t(1) << 26) && s.dep_max < 64 ? 1 : 0;
+      // kd_walk_wave: node index and depth share a word, the leaf key and the
+      // position in the leaf 64 bits
+      fs.walk_wave = s.nodes.size() < (size_t(1) << 26) && s.dep_max <= 43 ? 1 : 0;
       if (const char* e = std::getenv("WR_WALK_WAVE")) fs.walk_wave = fs.walk_wave && std::atoi(e) != 0;
       c->fast_ok = true;
       int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_fast<false, false>, kTraceBlock,
-                                                       search_lds_bytes(fs.sdepth)) != hipSuccess ||
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_fast_kernel<false, false>(wide), kTraceBlock,
+                                                       search_lds_bytes(fs.sdepth, wide)) != hipSuccess ||
           per_cu <= 0)
         per_cu = 8;
       // diagnostic: WR_FAST_WAVES_PER_CU caps the search's resident waves
@@ -1781,7 +1824,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       if (const char* e = std::getenv("WR_BVH_VERIFY")) c->verify = std::atoi(e) != 0;
       if (c->trace_log)
         std::fprintf(stderr, "[wr bvh] nodes %zu tris %zu depth %d lds %zu B/wave, %d waves/CU -> grid %d; kd grid %d\n",
-                     fbn, ftr, fs.sdepth, search_lds_bytes(fs.sdepth), per_cu, c->fast_blocks, c->trace_blocks);
+                     fbn, ftr, fs.sdepth, search_lds_bytes(fs.sdepth, wide), per_cu, c->fast_blocks, c->trace_blocks);
     }
   }
   *out = c;
@@ -1897,8 +1940,9 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   }
   QueueList ql;
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
-  if (c->fast_on && !c->api_spill && search_spill_entries(c->fs.sdepth) > 0)
-    HIPCHK(hipMalloc(&c->api_spill, search_spill_entries(c->fs.sdepth) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
+  if (c->fast_on && !c->api_spill && search_spill_entries(c->fs.sdepth, c->fs.wide) > 0)
+    HIPCHK(hipMalloc(&c->api_spill,
+                     search_spill_entries(c->fs.sdepth, c->fs.wide) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
   const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard[0], c->api_spill};
   trace_launch(c, c->stream, c->ctr, ts, tm, false, ql.Q, ql.max_rays,
                c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN), true);
