@@ -316,11 +316,13 @@ def main():
         if trace == "bvh":
             # the KD counters cover only the fallback rays (their own B_ray terms
             # minus the ray load / hit store, which every ray pays once here):
-            # + 64 B per BVH node record, 48 B per triangle record, 8 B per KD
-            # path entry replayed
-            total_bytes += 64.0 * cst.bvh_nodes + 48.0 * cst.bvh_tests + 8.0 * cst.kd_replay_steps \
+            # + 64 B per BVH node record (128 B per 4-wide node), 48 B per
+            # triangle record, 8 B per KD path entry replayed
+            node_bytes = 128.0 if cst.bvh_width == 4 else 64.0
+            total_bytes += node_bytes * cst.bvh_nodes + 48.0 * cst.bvh_tests + 8.0 * cst.kd_replay_steps \
                 - 48.0 * cst.fallback_rays
-            bvh = {"nodes_per_ray": round(cst.bvh_nodes / rays, 2), "tests_per_ray": round(cst.bvh_tests / rays, 2),
+            bvh = {"width": int(cst.bvh_width), "nodes_per_ray": round(cst.bvh_nodes / rays, 2),
+                   "tests_per_ray": round(cst.bvh_tests / rays, 2),
                    "replay_steps_per_ray": round(cst.kd_replay_steps / rays, 2),
                    "fallback_frac": round(cst.fallback_rays / rays, 5),
                    "kd_tests_per_fallback_ray": round(cst.prim_tests / max(1, cst.fallback_rays), 1)}
@@ -367,7 +369,7 @@ def main():
             roofline["traffic_over_ray_io"] = round(traffic / (48.0 * rays / max(1, trace_launches)), 3)
         if bvh:
             roofline["kernel"] = "k_trace_fast (verified BVH closest hit) + k_trace over its fallback rays"
-            roofline["algorithmic_bytes"] = ("BVH: 48 B per ray + 64 B per node + 48 B per triangle test + 8 B per "
+            roofline["algorithmic_bytes"] = ("BVH: 48 B per ray + 64 B per node (128 per 4-wide node) + 48 B per triangle test + 8 B per "
                                              "KD path entry replayed; fallback rays: SURVEY.md 8(d) B_ray")
             roofline["bvh"] = bvh
 

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define WR_API_VERSION 6
+#define WR_API_VERSION 7
 
 enum {
   WR_OK = 0,
@@ -145,6 +145,9 @@ typedef struct {
   int64_t deferred_rays;     /* WR_TRACE_BVH BDPT: rays settled off the pipeline's
                                 critical path, their paths shaded a step later
                                 (deferred hard rays; API v6)        */
+  int64_t bvh_width;         /* WR_TRACE_BVH: the search tree's width, 2 or 4 (4
+                                from 2^18 triangles); 0: KD walk
+                                (API v7)                                         */
 } wr_stats;
 
 /* The reference's in-memory Scene (scene/scene.h:35-42) as flat host arrays,

@@ -1263,6 +1263,7 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
   st->verify_mismatches += static_cast<int64_t>(sum.verify_bad);
   st->pipelines = std::max<int64_t>(st->pipelines, n);
   st->deferred_rays += static_cast<int64_t>(sum.deferred);
+  st->bvh_width = c->fast_on ? c->fs.wide : 0;
   if (c->trace_log && c->fast_on) {
     unsigned long long mx[3] = {0, 0, 0};
     for (int i = 0; i < n; ++i) {
@@ -2674,6 +2675,7 @@ static void add_stats(wr_stats* d, const wr_stats& s) {
   d->verify_mismatches += s.verify_mismatches;
   d->pipelines = std::max(d->pipelines, s.pipelines);
   d->deferred_rays += s.deferred_rays;
+  d->bvh_width = std::max(d->bvh_width, s.bvh_width);
 }
 
 static int ensure_dev_film(wr_context* d, float** buf, size_t* have, size_t nf) {

@@ -87,7 +87,7 @@ class WrStats(C.Structure):
                 ("prim_tests", C.c_int64), ("bvh_nodes", C.c_int64), ("bvh_tests", C.c_int64),
                 ("kd_replay_steps", C.c_int64), ("fallback_rays", C.c_int64), ("verify_rays", C.c_int64),
                 ("verify_mismatches", C.c_int64), ("pipelines", C.c_int64),
-                ("deferred_rays", C.c_int64)]
+                ("deferred_rays", C.c_int64), ("bvh_width", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
