@@ -597,7 +597,7 @@ struct Collapse8 {
 
 }  // namespace
 
-void build_fast(const wr::Scene& s, FastHost& out, int wide) {
+void build_fast(const wr::Scene& s, FastHost& out, int wide, bool with4) {
   out = FastHost();
   for (const auto& p : s.prims)
     if (p.type != wr::kTri) {
@@ -678,7 +678,7 @@ void build_fast(const wr::Scene& s, FastHost& out, int wide) {
     if (m < 0) m = nn / 2;
     B.inner(0, nn, m, 1);
   }
-  if (out.ok && wide == 4) {
+  if (out.ok && (wide == 4 || with4)) {
     out.nodes4.reserve(out.nodes.size() / 2 + 4);
     Collapse{out}.node(0, 1);
   }

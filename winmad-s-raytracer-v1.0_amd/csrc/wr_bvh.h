@@ -157,8 +157,9 @@ struct FastHost {
 };
 // Build the BVH over the scene's triangles and the KD membership data.  Scenes
 // with spheres keep the faithful traversal only (ok = false).
-// wide: the search tree built beside the binary one (4: nodes4, 8: nodes8)
-void build_fast(const wr::Scene& s, FastHost& out, int wide = WR_BVH_WIDE);
+// wide: the search tree built beside the binary one (4: nodes4, 8: nodes8);
+// with4: the 4-wide one as well (a binary-tree scene's latency-bound renders)
+void build_fast(const wr::Scene& s, FastHost& out, int wide = WR_BVH_WIDE, bool with4 = false);
 // scenes of at least this many triangles search the 4-wide tree (a binary
 // tree of 2^18 triangles is ~28 MB of nodes and records: past the 4 MB L2)
 #ifndef WR_BVH4_MIN_TRIS

@@ -569,6 +569,13 @@ struct wr_context {
   int issue_threads = 1;
   // verified-BVH traversal (wr_fast.h): built at wr_create for triangle scenes
   FastScene fs{};
+  // a binary-tree scene's 4-wide tree, searched by renders whose pipelines
+  // hold one group each (latency-bound: C2 at 1 iteration +6 %, -3 % at 20);
+  // wide_now: the tree the current render searches (0: fs)
+  int sdepth4 = 0;  // the 4-wide tree's search stack (search_scene)
+  bool fs4_ok = false;
+  bool lat_wide = true;  // env WR_BVH_WIDE_LAT=0: off
+  int wide_now = 0;
   Arena fast_mem;
   bool fast_ok = false;   // scene supports it
   bool fast_on = false;   // WR_TRACE_BVH mode selected
@@ -925,11 +932,26 @@ TraceSlot tslot(Pipe& p, int slot) {
   return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap, &p.sc[0].hard[slot][0], p.spill};
 }
 // t2 scratch + hard-ray list of a pipeline for launches of up to `rays` rays
+// search-stack spill entries per lane: the larger of the context's trees
+size_t max_spill_entries(const wr_context* c) {
+  size_t e = search_spill_entries(c->fs.sdepth, c->fs.wide);
+  if (c->fs4_ok) e = std::max(e, search_spill_entries(c->sdepth4, 4));
+  return e;
+}
+// the scene as the current render searches it: fs, or fs with its 4-wide
+// tree (every other field -- KD stack depth, diagnostics -- is fs's own)
+FastScene search_scene(const wr_context* c) {
+  FastScene F = c->fs;
+  if (c->wide_now == 4 && c->fs4_ok) {
+    F.wide = 4;
+    F.sdepth = c->sdepth4;
+  }
+  return F;
+}
 int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
   if (!c->fast_on) return WR_OK;
-  if (!p.spill && search_spill_entries(c->fs.sdepth, c->fs.wide) > 0)
-    HIPCHK(hipMalloc(&p.spill,
-                     search_spill_entries(c->fs.sdepth, c->fs.wide) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
+  if (!p.spill && max_spill_entries(c) > 0)
+    HIPCHK(hipMalloc(&p.spill, max_spill_entries(c) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
   if (p.t2_cap >= rays) return WR_OK;
   if (p.t2buf) (void)hipFree(p.t2buf);
   p.t2buf = nullptr;
@@ -997,9 +1019,10 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
   if (c->no_cut)  // measurement knob: the same launches without the dead-work elision
     for (int i = 0; i < Q.n; ++i) Q.q[i].cut = nullptr;
   if (c->fast_on && !c->stamps && ts.t2 && static_cast<size_t>(max_rays) <= ts.t2_cap) {
+    const FastScene F = search_scene(c);  // the render's search tree
     const int blocks = (max_rays + kTraceBlock - 1) / kTraceBlock;
     const int fgrid = std::max(1, std::min(c->fast_blocks, blocks));
-    const size_t lds = fast_lds_bytes(c->fs.depth), slds = search_lds_bytes(c->fs.sdepth, c->fs.wide);
+    const size_t lds = fast_lds_bytes(c->fs.depth), slds = search_lds_bytes(F.sdepth, F.wide);
     hipEvent_t f0 = nullptr, f1 = nullptr, fa = nullptr, fb = nullptr;
     if (c->trace_log) {
       (void)hipEventCreate(&f0);
@@ -1010,24 +1033,24 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     }
     if (late_prev) {  // + the previous step's deferred hard rays, beside the search
       const int lblocks = late_gn * (kLateTieBlocks + kLateScanBlocks);
-      auto kf = count ? trace_fast_kernel<true, true>(c->fs.wide) : trace_fast_kernel<false, true>(c->fs.wide);
+      auto kf = count ? trace_fast_kernel<true, true>(F.wide) : trace_fast_kernel<false, true>(F.wide);
       hipLaunchKernelGGL(kf, dim3(lblocks + fgrid),
-                         dim3(kTraceBlock), std::max(slds, lds), stream, c->ds, c->fs, Q, ctr, fetch, ts.t2, ts.spill,
+                         dim3(kTraceBlock), std::max(slds, lds), stream, c->ds, F, Q, ctr, fetch, ts.t2, ts.spill,
                          *late_prev, lblocks, late_gn, kLateTieBlocks, kLateLaneBlocks, kLateTieBlocks);
       if (c->verify)
-        hipLaunchKernelGGL(k_late_verify, dim3(64, late_gn), dim3(kTraceBlock), lds, stream, c->ds, c->fs, *late_prev,
+        hipLaunchKernelGGL(k_late_verify, dim3(64, late_gn), dim3(kTraceBlock), lds, stream, c->ds, F, *late_prev,
                            ctr);
     } else {
-      auto kf = count ? trace_fast_kernel<true, false>(c->fs.wide) : trace_fast_kernel<false, false>(c->fs.wide);
+      auto kf = count ? trace_fast_kernel<true, false>(F.wide) : trace_fast_kernel<false, false>(F.wide);
       hipLaunchKernelGGL(kf, dim3(fgrid),
-                         dim3(kTraceBlock), slds, stream, c->ds, c->fs, Q, ctr, fetch, ts.t2, ts.spill, LateArgs{}, 0,
+                         dim3(kTraceBlock), slds, stream, c->ds, F, Q, ctr, fetch, ts.t2, ts.spill, LateArgs{}, 0,
                          1, 0, 0, 0);
     }
     if (c->trace_log) (void)hipEventRecord(fa, stream);
     int* hard = reinterpret_cast<int*>(ts.t2 + ts.t2_cap);
     hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
                        dim3(std::max(1, std::min(c->resolve_blocks > 0 ? c->resolve_blocks : c->fast_blocks, blocks))),
-                       dim3(kTraceBlock), 0, stream, c->ds, c->fs,
+                       dim3(kTraceBlock), 0, stream, c->ds, F,
                        Q, ctr, ts.t2, hard, ts.hard_n, static_cast<int>(ts.t2_cap));
     if (c->trace_log) (void)hipEventRecord(fb, stream);
     // the hard rays are a few in 10^4: a small grid drains any count (one
@@ -1040,11 +1063,11 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     auto hk = hard_wave ? (count ? k_fast_hard<true, true> : k_fast_hard<false, true>)
                         : (count ? k_fast_hard<true, false> : k_fast_hard<false, false>);
     hipLaunchKernelGGL(hk, dim3(hgrid + sgrid),
-                       dim3(kTraceBlock), lds, stream, c->ds, c->fs, Q, ctr, hard, ts.hard_n,
+                       dim3(kTraceBlock), lds, stream, c->ds, F, Q, ctr, hard, ts.hard_n,
                        static_cast<int>(ts.t2_cap), hgrid, lgrid, std::min(hgrid, c->tie_wave_max));
     if (c->verify)
       hipLaunchKernelGGL(k_fast_verify, dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), lds,
-                         stream, c->ds, c->fs, Q, ctr);
+                         stream, c->ds, F, Q, ctr);
     tm.mark(WR_K_TRACE);
     if (c->trace_log) {
       (void)hipEventRecord(f1, stream);
@@ -1732,7 +1755,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       if (w == 2 || w == 4 || (w == 8 && WR_BVH_WIDE == 8)) wide = w;
     }
     wrf::FastHost fh;
-    wrf::build_fast(s, fh, wide);
+    wrf::build_fast(s, fh, wide, wide == 2);
     if (fh.ok) {
       const size_t fbn = fh.nodes.size(), ftr = fh.tris.size(), fpo = fh.prim_leaf_off.size(),
                    fpl = std::max<size_t>(1, fh.prim_leaf.size()), fpa = fh.path.size() / 2;
@@ -1803,6 +1826,11 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       // both trees
       fs.wide = wide;
       fs.sdepth = wide == 8 ? 7 * fh.depth8 + 1 : wide == 4 ? 3 * fh.depth4 + 1 : fh.depth + 1;
+      if (wide == 2 && !fh.nodes4.empty()) {
+        c->sdepth4 = 3 * fh.depth4 + 1;
+        c->fs4_ok = true;
+      }
+      if (const char* e = std::getenv("WR_BVH_WIDE_LAT")) c->lat_wide = std::atoi(e) != 0;
       fs.depth = std::max(fh.depth + 1, d.max_stack + 1);
       // kd_walk_wave: node index and depth share a word, the leaf key and the
       // position in the leaf 64 bits
@@ -1941,9 +1969,8 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   }
   QueueList ql;
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
-  if (c->fast_on && !c->api_spill && search_spill_entries(c->fs.sdepth, c->fs.wide) > 0)
-    HIPCHK(hipMalloc(&c->api_spill,
-                     search_spill_entries(c->fs.sdepth, c->fs.wide) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
+  if (c->fast_on && !c->api_spill && max_spill_entries(c) > 0)
+    HIPCHK(hipMalloc(&c->api_spill, max_spill_entries(c) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
   const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard[0], c->api_spill};
   trace_launch(c, c->stream, c->ctr, ts, tm, false, ql.Q, ql.max_rays,
                c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN), true);
@@ -2110,6 +2137,16 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   if (fit < 1) return WR_E_HIP;  // message set by the allocation
   const PiecePlan plan = plan_pieces(f_lo, f_hi, P, unit, cap, fit, c->piece_min);
   const int np = plan.pipes();
+  // a render whose pipelines hold one group each is latency-bound: its
+  // searches take the 4-wide tree when the scene has one beside the binary
+  // (DESIGN.md 4b, C2 at 1 iteration +6 %); longer renders keep the binary
+  size_t most_groups = 0;
+  for (const auto& pp : plan.per_pipe) most_groups = std::max(most_groups, pp.size());
+  struct WideNow {
+    wr_context* c;
+    ~WideNow() { c->wide_now = 0; }
+  } wide_guard{c};
+  c->wide_now = (most_groups <= 1 && c->fs4_ok && c->lat_wide) ? 4 : 0;
   // the buffer sets, queues and shadow-queue bounds below are laid out for `cap`
   // paths: a larger piece would write past them
   for (const auto& pp : plan.per_pipe)
