@@ -1286,7 +1286,7 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
   st->verify_mismatches += static_cast<int64_t>(sum.verify_bad);
   st->pipelines = std::max<int64_t>(st->pipelines, n);
   st->deferred_rays += static_cast<int64_t>(sum.deferred);
-  st->bvh_width = c->fast_on ? c->fs.wide : 0;
+  st->bvh_width = c->fast_on ? (c->wide_now ? c->wide_now : c->fs.wide) : 0;  // the tree this render searched
   if (c->trace_log && c->fast_on) {
     unsigned long long mx[3] = {0, 0, 0};
     for (int i = 0; i < n; ++i) {
