@@ -2137,16 +2137,18 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   if (fit < 1) return WR_E_HIP;  // message set by the allocation
   const PiecePlan plan = plan_pieces(f_lo, f_hi, P, unit, cap, fit, c->piece_min);
   const int np = plan.pipes();
-  // a render whose pipelines hold one group each is latency-bound: its
-  // searches take the 4-wide tree when the scene has one beside the binary
-  // (DESIGN.md 4b, C2 at 1 iteration +6 %); longer renders keep the binary
+  // a render too short to fill the pipelines that fit, each holding one
+  // group, is latency-bound: its searches take the 4-wide tree when the scene
+  // has one beside the binary (DESIGN.md 4b, C2 at 1 iteration +2.3 %);
+  // renders that fill the pipelines keep the binary (C2 at 20 iterations,
+  // 16 pipelines of one group each: 4-wide -3 %)
   size_t most_groups = 0;
   for (const auto& pp : plan.per_pipe) most_groups = std::max(most_groups, pp.size());
   struct WideNow {
     wr_context* c;
     ~WideNow() { c->wide_now = 0; }
   } wide_guard{c};
-  c->wide_now = (most_groups <= 1 && c->fs4_ok && c->lat_wide) ? 4 : 0;
+  c->wide_now = (np < fit && most_groups <= 1 && c->fs4_ok && c->lat_wide) ? 4 : 0;
   // the buffer sets, queues and shadow-queue bounds below are laid out for `cap`
   // paths: a larger piece would write past them
   for (const auto& pp : plan.per_pipe)
