@@ -277,8 +277,12 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
 // (its late lists, late_hard) beside this step's search; they come first so
 // that they are dispatched with the search's persistent blocks, not after them
 // W: the search tree's width (FastScene::wide)
+#ifndef WR_FAST4_WAVES
+#define WR_FAST4_WAVES 5  // the 4-wide search: 98 VGPRs at 4, held to 96 for 5 waves per SIMD
+#endif
 template <bool COUNT, bool LATE, int W>
-__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WR_FAST_WAVES, 8))) WR_NO_PK_FP32
+__global__ void __launch_bounds__(kTraceBlock)
+__attribute__((amdgpu_waves_per_eu(W == 4 && !LATE ? WR_FAST4_WAVES : WR_FAST_WAVES, 8))) WR_NO_PK_FP32
 k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* spill,
              LateArgs L, int lblocks, int gn, int hblocks, int lane_blocks, int wave_max) {
   extern __shared__ uint32_t smem[];
