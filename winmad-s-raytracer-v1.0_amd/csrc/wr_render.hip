@@ -312,8 +312,16 @@ TraceFastKernel trace_fast_kernel(int wide) {
 #endif
   return wide == 4 ? k_trace_fast<COUNT, LATE, 4> : k_trace_fast<COUNT, LATE, 2>;
 }
+#ifndef WR_RESOLVE_WAVES
+#define WR_RESOLVE_WAVES 0  // > 0: the resolve's register budget as waves per SIMD (0: the compiler's choice, 101 VGPRs)
+#endif
+#if WR_RESOLVE_WAVES > 0
+#define WR_RESOLVE_OCC __attribute__((amdgpu_waves_per_eu(WR_RESOLVE_WAVES, 8)))
+#else
+#define WR_RESOLVE_OCC
+#endif
 template <bool COUNT>
-__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32
+__global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32 WR_RESOLVE_OCC
 k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf, int* hard, int* hard_n,
                int hcap) {
   FastCounters fc{};
