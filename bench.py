@@ -105,6 +105,20 @@ def cpu_baseline(kind, scene_path, W, H, budget, chunks=16):
 REFDRV = os.path.join(REPO, "oracle", "_ref", "refdrv")
 
 
+def _cpu_share():
+    """CPUs this process may run on (its affinity mask), else os.cpu_count();
+    env WR_CPU_BASELINE_CORES overrides (a positive integer; anything else is
+    ignored)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    v = os.environ.get("WR_CPU_BASELINE_CORES", "").strip()
+    if v.isdigit() and int(v) > 0:
+        n = int(v)
+    return max(1, n)
+
+
 def cpu_reference(cfg_name, kind, W, H, tmp, shrink):
     """The reference ITSELF on the host: oracle/_ref/refdrv is the reference's own
     translation units compiled by oracle/Makefile (test infrastructure).  It
@@ -136,11 +150,9 @@ def cpu_reference(cfg_name, kind, W, H, tmp, shrink):
     sec = float(next(l for l in r.stdout.splitlines() if l.startswith("render_seconds")).split()[1])
     # all cores of this box's CPU share: the same sample in `ncores` concurrent
     # single-threaded reference processes (the reference has no threading).
-    # The GPU box gives one job 16 CPUs (OMP_NUM_THREADS / MAX_JOBS = 16 there)
-    # while os.cpu_count() shows the whole machine's: capped at the share
-    machine_cpus = os.cpu_count() or 1
-    share = int(os.environ.get("OMP_NUM_THREADS") or 16)
-    ncores = max(1, min(share, 16, machine_cpus))
+    # The GPU box gives one job 16 CPUs while os.cpu_count() shows the whole
+    # machine's: the CPUs this process may run on, capped at that share
+    ncores = max(1, min(16, _cpu_share()))
     procs = [subprocess.Popen([REFDRV, *map(str, args[:-1]), out + f".{k}"], stdout=subprocess.PIPE,
                               stderr=subprocess.DEVNULL, text=True, env=env) for k in range(ncores)]
     outs = [p.communicate(timeout=900) for p in procs]

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define WR_API_VERSION 7
+#define WR_API_VERSION 8
 
 enum {
   WR_OK = 0,
@@ -222,11 +222,17 @@ int wr_film_reduce(wr_context* ctx, float* film_dev, int64_t nfloat, int root);
  * ~5 GB per pair of iterations at 1080p): iterations / samples are dealt
  * round-robin to them so that one stream's late-bounce traversal tail overlaps
  * another's full launches.  1..16; default = the process's hardware queues
- * (GPU_MAX_HW_QUEUES) up to 16, or env WR_PIPES.  Loading the library raises
- * GPU_MAX_HW_QUEUES to 16 (unless set higher, or env WR_HW_QUEUES=n asks for n):
- * effective when the library loads before the process's first HIP call.
+ * (GPU_MAX_HW_QUEUES, read when wr_create runs) up to 16, or env WR_PIPES.
  * GPU-specific scheduling; no reference counterpart. */
 int wr_set_pipelines(wr_context* ctx, int n);
+/* Ask HIP for n hardware queues (1..32) -- one per render pipeline -- by
+ * raising GPU_MAX_HW_QUEUES to n (a larger value already set is kept).  HIP
+ * reads the variable once, when it initialises: call this at the top of main(),
+ * before the process's first HIP call and before other threads start (it
+ * writes the process environment).  Returns the queue count in effect for
+ * contexts created later, or WR_E_ARG.  The library never changes the
+ * environment otherwise (API v8). */
+int wr_request_hw_queues(int n);
 
 /* Allocate now what renders of this integrator and film size on the context
  * will use -- every pipeline's work buffers (each device of a multi-device
@@ -321,7 +327,9 @@ typedef struct {
   uint32_t fingerprint[2]; /* (lo, hi) of a 64-bit hash of the scene
                               (wr_scene_fingerprint) and the integrator's
                               settings, set by the writer; a resume whose
-                              own hash differs is refused (0 = not recorded) */
+                              own hash differs is refused.  0 = not recorded:
+                              the C++ mirror (csrc/integrators.h) refuses such
+                              a film too, e.g. one written before API v7 */
 } wr_checkpoint_info; /* 32 bytes */
 int wr_checkpoint_save(const char* path, const wr_checkpoint_info* info, const float* film);
 /* film == NULL reads the header only; else film_floats must be height*width*3.

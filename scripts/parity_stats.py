@@ -1,14 +1,22 @@
 #!/usr/bin/env python3
 """Distribution of GPU-vs-oracle film differences (counter RNG, same streams)
-over the parity cases of tests/test_gpu*.py plus the larger C3 / C4 films --
-the data the film gates in tests/_parity.py are set from.
+over parity cases beside the -m gpu suite's (larger C3 / C4 / 1080p films) --
+and the derivation of the film gates in tests/_parity.py from them.
 
-Per case: relative RMSE (RMSE / RMS(oracle)), per-channel RMSE, and the
+Measure: per case, relative RMSE (RMSE / RMS(oracle)), per-channel RMSE, the
 fraction of film values whose relative difference exceeds 1e-6 .. 1e-3
-(relative to max(|oracle|, 1e-3 x mean |oracle|)), plus ray-count deltas.
-Writes one JSON line per case to stdout (and --out).
+(relative to max(|oracle|, 1e-3 x mean |oracle|)), split pixels, their largest
+8-connected cluster and busiest row / column, plus ray-count deltas.  Writes
+one JSON line per case to stdout (and --out).
 
     python scripts/parity_stats.py [--out gpurun_out/parity_stats.jsonl] [--quick]
+
+Derive: the per-case maxima of such logs -- this script's and the suite's own
+(WR_PARITY_LOG=<file> WR_PARITY_MEASURE=1 pytest -m gpu: every
+tests/_parity.py gate logs its statistics) -- become
+tests/golden/parity_limits.json, which the gates read:
+
+    python scripts/parity_stats.py --derive profiles/r5/parity_suite.jsonl profiles/r5/parity_stats.jsonl
 """
 import argparse
 import json
@@ -45,8 +53,9 @@ def stats(a, b):
     out["pix_rel_gt_1e-3"] = int((rel > 1e-3).any(axis=2).sum())
     out["npix"] = int(rel.shape[0] * rel.shape[1])
     g = _parity.film_stats(a, b)
-    for k in ("bias", "bad_pixels", "trimmed_rel_rmse", "trimmed_bias"):
+    for k in ("bias", "bad_pixels", "trimmed_rel_rmse", "trimmed_bias", "max_cluster", "max_row", "max_col"):
         out[k] = g[k]
+    out["ch_rel_rmse"] = [float(x) for x in g["ch_rel_rmse"]]
     return out
 
 
@@ -60,25 +69,34 @@ def big_torus(W, H):
 def cases(quick):
     # (name, kind, scene maker, W, H, gpu kwargs, oracle call)
     c = [
-        ("bdpt_torus64_i4", "bdpt", lambda: _scenes.torus(64, 64), 64, 64, dict(iterations=4, seed=5489)),
-        ("bdpt_torus96x64_i2", "bdpt", lambda: _scenes.torus(96, 64), 96, 64, dict(iterations=2, seed=5489)),
-        ("bdpt_torus64_ctl0", "bdpt", lambda: _scenes.torus(64, 64), 64, 64,
+        ("bdpt_torus64x64_i4_s5489", "bdpt", lambda: _scenes.torus(64, 64), 64, 64, dict(iterations=4, seed=5489)),
+        ("bdpt_torus96x64_i2_s5489", "bdpt", lambda: _scenes.torus(96, 64), 96, 64, dict(iterations=2, seed=5489)),
+        ("bdpt_torus64x64_i2_s5489", "bdpt", lambda: _scenes.torus(64, 64), 64, 64, dict(iterations=2, seed=5489)),
+        ("bdpt_torus64x64_i2_s11_ctl0", "bdpt", lambda: _scenes.torus(64, 64), 64, 64,
          dict(iterations=2, seed=11, control_length=0)),
-        ("bdpt_spheres64_i4", "bdpt", lambda: _scenes.spheres(64, 64), 64, 64, dict(iterations=4, seed=5489)),
-        ("bdpt_torus256_i2", "bdpt", lambda: _scenes.torus(256, 256), 256, 256, dict(iterations=2, seed=5)),
-        ("pt_cbox64x48_s16", "pt", lambda: _scenes.cbox(64, 48), 64, 48, dict(spp=16, max_depth=7, seed=5489)),
-        ("pt_spheres64_s16", "pt", lambda: _scenes.spheres(64, 64), 64, 64, dict(spp=16, max_depth=7, seed=5489)),
-        ("pt_cbox40x30_s12", "pt", lambda: _scenes.cbox(40, 30), 40, 30, dict(spp=12, max_depth=7, seed=31)),
+        ("bdpt_spheres64x64_i4_s5489", "bdpt", lambda: _scenes.spheres(64, 64), 64, 64, dict(iterations=4, seed=5489)),
+        ("bdpt_torus256x256_i2_s5", "bdpt", lambda: _scenes.torus(256, 256), 256, 256, dict(iterations=2, seed=5)),
+        ("pt_cbox64x48_spp16_s5489", "pt", lambda: _scenes.cbox(64, 48), 64, 48,
+         dict(spp=16, max_depth=7, seed=5489)),
+        ("pt_spheres64x64_spp16_s5489", "pt", lambda: _scenes.spheres(64, 64), 64, 64,
+         dict(spp=16, max_depth=7, seed=5489)),
+        ("pt_cbox40x30_spp12_s31", "pt", lambda: _scenes.cbox(40, 30), 40, 30, dict(spp=12, max_depth=7, seed=31)),
         ("vcm_torus64_i3", "vcm", lambda: _scenes.torus(64, 64), 64, 64,
          dict(iterations=3, seed=3, radius_factor=0.05)),
         ("vcm_tent64_i2", "vcm", lambda: _scenes.tent(64, 64), 64, 64, dict(iterations=2, seed=3, radius_factor=0.05)),
     ]
     if not quick:
         c += [
-            ("bdpt_torus1080p_i1", "bdpt", lambda: _scenes.torus(1920, 1080), 1920, 1080,
+            ("bdpt_torus1920x1080_i1_s5489", "bdpt", lambda: _scenes.torus(1920, 1080), 1920, 1080,
              dict(iterations=1, seed=5489)),
-            ("pt_cbox480x270_s4", "pt", lambda: _scenes.cbox(480, 270), 480, 270, dict(spp=4, max_depth=7, seed=5489)),
-            ("bdpt_torus1m_384x216_i1", "bdpt", lambda: big_torus(384, 216), 384, 216, dict(iterations=1, seed=5489)),
+            ("bdpt_torus1920x1080_i1_s7", "bdpt", lambda: _scenes.torus(1920, 1080), 1920, 1080,
+             dict(iterations=1, seed=7)),
+            ("pt_cbox480x270_spp4_s5489", "pt", lambda: _scenes.cbox(480, 270), 480, 270,
+             dict(spp=4, max_depth=7, seed=5489)),
+            ("bdpt_torus1m384x216_i1_s5489", "bdpt", lambda: big_torus(384, 216), 384, 216,
+             dict(iterations=1, seed=5489)),
+            ("bdpt_cbox480x270_i1_s5489_ctl0", "bdpt", lambda: _scenes.cbox(480, 270, "bdpt"), 480, 270,
+             dict(iterations=1, seed=5489, control_length=0)),
             ("vcm_torus1080p_i1", "vcm", lambda: _scenes.torus(1920, 1080), 1920, 1080, dict(iterations=1, seed=5489)),
         ]
     return c
@@ -111,7 +129,10 @@ def run_case(name, kind, maker, W, H, kw, trace):
     r["d_shadow"] = int(st.shadow_rays - rst.shadow_rays)
     r["rays"] = int(rst.closest_rays + rst.shadow_rays)
     try:
-        (_parity.assert_vcm_parity if kind == "vcm" else _parity.assert_film_parity)(film, ref)
+        if kind == "vcm":
+            _parity.assert_vcm_parity(film, ref, case=name)
+        else:
+            _parity.assert_film_parity(film, ref, case=name)
         r["gate"] = "pass"
     except AssertionError as e:
         r["gate"] = "FAIL " + str(e)[:300]
@@ -119,12 +140,47 @@ def run_case(name, kind, maker, W, H, kw, trace):
     return r
 
 
+def derive(logs, out_path):
+    """Per-case maxima of the logged gate statistics -> tests/golden/parity_limits.json."""
+    cases = {}
+    for p in logs:
+        for line in open(p):
+            r = json.loads(line)
+            if r.get("kind", "film") == "vcm" or r["case"].startswith("vcm"):
+                continue
+            m = cases.setdefault(r["case"], {"bad_pixels": 0, "max_cluster": 0, "max_row": 0, "max_col": 0,
+                                             "bias": 0.0, "ch_rel_rmse": 0.0, "pixels": r.get("pixels") or r.get("npix"),
+                                             "samples": 0})
+            for k in ("bad_pixels", "max_cluster", "max_row", "max_col"):
+                m[k] = max(m[k], int(r[k]))
+            m["bias"] = max(m["bias"], abs(float(r["bias"])))
+            m["ch_rel_rmse"] = max(m["ch_rel_rmse"], max(float(x) for x in r["ch_rel_rmse"]))
+            m["samples"] += 1
+    doc = {"source": [os.path.relpath(p, REPO) for p in logs],
+           "note": "per-case maxima of the GPU-vs-oracle film statistics; tests/_parity.py derives its gates "
+                   "from them (split pixels <= max(16, 4x), cluster <= max(3, 2x), row/column <= max(4, 2x), "
+                   "|bias| <= max(2e-5, 4x))",
+           "cases": dict(sorted(cases.items()))}
+    with open(out_path, "w") as f:
+        json.dump(doc, f, indent=1)
+        f.write("\n")
+    for k, m in sorted(cases.items()):
+        print(f"{k:40s} n={m['samples']} bad={m['bad_pixels']} cl={m['max_cluster']} row={m['max_row']} "
+              f"col={m['max_col']} bias={m['bias']:.2e} chrel={m['ch_rel_rmse']:.2e}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--trace", default="reference", choices=["reference", "bvh"])
+    ap.add_argument("--derive", nargs="+", default=None, metavar="LOG",
+                    help="write tests/golden/parity_limits.json from these JSONL logs and exit")
     args = ap.parse_args()
+    if args.derive:
+        derive(args.derive, _parity.LIMITS_PATH)
+        return
+    os.environ["WR_PARITY_MEASURE"] = "1"
     f = open(args.out, "a") if args.out else None
     for cs in cases(args.quick):
         r = run_case(*cs, trace=args.trace)

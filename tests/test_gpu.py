@@ -108,7 +108,7 @@ def test_bdpt_matches_oracle_counter_rng(W, H, it):
     path = _scenes.torus(W, H)
     film, st = ctx(path).render_bdpt(W, H, iterations=it, seed=5489)
     ref, rst = _oracle.Scene(path).bdpt(W, H, it, 5489, mode=1)
-    assert_film_parity(film, ref)
+    assert_film_parity(film, ref, case=f"bdpt_torus{W}x{H}_i{it}_s5489")
     assert_ray_counts(st, rst)
 
 
@@ -116,7 +116,7 @@ def test_bdpt_all_lengths_and_control_length_filter():
     path = _scenes.torus(64, 64)
     f_all, _ = ctx(path).render_bdpt(64, 64, iterations=2, seed=11, control_length=0)
     r_all, _ = _oracle.Scene(path).bdpt(64, 64, 2, 11, mode=1, control_length=0)
-    assert_film_parity(f_all, r_all)
+    assert_film_parity(f_all, r_all, case="bdpt_torus64x64_i2_s11_ctl0")
     f3, _ = ctx(path).render_bdpt(64, 64, iterations=2, seed=11)
     assert f_all.mean() > f3.mean()  # the length-3 filter drops energy
 
@@ -139,7 +139,7 @@ def test_pt_matches_oracle_counter_rng():
     film, st = ctx(path).render_path(64, 48, spp=16, max_depth=7, seed=5489)
     ref, rst = _oracle.Scene(path).pt(64, 48, 16, 7, 5489, mode=1)
     film = film * np.float32(1.0 / 16)  # the oracle (like the reference) scales by 1/spp
-    assert_film_parity(film, ref)
+    assert_film_parity(film, ref, case="pt_cbox64x48_spp16_s5489")
     assert_ray_counts(st, rst)
 
 
@@ -158,7 +158,7 @@ def test_pt_sample_range_matches_oracle():
     path = _scenes.cbox(64, 48)
     film, st = ctx(path).render_path(64, 48, spp=9, max_depth=7, seed=8, sample_begin=3, sample_count=5)
     ref, rst = _oracle.Scene(path).pt_samples(64, 48, 9, 3, 5, 7, 8)
-    assert_film_parity(film, ref)
+    assert_film_parity(film, ref, case="pt_cbox64x48_spp9_k3n5_s8")
     assert_ray_counts(st, rst)
 
 
@@ -226,8 +226,26 @@ def test_bdpt_1080p_matches_oracle_counter_rng():
     path = _scenes.torus(W, H)
     film, st = ctx(path).render_bdpt(W, H, iterations=1, seed=5489)
     ref, rst = _oracle.Scene(path).bdpt(W, H, 1, 5489, mode=1)
-    assert_film_parity(film, ref)
+    assert_film_parity(film, ref, case="bdpt_torus1920x1080_i1_s5489")
     assert_ray_counts(st, rst)
+    if os.environ.get("WR_PARITY_MEASURE") == "1":  # the measurement run logs the real film only
+        return
+    # the gates catch the GPU film damaged the ways tests/test_parity_gates.py
+    # damages oracle films: one 8-row tile band not written (verdict r4: at
+    # 1080p that moves the per-channel RMSE by only ~3e-4), one row's splats a
+    # pixel off
+    sums = np.abs(ref).reshape(H // 8, 8, -1).sum(axis=(1, 2))
+    lit = np.nonzero(sums > 0)[0]
+    for band in (int(np.argmax(sums)), int(lit[len(lit) // 2])):
+        bad = film.copy()
+        bad[8 * band:8 * band + 8] = 0
+        with pytest.raises(AssertionError):
+            assert_film_parity(bad, ref, case="bdpt_torus1920x1080_i1_s5489")
+    row = int(np.argmax(np.abs(ref).sum(axis=(1, 2))))
+    bad = film.copy()
+    bad[row] = np.roll(film[row], 1, axis=0)
+    with pytest.raises(AssertionError):
+        assert_film_parity(bad, ref, case="bdpt_torus1920x1080_i1_s5489")
 
 
 def test_path_radiance_per_ray_matches_oracle():
@@ -425,7 +443,7 @@ def test_bdpt_pieces_render_like_whole_iterations(W, H, monkeypatch):
     assert np.allclose(got, ref, rtol=1e-4, atol=1e-6)
     assert np.allclose(one, ref1, rtol=1e-4, atol=1e-6)
     orc, ost = _oracle.Scene(path).bdpt(W, H, 3, 21, mode=1)
-    assert_film_parity(got, orc)
+    assert_film_parity(got, orc, case=f"bdpt_torus{W}x{H}_i3_s21")
     assert_ray_counts(gs, ost)
 
 
@@ -455,7 +473,7 @@ def test_bdpt_overlapped_passes_equal_the_sequential_schedule(name, maker, W, H,
     orc, ost = _oracle.Scene(path).bdpt(W, H, 3, 77, mode=1, control_length=ctl)
     # with every path length counted, a split path moves more pixels (the
     # gates of test_cbox_bdpt_film_matches_oracle); the rest keep the 2e-6 gate
-    assert_film_parity(fa, orc, max_bad_frac=0.01 if ctl else 0.06)
+    assert_film_parity(fa, orc, case=f"bdpt_{name}{W}x{H}_i3_s77_ctl{ctl}")
     assert_ray_counts(sa, ost, slack=64)
 
 
@@ -483,7 +501,7 @@ def test_bdpt_pieces_never_exceed_the_buffer_capacity(W, H, cap, pipes, monkeypa
     assert gs.closest_rays == rs.closest_rays and gs.shadow_rays == rs.shadow_rays
     assert np.allclose(got, ref, rtol=1e-4, atol=1e-6)
     orc, ost = _oracle.Scene(path).bdpt(W, H, 2, 33, mode=1)
-    assert_film_parity(got, orc)
+    assert_film_parity(got, orc, case=f"bdpt_torus{W}x{H}_i2_s33")
     assert_ray_counts(gs, ost)
 
 
@@ -511,11 +529,11 @@ def test_spheres_bdpt_and_pt_match_oracle_counter_rng():
     path = _scenes.spheres(64, 64)
     film, st = ctx(path).render_bdpt(64, 64, iterations=4, seed=5489)
     ref, rst = _oracle.Scene(path).bdpt(64, 64, 4, 5489, mode=1)
-    assert_film_parity(film, ref)
+    assert_film_parity(film, ref, case="bdpt_spheres64x64_i4_s5489")
     assert_ray_counts(st, rst)
     film, st = ctx(path).render_path(64, 64, spp=16, max_depth=7, seed=5489)
     ref, rst = _oracle.Scene(path).pt(64, 64, 16, 7, 5489, mode=1)
-    assert_film_parity(film * np.float32(1.0 / 16), ref)
+    assert_film_parity(film * np.float32(1.0 / 16), ref, case="pt_spheres64x64_spp16_s5489")
     assert_ray_counts(st, rst)
 
 
@@ -552,7 +570,7 @@ def test_bdpt_tiny_and_ragged_films_match_oracle(W, H):
     film, st = ctx(path).render_bdpt(W, H, iterations=3, seed=17)
     ref, rst = _oracle.Scene(path).bdpt(W, H, 3, 17, mode=1)
     assert_ray_counts(st, rst)
-    assert_film_parity(film, ref)
+    assert_film_parity(film, ref, case=f"bdpt_torus{W}x{H}_i3_s17")
 
 
 def test_zero_iterations_and_depth_zero():
@@ -563,7 +581,7 @@ def test_zero_iterations_and_depth_zero():
     film, st = ctx(path).render_path(16, 12, spp=4, max_depth=0, seed=2)
     ref, rst = _oracle.Scene(path).pt(16, 12, 4, 0, 2, mode=1)
     assert st.closest_rays == rst.closest_rays
-    assert_film_parity(film * np.float32(1.0 / 4), ref)
+    assert_film_parity(film * np.float32(1.0 / 4), ref, case="pt_cbox16x12_spp4_d0_s2")
 
 
 @pytest.mark.parametrize("spp", [8, 12])
@@ -574,7 +592,7 @@ def test_pt_non_square_spp_stratification_matches_oracle(spp):
     path = _scenes.cbox(40, 30)
     film, st = ctx(path).render_path(40, 30, spp=spp, max_depth=7, seed=31)
     ref, rst = _oracle.Scene(path).pt(40, 30, spp, 7, 31, mode=1)
-    assert_film_parity(film * np.float32(1.0 / spp), ref)
+    assert_film_parity(film * np.float32(1.0 / spp), ref, case=f"pt_cbox40x30_spp{spp}_s31")
     assert_ray_counts(st, rst)
 
 
@@ -587,7 +605,7 @@ def test_cbox_bdpt_film_matches_oracle():
         ref, rst = _oracle.Scene(path).bdpt(64, 48, 3, 5489, mode=1, control_length=ctl)
         # every path length counts with control_length 0, so a split path (tests/_parity.py)
         # moves more pixels: 113 of 3,072 measured; the other pixels keep the 2e-6 gate
-        assert_film_parity(film, ref, max_bad_frac=0.01 if ctl else 0.06)
+        assert_film_parity(film, ref, case=f"bdpt_cbox64x48_i3_s5489_ctl{ctl}")
         assert_ray_counts(st, rst, slack=64)
 
 
@@ -600,7 +618,7 @@ def test_bdpt_1m_scene_film_matches_oracle():
     path = big_torus(W, H)
     film, st = ctx(path).render_bdpt(W, H, iterations=1, seed=5489)
     ref, rst = _oracle.Scene(path).bdpt(W, H, 1, 5489, mode=1)
-    assert_film_parity(film, ref)
+    assert_film_parity(film, ref, case="bdpt_torus1m384x216_i1_s5489")
     assert_ray_counts(st, rst)
 
 
@@ -611,5 +629,5 @@ def test_pt_c3_film_480x270_matches_oracle():
     path = _scenes.cbox(W, H)
     film, st = ctx(path).render_path(W, H, spp=4, max_depth=7, seed=5489)
     ref, rst = _oracle.Scene(path).pt(W, H, 4, 7, 5489, mode=1)
-    assert_film_parity(film * np.float32(1.0 / 4), ref)
+    assert_film_parity(film * np.float32(1.0 / 4), ref, case="pt_cbox480x270_spp4_s5489")
     assert_ray_counts(st, rst)

@@ -147,6 +147,14 @@ def test_cli_checkpoint_resume_and_devices(mode, tmp_path):
     r = subprocess.run([os.path.join(native.PKG_DIR, "wr_tot"), *map(str, [other, tmp_path / "x.pfm", *base[2:],
                         "--checkpoint", ck])], capture_output=True, text=True, cwd=tmp_path, timeout=300)
     assert r.returncode != 0 and "another scene" in r.stderr, (r.returncode, r.stderr)
+    # a film of the same render shape without a fingerprint (pre-v7, or saved with 0) is refused too
+    film0, info0 = native.checkpoint_load(str(ck))
+    nofp = tmp_path / "nofp.bin"
+    native.checkpoint_save(str(nofp), film0, info0["kind"], info0["done"], info0["total"], info0["seed"],
+                           fingerprint=0)
+    r = subprocess.run([os.path.join(native.PKG_DIR, "wr_tot"), *map(str, [base[0], tmp_path / "y.pfm", *base[2:],
+                        "--checkpoint", nofp])], capture_output=True, text=True, cwd=tmp_path, timeout=300)
+    assert r.returncode != 0 and "no scene fingerprint" in r.stderr, (r.returncode, r.stderr)
     _tot([base[0], tmp_path / "resumed.pfm", *base[2:], "--checkpoint", ck, "--checkpoint-every", 2], tmp_path)
     assert np.allclose(_pfm(tmp_path / "resumed.pfm"), _pfm(tmp_path / "full.pfm"), rtol=1e-4, atol=1e-6)
     two = _tot([base[0], tmp_path / "two.pfm", *base[2:], "--devices", "0,0", "--trace", "reference"], tmp_path)

@@ -193,6 +193,40 @@ def test_bvh_verify_every_ray_against_the_kd_walk(name, maker, kind, monkeypatch
         _, st = c.render_bdpt(256, 256, iterations=4, seed=3)
     assert st.verify_rays == st.closest_rays + st.shadow_rays > 0
     assert st.verify_mismatches == 0, (st.verify_mismatches, st.verify_rays)
+    # the tree each render searched: the 1M scene has only the 4-wide tree; the
+    # torus render's 4 pieces make two groups on its one pipeline (not the
+    # latency path), so it searches the binary tree, as VCM and PT do
+    assert st.bvh_width == {"torus": 2, "torus_vcm": 2, "cbox": 2, "torus1m": 4}[name], (name, st.bvh_width)
+
+
+@pytest.mark.parametrize("lat", ["latency", "full"])
+def test_bvh_tree_of_each_schedule_verified(lat, monkeypatch):
+    """Pins the two trees a binary-tree scene's BDPT renders search, each with
+    every ray verified against the KD walk (WR_BVH_VERIFY):
+      * latency: a short render (two iterations = two pieces = one group on
+        one pipeline) searches the 4-wide tree (wide_now) -- the path of the
+        round-4 fault, where the searched scene was copied before its KD stack
+        depth was set;
+      * full: pieces that fill 16 pipelines with several groups each, and
+        WR_BVH_WIDE_LAT=0, search the binary tree -- the headline's tree."""
+    monkeypatch.setenv("WR_BVH_VERIFY", "1")
+    W = H = 256
+    if lat == "full":
+        monkeypatch.setenv("WR_BVH_WIDE_LAT", "0")
+        monkeypatch.setenv("WR_PIECE_MIN", "4096")
+        monkeypatch.setenv("WR_PIECE_CAP", "4096")
+    s = native.Scene(_scenes.torus(W, H))
+    c = native.Context(s, 0, trace=native.TRACE_BVH)
+    if lat == "full":
+        c.set_pipelines(16)
+    _, st = c.render_bdpt(W, H, iterations=4 if lat == "full" else 2, seed=31)
+    c.close()
+    assert st.verify_rays == st.closest_rays + st.shadow_rays > 0
+    assert st.verify_mismatches == 0, (st.verify_mismatches, st.verify_rays)
+    if lat == "full":
+        assert st.pipelines == 16 and st.bvh_width == 2, (st.pipelines, st.bvh_width)
+    else:
+        assert st.pipelines == 1 and st.bvh_width == 4, (st.pipelines, st.bvh_width)
 
 
 @pytest.mark.parametrize("name,maker,n", [("torus", lambda: _scenes.torus(256, 256), 200_000),
@@ -261,7 +295,7 @@ def test_deferred_hard_rays_render_the_same_film(name, maker, W, H, its, monkeyp
     assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
     assert _film_close(fa, fb)
     ref, rst = _oracle.Scene(path).bdpt(W, H, its, 5489, mode=1)
-    assert_film_parity(fa, ref, max_bad_frac=0.01)
+    assert_film_parity(fa, ref, case=f"bdpt_{name}{W}x{H}_i{its}_s5489_defer")
     assert_ray_counts(sa, rst, slack=64)
     # and every deferred answer is the KD walk's, bit for bit
     monkeypatch.setenv("WR_DEFER", "1")

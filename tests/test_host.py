@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     assert declared == set(native.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.wr_api_version() == 7
+    assert L.wr_api_version() == 8
 
 
 @pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),

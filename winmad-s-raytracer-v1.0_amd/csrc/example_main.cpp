@@ -1,10 +1,11 @@
 // The reference's main() (src/main.cpp:29-97) with INTEGRATION.md section 1's
 // change applied and nothing else: the -p / -bpt / -vcm branches construct the
 // winmad:: mirror classes (csrc/integrators.h) instead of the CPU integrators.
-// No environment set-up, no trace-mode or pipeline calls: it runs at the
-// library's defaults (loading libwinmad_rt.so raises GPU_MAX_HW_QUEUES to 16
-// before the first HIP call; the verified-BVH traversal is the default for
-// triangle scenes; init() reserves the work buffers).
+// No trace-mode or pipeline calls: it runs at the library's defaults (the
+// verified-BVH traversal is the default for triangle scenes; init() reserves
+// the work buffers).  Its first statement asks HIP for 16 hardware queues, one
+// per render pipeline (wr_request_hw_queues: before the first HIP call; the
+// library itself never changes the environment).
 //
 //     example_main <scene> <out.ppm> -bpt|-vcm|-p [iterations]
 //
@@ -24,6 +25,7 @@
 winmad::Parameters para;
 
 int main(int argc, char* argv[]) {
+  wr_request_hw_queues(16);  // added: 16 render pipelines, each on its own hardware queue
   if (argc < 4) {
     std::printf("usage: %s <scene> <out.ppm> -bpt|-vcm|-p [iterations]\n", argv[0]);
     return 2;

@@ -84,6 +84,12 @@ void SurfaceIntegrator::batched(int kind, int total, uint32_t seed, const std::v
       if (have.width != width || have.height != height || have.kind != kind || have.total != total ||
           have.seed != seed)
         throw std::runtime_error("checkpoint " + checkpointPath + " belongs to another render");
+      // a film without a fingerprint (written before API v7, or saved with 0)
+      // cannot be matched to a scene: refused like a foreign one
+      if (have.fingerprint[0] == 0 && have.fingerprint[1] == 0)
+        throw std::runtime_error("checkpoint " + checkpointPath +
+                                 " carries no scene fingerprint (written before API v7 or without one); "
+                                 "delete it to render from the start");
       if (have.fingerprint[0] != want.fingerprint[0] || have.fingerprint[1] != want.fingerprint[1])
         throw std::runtime_error("checkpoint " + checkpointPath +
                                  " was rendered from another scene or with other integrator settings");

@@ -74,9 +74,9 @@ int main(int argc, char** argv) {
     return 2;
   }
   // before any HIP call: one hardware queue per render pipeline
-  {
-    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-    if (!q || std::atoi(q) < hw_queues) setenv("GPU_MAX_HW_QUEUES", std::to_string(hw_queues).c_str(), 1);
+  if (wr_request_hw_queues(hw_queues) < 0) {
+    std::fprintf(stderr, "%s\n", wr_last_error());
+    return 2;
   }
   if (gpus > 0 && devices.empty())
     for (int k = 0; k < gpus; ++k) devices.push_back(k);

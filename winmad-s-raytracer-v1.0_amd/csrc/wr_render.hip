@@ -39,28 +39,20 @@ using namespace wrd;
 
 // =============================================================== errors
 static int fail(int code, const std::string& msg) { return wr::set_error(code, msg); }
-// Load-time set-up: one hardware queue per render pipeline.  HIP gives a
-// process GPU_MAX_HW_QUEUES queues (default 4; the GPU box exports 4), and
-// pipelines beyond them share a queue and serialize (concurrent
-// pipelines).  When the library is loaded before the process's first HIP call
-// -- a C++ program linked to it, like the reference's main.cpp with the
-// SurfaceIntegrator mirror -- this raises the variable to 16
-// so that the library default is the measured configuration.  A plain setenv
-// before HIP initialises (never a re-exec).  WR_HW_QUEUES=n sets exactly n
-// instead (e.g. 4 keeps HIP's default); a larger GPU_MAX_HW_QUEUES is kept.
-// When HIP is already initialised (a Python process that touched the GPU
-// first) the variable no longer matters to HIP, and wr_create sizes the
-// pipelines by what HIP saw: see hwq_at_load below.
-static int g_hwq_at_load = 0;  // GPU_MAX_HW_QUEUES as the library found it (0 = unset)
-__attribute__((constructor)) static void wr_raise_hw_queues() {
-  const char* cur = std::getenv("GPU_MAX_HW_QUEUES");
-  g_hwq_at_load = cur ? std::atoi(cur) : 0;
-  if (const char* w = std::getenv("WR_HW_QUEUES")) {
-    const int n = std::atoi(w);
-    if (n > 0) setenv("GPU_MAX_HW_QUEUES", std::to_string(std::min(n, 32)).c_str(), 1);
-    return;
-  }
-  if (!cur || std::atoi(cur) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+// Hardware queues: one per render pipeline.  HIP gives a process
+// GPU_MAX_HW_QUEUES queues (default 4; the GPU box exports 4), read once when
+// HIP initialises, and pipelines beyond them share a queue and serialize
+// (concurrent pipelines).  The library never writes the process
+// environment by itself: a host that wants the measured configuration (16
+// pipelines) asks for it with wr_request_hw_queues() before its first HIP call
+// (example_main / tot_main do; bench.py and winmad_rt/native.py set the
+// variable before HIP starts).  wr_create sizes the pipelines by the variable
+// as it reads then, i.e. by what HIP saw, unless the caller changed it after
+// HIP started.
+static int hw_queues_in_effect() {
+  const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+  const int n = q ? std::atoi(q) : 0;
+  return n > 0 ? n : 4;  // HIP's default
 }
 
 // Every C-ABI entry that selects a device (hipSetDevice) leaves the caller's
@@ -1396,6 +1388,13 @@ extern "C" {
 const char* wr_last_error(void) { return wr::last_error(); }
 int wr_api_version(void) { return WR_API_VERSION; }
 
+int wr_request_hw_queues(int n) {
+  if (n < 1 || n > 32) return fail(WR_E_ARG, "hardware queues: 1..32");
+  if (hw_queues_in_effect() < n && setenv("GPU_MAX_HW_QUEUES", std::to_string(n).c_str(), 1) != 0)
+    return fail(WR_E_ARG, "setenv GPU_MAX_HW_QUEUES failed");
+  return hw_queues_in_effect();
+}
+
 int wr_scene_load(const char* path, wr_scene** out) {
   if (!path || !out) return fail(WR_E_ARG, "null argument");
   *out = nullptr;
@@ -1514,11 +1513,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   // one pipeline per hardware queue of this process (HIP's GPU_MAX_HW_QUEUES,
   // default 4; pipeline 0 shares the context stream), at most 16: streams that
   // share a hardware queue serialize behind each other
-  {
-    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-    const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
-    c->npipes = std::max(1, std::min(kMaxPipes, hwq));
-  }
+  c->npipes = std::max(1, std::min(kMaxPipes, hw_queues_in_effect()));
   if (const char* e = std::getenv("WR_PIPES")) c->npipes = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   if (const char* e = std::getenv("WR_PIECE_CAP")) c->piece_cap = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("WR_PIECE_MIN")) c->piece_min = std::max(1, std::atoi(e));
@@ -1845,8 +1840,15 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       if (const char* e = std::getenv("WR_BVH_WIDE_LAT")) c->lat_wide = std::atoi(e) != 0;
       fs.depth = std::max(fh.depth + 1, d.max_stack + 1);
       // kd_walk_wave: node index and depth share a word, the leaf key and the
-      // position in the leaf 64 bits
-      fs.walk_wave = s.nodes.size() < (size_t(1) << 26) && s.dep_max <= 43 ? 1 : 0;
+      // position in the leaf 64 bits (the key's lowest bit is 64 - dep_max, so
+      // every leaf must hold fewer than 2^(64 - dep_max) references)
+      size_t kd_max_leaf = 0;
+      for (const auto& k : s.nodes)
+        if (k.axis < 0) kd_max_leaf = std::max(kd_max_leaf, static_cast<size_t>(k.count));
+      fs.walk_wave = s.nodes.size() < (size_t(1) << 26) && s.dep_max <= 43 &&
+                             kd_max_leaf < (size_t(1) << (64 - std::max(s.dep_max, 0)))
+                         ? 1
+                         : 0;
       if (const char* e = std::getenv("WR_WALK_WAVE")) fs.walk_wave = fs.walk_wave && std::atoi(e) != 0;
       c->fast_ok = true;
       int per_cu = 0;

@@ -25,7 +25,7 @@ EXPORTS = ["wr_scene_load", "wr_scene_from_desc", "wr_scene_info_get", "wr_scene
            "wr_comm_init", "wr_film_reduce", "wr_set_pipelines", "wr_set_trace_mode", "wr_trace_closest", "wr_occluded",
            "wr_render_bdpt", "wr_render_path", "wr_render_vcm", "wr_path_radiance", "wr_film_write_ppm",
            "wr_film_write_image", "wr_checkpoint_save", "wr_checkpoint_load", "wr_last_error", "wr_api_version",
-           "wr_reserve"]
+           "wr_reserve", "wr_request_hw_queues"]
 CKPT_BDPT, CKPT_VCM, CKPT_PT = 1, 2, 3
 
 
@@ -118,19 +118,30 @@ def _share_torch_runtime():
         pass
 
 
-def _keep_hw_queues_if_hip_is_up():
-    """The library raises GPU_MAX_HW_QUEUES to 16 when it loads (one hardware
-    queue per render pipeline), which only takes effect if HIP has not been
-    initialised yet.  When torch already initialised it, HIP keeps the queues it
-    read then: pin the library to that value (WR_HW_QUEUES) so that it does not
-    start more pipelines than there are queues (they would serialize)."""
+def _hip_is_up():
     torch = sys.modules.get("torch")
     try:
-        up = torch is not None and torch.cuda.is_initialized()
+        return torch is not None and torch.cuda.is_initialized()
     except Exception:
-        up = False
-    if up and "WR_HW_QUEUES" not in os.environ:
-        os.environ["WR_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES") or "4"
+        return False
+
+
+def _request_hw_queues(L):
+    """One hardware queue per render pipeline (concurrent
+    pipelines): HIP reads GPU_MAX_HW_QUEUES once, when it initialises, and the
+    library sizes its pipelines by it.  If HIP is not up yet, ask for 16
+    (env WR_HW_QUEUES=n asks for n; a larger GPU_MAX_HW_QUEUES is kept) through
+    wr_request_hw_queues -- the library never changes the environment by
+    itself.  If torch already initialised HIP, the variable stays as HIP read
+    it, so the library starts no more pipelines than there are queues."""
+    if _hip_is_up():
+        return
+    want = 16
+    try:
+        want = max(1, min(32, int(os.environ.get("WR_HW_QUEUES", "16"))))
+    except ValueError:
+        pass
+    L.wr_request_hw_queues(want)
 
 
 def lib():
@@ -141,8 +152,9 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C {PKG_DIR}` "
                                "(or __graft_entry__.build()); there is no CPU fallback")
-        _keep_hw_queues_if_hip_is_up()
         L = C.CDLL(LIB_PATH)
+        L.wr_request_hw_queues.argtypes = [C.c_int]
+        _request_hw_queues(L)
         P, I, I64 = C.c_void_p, C.c_int, C.c_int64
         L.wr_scene_load.argtypes = [C.c_char_p, C.POINTER(P)]
         L.wr_scene_from_desc.argtypes = [C.POINTER(WrSceneDesc), C.POINTER(P)]
