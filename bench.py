@@ -47,7 +47,7 @@ L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2, 8 XCDs x 4 MiB, ~34.5 TB/s agg
 # (profiles/<round>/traffic_<config>.json; C2's older rounds: traffic.json);
 # the newest round's file wins and its name is in the line (traffic_source).
 PROFILES = os.path.join(REPO, "profiles")
-ROUNDS = ("r4", "r3", "r2", "r1")
+ROUNDS = ("r5", "r4", "r3", "r2", "r1")
 
 
 def pmc_traffic(config):
@@ -224,8 +224,7 @@ def main():
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting replay")
     ap.add_argument("--trace", choices=["auto", "reference", "bvh"], default="auto",
                     help="traversal: the reference's KD walk, or the verified BVH search (same (t, primitive) "
-                         "answers, DESIGN.md section 4b); auto = the faster one: bvh for every config (scenes with "
-                         "spheres, which the BVH mode does not cover, use the KD walk)")
+                         "answers, DESIGN.md section 4b); auto = the faster one: bvh for every config")
     ap.add_argument("--no-compare", action="store_true",
                     help="skip the single-GPU comparison run in the other traversal mode")
     ap.add_argument("--no-cut", action="store_true",
@@ -355,17 +354,34 @@ def main():
         # actually limits the kernel (PMC) is the latency
         # of dependent L2 round trips plus VALU issue, not any bandwidth.
         hbm = None
+        lib_sha = native.library_sha16()
         if traffic and wall_s > 0:
             hbm_gbs = traffic * trace_launches / wall_s / 1e9
             hbm = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "source": "PMC FETCH_SIZE x2 + WRITE_SIZE per launch "
                    "x launches / trace_wall_ms", "l2_hit_rate": tr_rec.get("l2_hit_rate"),
-                   "pmc_build": tr_rec.get("head")}
+                   "pmc_build": tr_rec.get("head"), "pmc_lib_sha": tr_rec.get("lib_sha"),
+                   "pmc_lib_is_this_run": tr_rec.get("lib_sha") == lib_sha}
+        state_hbm = None
+        if tr_rec and tr_rec.get("state_bytes_per_launch") and traffic:
+            # the path-state kernels (gen, vertex, resolve) beside the traversal:
+            # the whole step's HBM bytes over the whole timed wall
+            sb = tr_rec["state_bytes_per_launch"] * trace_launches
+            tb = traffic * trace_launches
+            state_hbm = {"bytes_per_trace_step": round(tr_rec["state_bytes_per_launch"]),
+                         "achieved": round(sb / elapsed / 1e9, 1), "unit": "GB/s",
+                         "whole_step_achieved": round((sb + tb) / elapsed / 1e9, 1), "peak": HBM_PEAK_GBS,
+                         "whole_step_frac": round((sb + tb) / elapsed / 1e9 / HBM_PEAK_GBS, 4),
+                         "source": "PMC FETCH_SIZE x2 + WRITE_SIZE of every non-traversal kernel, per traversal step "
+                                   "x launches / elapsed (traversal: roofline.traffic)",
+                         "top": sorted(((k, round(v["bytes_per_step"])) for k, v in tr_rec["state_kernels"].items()),
+                                       key=lambda kv: -kv[1])[:4]}
         roofline = {"bound": "l2", "achieved": round(achieved, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / L2_PEAK_GBS, 4),
                     "limiter": "latency of dependent L2 round trips + VALU issue (PMC, DESIGN.md section 4)",
                     "algorithmic_bytes": "SURVEY.md 8(d) B_ray, counted by a replay of the timed iterations",
                     "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src, "hbm": hbm,
+                    "state_hbm": state_hbm,
                     "kernel": "k_trace (KD closest-hit traversal)",
                     "bytes_per_launch": round(per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                     "trace_wall_ms": round(st.trace_wall_ms, 3),
@@ -401,7 +417,7 @@ def main():
             orays = ost.closest_rays + ost.shadow_rays
             other = {"trace": o_mode, "value": round(orays / odt / 1e6, 2), "ms_per_step": round(odt / K * 1e3, 3),
                      "same_ray_count": bool(orays == rays)}
-        except native.WrError as e:  # e.g. the BVH mode on a scene with spheres
+        except native.WrError as e:  # e.g. a scene without a verified BVH
             other = {"trace": o_mode, "error": str(e)}
 
     cpu = port = None

@@ -148,6 +148,15 @@ typedef struct {
   int64_t bvh_width;         /* WR_TRACE_BVH: the search tree's width, 2 or 4 (4
                                 from 2^18 triangles); 0: KD walk
                                 (API v7)                                         */
+  int64_t work_bytes;        /* render calls: device bytes of the work buffers the
+                                pipelines of this call hold (API v8)              */
+  int64_t work_paths;        /* ... and the paths they hold at once (buffer sets x
+                                paths per set), so work_bytes / work_paths is the
+                                memory per path in flight (API v8)               */
+  int64_t redone;            /* BDPT: renders redone with smaller pieces because
+                                a vertex pool or shadow queue sized by use filled
+                                up (the film is the one of an unbounded render;
+                                DESIGN.md 3; API v8)                              */
 } wr_stats;
 
 /* The reference's in-memory Scene (scene/scene.h:35-42) as flat host arrays,
@@ -246,13 +255,14 @@ int wr_reserve(wr_context* ctx, int integrator, int32_t width, int32_t height);
 /* Traversal mode of every later call on the context.
  *   WR_TRACE_REFERENCE: the reference's KD tree, walked exactly as
  *     KDtreeAccel::traverse (scene/KDtreeAccel.cpp:309-388) walks it.
- *   WR_TRACE_BVH (default for scenes of triangles only): a BVH search for the
- *     smallest hit, accepted only when the winner is provably the reference's
- *     (unique within EPS, in a KD leaf the reference's traversal reaches, the
- *     ray not grazing the winner's plane); every other ray is traced in the
- *     reference mode.  Same rays, same (t, primitive) answers; see DESIGN.md 4b.
- * Scenes with spheres always use WR_TRACE_REFERENCE (WR_E_SCENE if asked for
- * the BVH).  Env WR_TRACE_BVH=0 / 1 sets the mode at wr_create. */
+ *   WR_TRACE_BVH (default): a BVH search over the triangles and spheres for
+ *     the smallest hit, accepted only when the winner is provably the
+ *     reference's (unique within EPS, in a KD leaf the reference's traversal
+ *     reaches, the ray not grazing a tested triangle's plane, its origin inside
+ *     the region the sphere boxes are grown for); every other ray is traced in
+ *     the reference mode.  Same rays, same (t, primitive) answers; see
+ *     DESIGN.md 4b.  (Spheres: API v8.)
+ * Env WR_TRACE_BVH=0 / 1 sets the mode at wr_create. */
 enum { WR_TRACE_REFERENCE = 0, WR_TRACE_BVH = 1 };
 int wr_set_trace_mode(wr_context* ctx, int mode);
 

@@ -16,6 +16,8 @@ PMC_ARGS=$(echo " $ARGS " | grep -oE -- "--(config|trace|steps) [a-z0-9]+" | tr 
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
+# the library these counters describe (bench.py compares it with the one it loads)
+sha256sum winmad-s-raytracer-v1.0_amd/libwinmad_rt.so | cut -c1-16 > $OUT/lib.sha
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace pass failed rc=$?"; tail -5 $OUT/trace.log; exit 1; }
 echo "trace pass ok"
 i=0

@@ -13,7 +13,11 @@ Writes
                     "HBM [CDNA4]": FETCH_SIZE / WRITE_SIZE are in KiB, and on
                     gfx950 FETCH_SIZE counts half the bytes of a read, so
                     traffic = 2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE.
-                    bench.py reports it as roofline.traffic.
+                    bench.py reports it as roofline.traffic.  Beside it the
+                    path-state kernels' bytes (gen, vertex and resolve kernels:
+                    everything but the traversal) per traversal step, and per
+                    kernel -- bench.py's roofline.state_hbm -- and the sha256
+                    prefix of the library the passes ran (lib.sha).
 """
 import csv
 import glob
@@ -82,6 +86,20 @@ def main():
                     "hbm_bytes_per_launch": (2 * 1024 * fetch + 1024 * write)
                     if fetch is not None and write is not None else None,
                     "l2_hit_rate": hit / (hit + miss) if hit is not None and miss else None})
+        # every other kernel of the render (path state: gen, vertex / resolve
+        # kernels, film clears) per traversal step, by kernel
+        state = {}
+        for k, cs in per.items():
+            if k in tr or "true" in k.split("<", 1)[-1].split(",", 1)[0]:  # (the counting build: warm-up only)
+                continue
+            f, w = cs.get("FETCH_SIZE"), cs.get("WRITE_SIZE")
+            if f and w and steps:
+                state[k] = {"dispatches": len(f), "bytes_per_step": (2 * 1024 * sum(f) + 1024 * sum(w)) / steps}
+        if state:
+            out["state_kernels"] = state
+            out["state_bytes_per_launch"] = sum(v["bytes_per_step"] for v in state.values())
+    sha = os.path.join(src, "lib.sha")
+    out["lib_sha"] = open(sha).read().strip() if os.path.exists(sha) else None
     with open(os.path.join(dst, f"traffic_{config}.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))

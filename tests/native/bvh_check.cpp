@@ -36,13 +36,21 @@ int main(int argc, char** argv) {
   for (const auto& r : f.tris) {
     int p;
     std::memcpy(&p, &r.c[1], 4);
+    const bool sph = p < 0;  // a sphere's record: -(prim + 1)
+    if (sph) p = -p - 1;
     if (p < 0 || static_cast<size_t>(p) >= np) return fail("bad prim id in a record");
     ++seen[static_cast<size_t>(p)];
     const wr::Prim& q = s.prims[static_cast<size_t>(p)];
-    const float want[10] = {q.p0.x, q.p0.y, q.p0.z, q.p0.x - q.p1.x, q.p0.y - q.p1.y, q.p0.z - q.p1.z,
-                            q.p0.x - q.p2.x, q.p0.y - q.p2.y, q.p0.z - q.p2.z};
-    const float got[9] = {r.a[0], r.a[1], r.a[2], r.a[3], r.b[0], r.b[1], r.b[2], r.b[3], r.c[0]};
-    if (std::memcmp(want, got, sizeof got) != 0) return fail("record differs from the triangle");
+    if (sph != (q.type != wr::kTri)) return fail("record type differs from the primitive's");
+    if (sph) {
+      const float want[4] = {q.c.x, q.c.y, q.c.z, q.r};
+      if (std::memcmp(want, r.a, sizeof want) != 0) return fail("record differs from the sphere");
+    } else {
+      const float want[10] = {q.p0.x, q.p0.y, q.p0.z, q.p0.x - q.p1.x, q.p0.y - q.p1.y, q.p0.z - q.p1.z,
+                              q.p0.x - q.p2.x, q.p0.y - q.p2.y, q.p0.z - q.p2.z};
+      const float got[9] = {r.a[0], r.a[1], r.a[2], r.a[3], r.b[0], r.b[1], r.b[2], r.b[3], r.c[0]};
+      if (std::memcmp(want, got, sizeof got) != 0) return fail("record differs from the triangle");
+    }
     int lb, ln;
     std::memcpy(&lb, &r.c[2], 4);
     std::memcpy(&ln, &r.c[3], 4);
@@ -85,6 +93,14 @@ int main(int argc, char** argv) {
       for (int j = 0; j < cnt; ++j) {
         int p;
         std::memcpy(&p, &f.tris[static_cast<size_t>(first + j)].c[1], 4);
+        if (p < 0) {  // a sphere: its reference box and centre +- r inside the leaf box
+          const wr::Prim& q = s.prims[static_cast<size_t>(-p - 1)];
+          const float c[3] = {q.c.x, q.c.y, q.c.z}, bl[3] = {q.bl.x, q.bl.y, q.bl.z}, br[3] = {q.br.x, q.br.y, q.br.z};
+          for (int a = 0; a < 3; ++a)
+            if (bl[a] < it.lo[a] || br[a] > it.hi[a] || c[a] - q.r < it.lo[a] || c[a] + q.r > it.hi[a])
+              return fail("sphere outside its leaf box");
+          continue;
+        }
         const wr::Prim& q = s.prims[static_cast<size_t>(p)];
         const float v[3][3] = {{q.p0.x, q.p0.y, q.p0.z}, {q.p1.x, q.p1.y, q.p1.z}, {q.p2.x, q.p2.y, q.p2.z}};
         for (auto& w : v)

@@ -1,5 +1,6 @@
 """CPU checks of the verified-BVH data built on the host (wr_bvh.cpp): every
-triangle in exactly one BVH leaf with its Triangle::hit record, boxes nested and
+triangle / sphere in exactly one BVH leaf with its Triangle::hit record (a
+sphere: centre and radius, its box inside the leaf's), boxes nested and
 holding their triangles, and the KD membership data (each primitive's leaves,
 its position in them, the root paths) equal to the reference tree's
 (tests/native/bvh_check.cpp, compiled here from the product's own sources)."""
@@ -39,8 +40,9 @@ def small_torus():
     return _scenes.path("torus_small.scene", scenes.torus_scene(64, 64, "bdpt", torus_obj=p))
 
 
-@pytest.mark.parametrize("maker", [lambda: _scenes.torus(64, 64), lambda: _scenes.cbox(64, 48), small_torus],
-                         ids=["torus", "cbox_dragon", "synthetic_torus_40k"])
+@pytest.mark.parametrize("maker", [lambda: _scenes.torus(64, 64), lambda: _scenes.cbox(64, 48), small_torus,
+                                   lambda: _scenes.spheres(64, 64)],
+                         ids=["torus", "cbox_dragon", "synthetic_torus_40k", "spheres"])
 def test_bvh_structure(maker):
     r = subprocess.run([checker(), maker()], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
@@ -73,8 +75,9 @@ def test_bvh_wide_tree_structure():
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("maker", [lambda: _scenes.torus(64, 64), lambda: _scenes.cbox(64, 48), small_torus],
-                         ids=["torus", "cbox_dragon", "synthetic_torus_40k"])
+@pytest.mark.parametrize("maker", [lambda: _scenes.torus(64, 64), lambda: _scenes.cbox(64, 48), small_torus,
+                                   lambda: _scenes.spheres(64, 64)],
+                         ids=["torus", "cbox_dragon", "synthetic_torus_40k", "spheres"])
 def test_bvh_8wide_quantised_tree_structure(maker):
     """The 8-wide search tree (WR_BVH_WIDE=8): the binary tree's leaves, each
     once, every byte-quantised child box decoded with the device's formula

@@ -45,20 +45,32 @@ def big_torus(W, H):
     return _scenes.path(f"torus1m_{W}x{H}.scene", scenes.torus_scene(W, H, "bdpt", torus_obj=p))
 
 
-SCENES = [("torus", lambda: _scenes.torus(256, 256)), ("cbox", lambda: _scenes.cbox(256, 192))]
+SCENES = [("torus", lambda: _scenes.torus(256, 256)), ("cbox", lambda: _scenes.cbox(256, 192)),
+          ("spheres", lambda: _scenes.spheres(256, 256))]
 
 
 @pytest.mark.parametrize("name,maker", [("torus64", lambda: _scenes.torus(64, 64)),
-                                        ("cbox64x48", lambda: _scenes.cbox(64, 48))])
+                                        ("cbox64x48", lambda: _scenes.cbox(64, 48)),
+                                        ("spheres64", lambda: _scenes.spheres(64, 64))])
 def test_bvh_golden_corpus_bit_exact(name, maker):
     _check_golden_corpus(pair(maker())[1], name)
 
 
-def test_bvh_mode_refused_with_spheres():
+def test_bvh_is_the_default_for_sphere_scenes():
+    """Spheres are in the verified BVH (round 5): a scene with spheres gets the
+    BVH search by default -- the binary tree (PT), and the 4-wide one for a
+    BDPT render short enough to take the latency path (one group) -- with the
+    same film and rays as the KD walk's."""
     c = native.Context(native.Scene(_scenes.spheres(64, 64)), 0)
-    with pytest.raises(native.WrError) as e:
-        c.set_trace_mode(native.TRACE_BVH)
-    assert e.value.code == native.WR_E_SCENE
+    fb, sb = c.render_bdpt(64, 64, iterations=2, seed=3)
+    fp, sp = c.render_path(64, 64, spp=4, seed=3)
+    assert sb.bvh_width == 4 and sp.bvh_width == 2, (sb.bvh_width, sp.bvh_width)
+    c.set_trace_mode(native.TRACE_REFERENCE)
+    fb0, sb0 = c.render_bdpt(64, 64, iterations=2, seed=3)
+    fp0, sp0 = c.render_path(64, 64, spp=4, seed=3)
+    assert sb0.bvh_width == 0
+    assert (sb.closest_rays, sb.shadow_rays, sp.closest_rays) == (sb0.closest_rays, sb0.shadow_rays, sp0.closest_rays)
+    assert _film_close(fb, fb0) and _film_close(fp, fp0)
 
 
 def _unit(v):
@@ -174,7 +186,10 @@ def test_bvh_bdpt_render_1m_triangles():
 @pytest.mark.parametrize("name,maker,kind", [("torus", lambda: _scenes.torus(256, 256), "bdpt"),
                                              ("torus_vcm", lambda: _scenes.torus(256, 256), "vcm"),
                                              ("cbox", lambda: _scenes.cbox(256, 192), "pt"),
-                                             ("torus1m", lambda: big_torus(128, 72), "bdpt")])
+                                             ("torus1m", lambda: big_torus(128, 72), "bdpt"),
+                                             ("spheres", lambda: _scenes.spheres(256, 256), "bdpt"),
+                                             ("spheres_pt", lambda: _scenes.spheres(256, 192, "pt"), "pt"),
+                                             ("spheres_vcm", lambda: _scenes.spheres(256, 256), "vcm")])
 def test_bvh_verify_every_ray_against_the_kd_walk(name, maker, kind, monkeypatch):
     """WR_BVH_VERIFY: every ray of a render is traced again by the reference's
     KD walk inside the library and the (t, primitive) pairs are compared bit for
@@ -196,7 +211,8 @@ def test_bvh_verify_every_ray_against_the_kd_walk(name, maker, kind, monkeypatch
     # the tree each render searched: the 1M scene has only the 4-wide tree; the
     # torus render's 4 pieces make two groups on its one pipeline (not the
     # latency path), so it searches the binary tree, as VCM and PT do
-    assert st.bvh_width == {"torus": 2, "torus_vcm": 2, "cbox": 2, "torus1m": 4}[name], (name, st.bvh_width)
+    assert st.bvh_width == {"torus": 2, "torus_vcm": 2, "cbox": 2, "torus1m": 4, "spheres": 2, "spheres_pt": 2,
+                            "spheres_vcm": 2}[name], (name, st.bvh_width)
 
 
 @pytest.mark.parametrize("lat", ["latency", "full"])
@@ -368,3 +384,69 @@ def test_bvh_matches_reference_mode_on_plane_grazing_rays(name, maker):
     ok = _same_hits(a, b)
     print(name, rays.shape[0], "rays,", int((a["prim"] >= 0).sum()), "hits,", int((~ok).sum()), "mismatches")
     assert ok.all(), (name, int((~ok).sum()), rays.shape[0], np.nonzero(~ok)[0][:8])
+
+
+def _sphere_rim_rays(rng, n, centres, radii, lo, hi):
+    """Rays passing a sphere at its rim: closest approach r (1 + s), s from
+    -1e-2 to 1e-2 on a log scale down to 1e-8 (both signs), from origins
+    anywhere in the scene box -- where Sphere::hit's t_hc is at its rounding
+    noise (wr_bvh.cpp, sphere_grow)."""
+    k = rng.integers(0, len(radii), n)
+    c, r = centres[k], radii[k]
+    o = rng.uniform(lo, hi, (n, 3))
+    to_c = c - o
+    dist = np.linalg.norm(to_c, axis=1)
+    u = to_c / dist[:, None]
+    w = np.cross(u, rng.normal(size=(n, 3)))
+    w /= np.linalg.norm(w, axis=1, keepdims=True)
+    s = 10.0 ** rng.uniform(-8, -2, n) * np.where(rng.random(n) < 0.5, 1.0, -1.0)
+    b = np.clip(r * (1 + s) / np.maximum(dist, 1e-9), -1.0, 1.0)  # sin of the angle off the centre
+    d = u * np.sqrt(1 - b * b)[:, None] + w * b[:, None]
+    ok = dist > r * 1.05
+    return native.rays_from_arrays(o[ok].astype(np.float32), _unit(d[ok]))
+
+
+def test_bvh_matches_reference_mode_on_sphere_rim_rays():
+    """Spheres in the verified BVH: rays grazing a sphere's rim, where the
+    reference's t_hc is decided by rounding, from origins inside the scene (the
+    search's sphere boxes cover them) and far outside it (taken to the KD walk):
+    the BVH mode's (t, primitive) equals the reference KD walk's bit for bit,
+    and so do the occlusion answers."""
+    ref, fast = pair(_scenes.spheres(256, 256))
+    rng = np.random.default_rng(17)
+    centres = np.array([[-0.5, 0.3, -0.82], [0.55, 0.6, -0.86], [0.05, -0.45, -1.0]])
+    radii = np.array([0.45, 0.42, 0.28])
+    near = _sphere_rim_rays(rng, 400_000, centres, radii, np.array([-1.0, -1.0, -1.3]), np.array([1.0, 1.0, 1.0]))
+    far = _sphere_rim_rays(rng, 100_000, centres, radii, np.array([-60.0, -60.0, -60.0]), np.array([60.0, 60.0, 60.0]))
+    for name, rays in (("near", near), ("far", far)):
+        a = ref.trace_closest(rays)
+        b = fast.trace_closest(rays)
+        ok = _same_hits(a, b)
+        pd = a["p"].astype(np.float64)
+        on = np.abs(np.linalg.norm(pd[:, None, :] - centres[None], axis=2) - radii[None]).min(axis=1) < 1e-3
+        sph = (a["prim"] >= 0) & on
+        print(name, rays.shape[0], "rays,", int(sph.sum()), "sphere hits,", int((~ok).sum()), "mismatches")
+        assert ok.all(), (name, int((~ok).sum()), rays.shape[0], np.nonzero(~ok)[0][:8])
+        # (half of the rim rays pass outside; most far ones meet the box's walls first)
+        assert sph.sum() > (0.1 if name == "near" else 0.01) * rays.shape[0], (name, int(sph.sum()))
+    o = near[:200_000, 0:3]
+    q = o + near[:200_000, 3:6] * 2.0
+    assert np.array_equal(ref.occluded(near[:200_000], q), fast.occluded(near[:200_000], q))
+
+
+def test_bvh_sphere_films_match_the_oracle():
+    """Spheres scene in the BVH mode (the library default) against the oracle:
+    BDPT and PT films under the same gates as the KD walk's, same ray counts."""
+    import _oracle
+    from _parity import assert_film_parity, assert_ray_counts
+    path = _scenes.spheres(64, 64)
+    c = native.Context(native.Scene(path), 0, trace=native.TRACE_BVH)
+    film, st = c.render_bdpt(64, 64, iterations=4, seed=5489)
+    ref, rst = _oracle.Scene(path).bdpt(64, 64, 4, 5489, mode=1)
+    assert_film_parity(film, ref, case="bdpt_spheres64x64_i4_s5489")
+    assert_ray_counts(st, rst)
+    assert st.bvh_width == 2
+    film, st = c.render_path(64, 64, spp=16, max_depth=7, seed=5489)
+    ref, rst = _oracle.Scene(path).pt(64, 64, 16, 7, 5489, mode=1)
+    assert_film_parity(film * np.float32(1.0 / 16), ref, case="pt_spheres64x64_spp16_s5489")
+    assert_ray_counts(st, rst)

@@ -1,0 +1,84 @@
+"""BDPT work buffers sized by use (verdict r4, What's missing 1).
+
+The reference stores light vertices with push_back and connects only what
+exists (bidirPathTracing.cpp:101-102, :220-257).  The overlapped BDPT
+schedule's light / camera vertex stores are pools and its shadow / aux queues
+hold 2 rays per path (the worst case is 11 per path and step, 9 light and 4
+camera vertices per path).  A render that fills one drops the appends past
+it, counts them, and is redone from the film as it was with pieces whose worst
+case fits (wr_render.hip, render_bdpt_one).  These tests force tiny pools
+(WR_BDPT_POOL_SCALE) and check the redone render against the unbounded layout
+(WR_BDPT_POOL_SCALE=0) and the oracle.
+"""
+import numpy as np
+import pytest
+
+import _oracle
+import _scenes
+from _parity import assert_film_parity, assert_ray_counts
+from winmad_rt import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _render(path, W, H, it, seed, scale, monkeypatch, ctl=3, pipes=None, film_ptr=None):
+    monkeypatch.setenv("WR_BDPT_POOL_SCALE", str(scale))
+    c = native.Context(native.Scene(path), 0)
+    if pipes:
+        c.set_pipelines(pipes)
+    try:
+        return c.render_bdpt(W, H, iterations=it, seed=seed, control_length=ctl, film_ptr=film_ptr)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("name,maker,W,H,it,seed,ctl,scale,case", [
+    ("torus", lambda: _scenes.torus(256, 256), 256, 256, 2, 5, 3, 0.002, "bdpt_torus256x256_i2_s5"),
+    ("cbox", lambda: _scenes.cbox(64, 48, "bdpt"), 64, 48, 3, 5489, 0, 0.02, "bdpt_cbox64x48_i3_s5489_ctl0"),
+])
+def test_pool_overflow_is_redone_exactly(name, maker, W, H, it, seed, ctl, scale, case, monkeypatch):
+    """Tiny pools overflow: the render is redone (st.redone) and equals the
+    unbounded render -- same rays, same film up to the order of float atomics
+    -- and the oracle's film, under the gates of the same render with the
+    default buffers (its measured split limits)."""
+    path = maker()
+    small, ss = _render(path, W, H, it, seed, scale, monkeypatch, ctl=ctl, pipes=4)
+    full, sf = _render(path, W, H, it, seed, 0, monkeypatch, ctl=ctl, pipes=4)
+    assert ss.redone == 1 and sf.redone == 0, (ss.redone, sf.redone)
+    assert ss.closest_rays == sf.closest_rays and ss.shadow_rays == sf.shadow_rays
+    assert np.allclose(small, full, rtol=1e-4, atol=1e-6)
+    ref, rst = _oracle.Scene(path).bdpt(W, H, it, seed, mode=1, control_length=ctl)
+    assert_film_parity(small, ref, case=case)
+    assert_ray_counts(ss, rst, slack=64)
+
+
+def test_pool_overflow_redo_keeps_a_device_film(monkeypatch):
+    """A device film that already holds a sum (a resumed or sharded render) is
+    restored before the redo: the result is that sum plus the render, as with
+    unbounded buffers."""
+    torch = pytest.importorskip("torch")
+    path = _scenes.torus(96, 64)
+    base = torch.rand((64, 96, 3), dtype=torch.float32, device="cuda:0")
+    dev = base.clone()
+    _, st = _render(path, 96, 64, 2, 7, 0.002, monkeypatch, film_ptr=dev.data_ptr())
+    torch.cuda.synchronize()
+    ref, _ = _render(path, 96, 64, 2, 7, 0, monkeypatch)
+    assert st.redone == 1
+    assert np.allclose(dev.cpu().numpy() - base.cpu().numpy(), ref, rtol=1e-4, atol=1e-5)
+
+
+def test_default_pools_hold_the_headline_render_at_1k_per_path(monkeypatch):
+    """The default sizing: the C2 frame (1080p torus, 2 iterations, 16
+    pipelines) is not redone, and the work buffers hold <= 1.2 KB per path in
+    flight (3.0 KB with the worst-case layout)."""
+    monkeypatch.delenv("WR_BDPT_POOL_SCALE", raising=False)
+    path = _scenes.torus(1920, 1080)
+    c = native.Context(native.Scene(path), 0)
+    film, st = c.render_bdpt(1920, 1080, iterations=2, seed=5)
+    c.close()
+    per_path = st.work_bytes / max(1, st.work_paths)
+    print(f"work buffers: {st.work_bytes / 2**30:.2f} GiB for {st.work_paths} paths = {per_path:.0f} B per path")
+    assert st.redone == 0
+    assert per_path <= 1200, per_path
+    _, sf = _render(path, 1920, 1080, 2, 5, 0, monkeypatch)
+    assert sf.work_bytes / sf.work_paths > 2.5 * per_path, (sf.work_bytes / sf.work_paths, per_path)

@@ -118,8 +118,18 @@ __device__ __forceinline__ void cvst3(float* s, int i, int k, V3 v) {
 struct BdptBuf {
   int P = 0, cap_sq = 0;
   float *ls, *cs;  // light / camera subpath state, PS_WORDS floats per path
-  float* vs;       // stored light vertices, VS_WORDS floats per slot k * P + p (k < kVMax)
-  float* cv;       // overlapped schedule: stored camera vertices, CV_WORDS floats per slot j * P + p (j < kCvMax)
+  float* vs;       // stored light vertices, VS_WORDS floats per record (sequential schedule: record k * P + p)
+  float* cv;       // overlapped schedule: stored camera vertices, CV_WORDS floats per record
+  // Overlapped schedule: the vertex stores are pools, sized by use rather than
+  // by the worst case (the reference pushes only the vertices a path makes,
+  // bidirPathTracing.cpp:101-102): vertex k of path p is record vidx[k * P +
+  // p] of vs (cidx for cv), taken from the step counters' vpool / cpool; -1
+  // when the pool was full.  A full pool or shadow queue sets the render's
+  // overflow counter and the host renders again with pieces the worst case
+  // fits (wr_render.hip, render_bdpt_one).  Null: records k * P + p.
+  int* vidx;
+  int* cidx;
+  int vcap = 0, ccap = 0;
   // extension-ray queues (double buffered, SoA with stride qs).  Overlapped
   // schedule: qs = 2P, the light pass's rays of a bounce first (count
   // ext[b]), the camera pass's behind them (count ext[kCamSlot + b])
@@ -152,6 +162,7 @@ struct BdptArgs {
   uint32_t seed, iter;
   int ctl, maxlen, faithful;
   int overlap = 0;  // 1: the overlapped schedule (light splats into the step's sq, CV store, light-side connections)
+  int untiled = 0;  // 1: camera paths in plain path order (a render redone with small pieces, BdptBuf)
 };
 // First queue index of the camera pass's extension rays of step `slot`
 // (kCamSlot + bounce): overlapped, behind the light pass's rays of the same
@@ -164,6 +175,29 @@ struct BdptGroup {
 };
 
 __device__ __forceinline__ bool len_ok(int ctl, int L) { return ctl <= 0 || L == ctl; }
+
+// record of stored light vertex k / camera vertex j of path p (-1: the pool was full)
+__device__ __forceinline__ int lv_slot(const BdptBuf& B, int k, int p) {
+  return B.vidx ? B.vidx[size_t(k) * B.P + p] : k * B.P + p;
+}
+__device__ __forceinline__ int cv_slot(const BdptBuf& B, int j, int p) {
+  return B.cidx ? B.cidx[size_t(j) * B.P + p] : j * B.P + p;
+}
+// A pool record for this lane (called by the lanes that store, together:
+// one atomic per wave); -1 and the overflow counter when the pool is full
+__device__ __forceinline__ int pool_take(const BdptArgs& A, int* counter, int cap) {
+  const int i = wave_append(counter, true);
+  if (i < cap) return i;
+  atomicAdd(&A.ctr->overflow, 1ull);
+  return -1;
+}
+// a shadow / aux queue slot from wave_append: within the queue, or the overflow counter
+__device__ __forceinline__ bool sq_fits(const BdptArgs& A, bool want, int si) {
+  if (!want) return false;
+  if (si < A.B.cap_sq) return true;
+  atomicAdd(&A.ctr->overflow, 1ull);
+  return false;
+}
 // Numerators of three MIS weights -- connectVertices (:658-664),
 // getDirectIllumination's outer weight (:529) and connectToCamera's (:360):
 // 1 in every product build.  scripts/perturbation_check.sh builds variants
@@ -319,7 +353,7 @@ __device__ __forceinline__ void queue_connection(const BdptArgs& A, int qslot, b
   const BdptBuf::Sq& Q = B.sq[qslot & 1];
   const int cap = B.cap_sq;
   const int si = wave_append(&A.sc->sq[qslot], shoot);
-  if (shoot) {
+  if (sq_fits(A, shoot, si)) {
     st3(Q.o, cap, si, hp);
     st3(Q.d, cap, si, sdir);
     st3(Q.tgt, cap, si, stgt);
@@ -355,21 +389,27 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
       dvc /= fabsf(b.wi.z);
       if (!b.delta) {  // lightStates.push_back (:101-102)
         const int k = psi(B.ls, p, PS_VCOUNT);
-        const int slot = k * P + p;
-        vst3(B.vs, slot, VS_POS, h.p);
-        vst3(B.vs, slot, VS_N, h.n);
-        vst3(B.vs, slot, VS_WI, b.wi);
-        vst3(B.vs, slot, VS_THR, thr);
-        vsf(B.vs, slot, VS_DVCM) = dvcm;
-        vsf(B.vs, slot, VS_DVC) = dvc;
-        vsf(B.vs, slot, VS_CONT) = b.cont;
-        vsf(B.vs, slot, VS_PD) = b.pd;
-        vsf(B.vs, slot, VS_PG) = b.pg;
-        vsi(B.vs, slot, VS_LEN) = len;
-        vsi(B.vs, slot, VS_NSPEC) = nspec;
-        vsi(B.vs, slot, VS_MAT) = b.mat;
+        int slot = k * P + p;
+        if (B.vidx) {  // a pool record (the storing lanes of the wave take theirs together)
+          slot = pool_take(A, &A.sc->vpool, B.vcap);
+          B.vidx[size_t(k) * P + p] = slot;
+        }
+        if (slot >= 0) {
+          vst3(B.vs, slot, VS_POS, h.p);
+          vst3(B.vs, slot, VS_N, h.n);
+          vst3(B.vs, slot, VS_WI, b.wi);
+          vst3(B.vs, slot, VS_THR, thr);
+          vsf(B.vs, slot, VS_DVCM) = dvcm;
+          vsf(B.vs, slot, VS_DVC) = dvc;
+          vsf(B.vs, slot, VS_CONT) = b.cont;
+          vsf(B.vs, slot, VS_PD) = b.pd;
+          vsf(B.vs, slot, VS_PG) = b.pg;
+          vsi(B.vs, slot, VS_LEN) = len;
+          vsi(B.vs, slot, VS_NSPEC) = nspec;
+          vsi(B.vs, slot, VS_MAT) = b.mat;
+        }
         psi(B.ls, p, PS_VCOUNT) = k + 1;
-        if (A.overlap) {  // the camera vertices stored at earlier steps (lengths < len)
+        if (A.overlap && slot >= 0) {  // the camera vertices stored at earlier steps (lengths < len)
           lslot = slot;
           llen = len;
           lconn = psi(B.cs, p, PS_CVCOUNT);
@@ -444,7 +484,7 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
   // the next step's extension rays, like the camera vertices' rays
   const int sslot = A.overlap ? kCamSlot + oslot : kCamSlot;
   const int si = wave_append(&A.sc->sq[sslot], splat);
-  if (splat) {
+  if (sq_fits(A, splat, si)) {
     const BdptBuf::Sq& Q = B.sq[sslot & 1];
     st3(Q.o, B.cap_sq, si, s_o);
     st3(Q.d, B.cap_sq, si, s_d);
@@ -461,8 +501,8 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
       bool shoot = false;
       int pix = -1;
       V3 hp{}, sdir{}, stgt{}, sval{};
-      if (j < lconn) {
-        const int cs = j * P + p;
+      const int cs = j < lconn ? cv_slot(B, j, p) : -1;
+      if (cs >= 0) {
         const int clen = cvi(B.cv, cs, CV_LEN);
         if (llen + 1 + clen > A.maxlen) {
           lconn = j;  // camera vertices are stored by increasing length
@@ -539,7 +579,7 @@ __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s, int ebas
   // path <-> pixel mapping stays the reference's (x = p / W, y = p % W, :422-423).
   // A tiled piece is whole 8-row bands (base and n multiples of 8 W), so the
   // tiles are the piece's own.
-  const bool tiled = (A.W % 8) == 0 && (A.H % 8) == 0;
+  const bool tiled = !A.untiled && (A.W % 8) == 0 && (A.H % 8) == 0;
   const int tiles_y = A.W / 8;
   int l;
   if (tiled) {
@@ -716,7 +756,12 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
           // (len < l, l + 1 + len <= maxlen) is kept for that light vertex
           if (A.overlap && 2 * len + 2 <= A.maxlen) {
             const int j = psi(B.cs, p, PS_CVCOUNT);
-            const int cs = j * P + p;
+            int cs = j * P + p;
+            if (B.cidx) {  // a pool record
+              cs = pool_take(A, &A.sc->cpool, B.ccap);
+              B.cidx[size_t(j) * P + p] = cs;
+            }
+            if (cs >= 0) {
             cvst3(B.cv, cs, CV_POS, hp);
             cvst3(B.cv, cs, CV_N, h.n);
             cvst3(B.cv, cs, CV_WI, b.wi);
@@ -730,6 +775,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
             cvi(B.cv, cs, CV_NSPEC) = cnspec;
             cvi(B.cv, cs, CV_MAT) = b.mat;
             cvi(B.cv, cs, CV_PIX) = pix;
+            }
             psi(B.cs, p, PS_CVCOUNT) = j + 1;
           }
         }
@@ -750,7 +796,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
   // DI queue entries
   {
     const int ni = wave_append(&A.sc->sq[oslot], nee);
-    if (nee) {
+    if (sq_fits(A, nee, ni)) {
       st3(Q.o, cap, ni, hp);
       st3(Q.d, cap, ni, nee_d);
       st3(Q.tgt, cap, ni, nee_tgt);
@@ -759,7 +805,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
       Q.pix[ni] = pix;
     }
     const int bi = wave_append(&A.sc->sq[oslot], dib);
-    if (dib) {
+    if (sq_fits(A, dib, bi)) {
       st3(Q.o, cap, bi, dib_o);
       st3(Q.d, cap, bi, dib_d);
       Q.cut[bi] = -WR_INF;  // needs the closest hit (same light?)
@@ -772,8 +818,8 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
     for (int k = 0; __ballot(conn_phase && k < nv); ++k) {
       bool shoot = false;
       V3 sdir{}, stgt{}, sval{};
-      if (conn_phase && k < nv) {
-        const int slot = k * P + p;
+      const int slot = conn_phase && k < nv ? lv_slot(B, k, p) : -1;
+      if (slot >= 0) {
         const int llen = vsi(B.vs, slot, VS_LEN);
         if (llen + 1 + len > A.maxlen) {
           nv = k;  // break (:237-239)
@@ -867,7 +913,7 @@ __device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int
   const DevScene& S = A.S;
   const BdptBuf::Sq& Q = B.sq[slot & 1];
   const BdptBuf::Di& D = B.di[slot & 1];
-  const int n = A.sc->sq[slot], cap = B.cap_sq;
+  const int cap = B.cap_sq, n = min(A.sc->sq[slot], cap);  // (appends past cap were dropped: overflow)
   const int gstride = nblk * blockDim.x;
   const int nround = (n + gstride - 1) / gstride * gstride;
   for (int j = bid * blockDim.x + threadIdx.x; j < nround; j += gstride) {

@@ -1,5 +1,5 @@
 // Host build of the verified-BVH fast path (wr_bvh.h): a binned-SAH BVH over the
-// scene's triangles, and for every triangle the root-to-leaf paths of the
+// scene's triangles and spheres, and for every primitive the root-to-leaf paths of the
 // reference KD leaves that hold it (KDtreeAccel::buildTree,
 // src/scene/KDtreeAccel.cpp:118-307, as restated in wr_scene.cpp).
 #include "wr_bvh.h"
@@ -94,18 +94,31 @@ struct Builder {
     for (int i = b; i < e; ++i) {
       const wr::Prim& p = s.prims[tri_prim[idx[i]]];
       TriRec r;
-      // A..F exactly as Triangle::hit forms them (triangle.cpp:24-30)
-      r.a[0] = p.p0.x;
-      r.a[1] = p.p0.y;
-      r.a[2] = p.p0.z;
-      r.a[3] = p.p0.x - p.p1.x;
-      r.b[0] = p.p0.y - p.p1.y;
-      r.b[1] = p.p0.z - p.p1.z;
-      r.b[2] = p.p0.x - p.p2.x;
-      r.b[3] = p.p0.y - p.p2.y;
-      r.c[0] = p.p0.z - p.p2.z;
       const int32_t prim = tri_prim[idx[i]];
-      std::memcpy(&r.c[1], &prim, 4);
+      if (p.type == wr::kTri) {
+        // A..F exactly as Triangle::hit forms them (triangle.cpp:24-30)
+        r.a[0] = p.p0.x;
+        r.a[1] = p.p0.y;
+        r.a[2] = p.p0.z;
+        r.a[3] = p.p0.x - p.p1.x;
+        r.b[0] = p.p0.y - p.p1.y;
+        r.b[1] = p.p0.z - p.p1.z;
+        r.b[2] = p.p0.x - p.p2.x;
+        r.b[3] = p.p0.y - p.p2.y;
+        r.c[0] = p.p0.z - p.p2.z;
+        std::memcpy(&r.c[1], &prim, 4);
+      } else {
+        // a sphere: -(prim + 1) as in the KD refs (wr_traverse.h); Sphere::hit
+        // reads its centre, radius and box from the primitive arrays
+        r.a[0] = p.c.x;
+        r.a[1] = p.c.y;
+        r.a[2] = p.c.z;
+        r.a[3] = p.r;
+        r.b[0] = r.b[1] = r.b[2] = r.b[3] = 0.f;
+        r.c[0] = 0.f;
+        const int32_t code = -(prim + 1);
+        std::memcpy(&r.c[1], &code, 4);
+      }
       // the primitive's KD leaf list (prim_leaf range): no extra lookup when it wins
       const int32_t lb = leaf_off[static_cast<size_t>(prim)];
       const int32_t ln = leaf_off[static_cast<size_t>(prim) + 1] - lb;
@@ -597,13 +610,22 @@ struct Collapse8 {
 
 }  // namespace
 
+// Sphere::hit (sphere.cpp:17-78) forms t = t_ca -+ sqrt(t_hc), t_hc = r^2 -
+// |oc|^2 + t_ca^2 with oc = centre - origin: a sum of terms of magnitude up to
+// M^2 (M = |oc| or r) whose float rounding moves t_hc by up to ~1.2e-6 M^2.
+// The square root turns that into an error of t of at most 2.7e-5 M^2 when the
+// accepted t_hc (> EPS) is far above the noise, and of up to ~2 sqrt(1.2e-6) M
+// where the noise decides (a ray at the sphere's rim; there the "hit" lies
+// within r + 2.2e-3 M of the centre).  So every t Sphere::hit accepts lies on
+// the ray within sphere_grow(M) of the sphere's box, with M bounded by the
+// distance of the ray's origin from the centre plus r: the BVH boxes of
+// spheres are grown by that for every origin in the region the render's rays
+// start from (the scene's box and the camera: FastHost::org_lo / org_hi), and
+// the search sends a ray from outside it to the KD walk (wr_fast.h).
+double sphere_grow(double M) { return 3e-5 * M * M + 2.5e-3 * M + 2.0 * 1e-3; }
+
 void build_fast(const wr::Scene& s, FastHost& out, int wide, bool with4) {
   out = FastHost();
-  for (const auto& p : s.prims)
-    if (p.type != wr::kTri) {
-      out.why = "scene has spheres (the fast path covers triangles only)";
-      return;
-    }
   if (s.prims.empty() || s.nodes.empty()) {
     out.why = "empty scene";
     return;
@@ -616,9 +638,52 @@ void build_fast(const wr::Scene& s, FastHost& out, int wide, bool with4) {
   std::vector<Box> box(n);
   std::vector<float> cen(3 * n);
   std::vector<int> tri_prim(n), idx(n);
+  // where the renderer's rays start: the scene (its KD root box) and the camera
+  {
+    const float rl[3] = {s.root_l.x, s.root_l.y, s.root_l.z}, rr[3] = {s.root_r.x, s.root_r.y, s.root_r.z};
+    const float cp[3] = {s.cam.pos.x, s.cam.pos.y, s.cam.pos.z};
+    float ext = 0.f;
+    for (int k = 0; k < 3; ++k) {
+      out.org_lo[k] = std::min(rl[k], cp[k]);
+      out.org_hi[k] = std::max(rr[k], cp[k]);
+      ext = std::max(ext, out.org_hi[k] - out.org_lo[k]);
+    }
+    // slack: extension rays start EPS past a surface point, which may lie on the box
+    const float slack = 0.01f * ext + 0.01f;
+    for (int k = 0; k < 3; ++k) {
+      out.org_lo[k] -= slack;
+      out.org_hi[k] += slack;
+    }
+  }
+  for (const auto& p : s.prims) out.spheres += p.type != wr::kTri ? 1 : 0;
   auto prep = [&](size_t i0, size_t i1) {
     for (size_t i = i0; i < i1; ++i) {
       const wr::Prim& p = s.prims[i];
+      tri_prim[i] = static_cast<int>(i);
+      idx[i] = static_cast<int>(i);
+      if (p.type != wr::kTri) {
+        // the reference's box (AABB::extend, as box.hit tests it) grown by the
+        // reach of Sphere::hit's rounding for the farthest ray origin
+        const float c[3] = {p.c.x, p.c.y, p.c.z};
+        double M2 = 0.0;
+        for (int k = 0; k < 3; ++k) {
+          const double a = std::max(std::fabs(static_cast<double>(out.org_lo[k]) - c[k]),
+                                    std::fabs(static_cast<double>(out.org_hi[k]) - c[k]));
+          M2 += a * a;
+        }
+        const double M = std::sqrt(M2) + std::fabs(static_cast<double>(p.r));
+        const double g = sphere_grow(M) + 1e-6 * (1.0 + std::max({std::fabs(p.bl.x), std::fabs(p.bl.y),
+            std::fabs(p.bl.z), std::fabs(p.br.x), std::fabs(p.br.y), std::fabs(p.br.z)}));
+        Box b;
+        const float bl[3] = {p.bl.x, p.bl.y, p.bl.z}, br[3] = {p.br.x, p.br.y, p.br.z};
+        for (int k = 0; k < 3; ++k) {
+          b.lo[k] = std::nextafter(static_cast<float>(std::min(bl[k], c[k] - std::fabs(p.r)) - g), -INFINITY);
+          b.hi[k] = std::nextafter(static_cast<float>(std::max(br[k], c[k] + std::fabs(p.r)) + g), INFINITY);
+          cen[3 * i + k] = 0.5f * (b.lo[k] + b.hi[k]);
+        }
+        box[i] = b;
+        continue;
+      }
       const float v[3][3] = {{p.p0.x, p.p0.y, p.p0.z}, {p.p1.x, p.p1.y, p.p1.z}, {p.p2.x, p.p2.y, p.p2.z}};
       Box b;
       for (auto& q : v) b.grow(q);
@@ -636,8 +701,6 @@ void build_fast(const wr::Scene& s, FastHost& out, int wide, bool with4) {
         cen[3 * i + k] = 0.5f * (b.lo[k] + b.hi[k]);
       }
       box[i] = b;
-      tri_prim[i] = static_cast<int>(i);
-      idx[i] = static_cast<int>(i);
     }
   };
   // the KD membership data first (the triangle records carry their

@@ -82,7 +82,8 @@ static_assert(sizeof(BNode8) == 128, "8-wide BVH node is 128 bytes");
 // 48 bytes per triangle, in BVH leaf order, laid out as the KD refs
 // (wr_traverse.h): (p0.xyz, A), (B, C, D, E), (F, prim, lb, ln) with A..F =
 // p0 - p1, p0 - p2 exactly as Triangle::hit forms them and [lb, lb + ln) the
-// primitive's range of prim_leaf.
+// primitive's range of prim_leaf.  A sphere: (centre, r), 0, (0, -(prim + 1),
+// lb, ln) -- Sphere::hit reads its geometry from the primitive arrays.
 struct TriRec {
   float a[4], b[4], c[4];
 };
@@ -152,11 +153,14 @@ struct FastHost {
   std::vector<PrimRec> prim_rec;  // per primitive
   int depth = 0;               // deepest node chain (stack bound)
   int leaves = 0;
+  int spheres = 0;             // sphere primitives in the tree
+  float org_lo[3] = {0.f, 0.f, 0.f}, org_hi[3] = {0.f, 0.f, 0.f};  // where rays start (scene box + camera):
+                                                                 // sphere boxes are grown for origins in it
   bool ok = false;
   std::string why;  // when !ok: why the fast path is off for this scene
 };
-// Build the BVH over the scene's triangles and the KD membership data.  Scenes
-// with spheres keep the faithful traversal only (ok = false).
+// Build the BVH over the scene's triangles and spheres and the KD membership
+// data.
 // wide: the search tree built beside the binary one (4: nodes4, 8: nodes8);
 // with4: the 4-wide one as well (a binary-tree scene's latency-bound renders)
 void build_fast(const wr::Scene& s, FastHost& out, int wide = WR_BVH_WIDE, bool with4 = false);

@@ -48,7 +48,12 @@ struct FastScene {
   const int* node_path;  // KD leaf node -> path record offset
   const float4* node_cell;  // 2 per KD node: cell lo, hi
   const float4* prim_rec;   // 8 per primitive (wrf::PrimRec): its first four leaves' cells and records
-  V3 lo, hi;  // union of the (grown) triangle boxes
+  V3 lo, hi;  // union of the (grown) triangle / sphere boxes
+  // spheres in the tree (0: triangles only).  Their boxes are grown for ray
+  // origins inside [org_lo, org_hi] (wr_bvh.cpp, sphere_grow); a ray from
+  // outside takes the KD walk
+  int sph;
+  V3 org_lo, org_hi;
   int depth;   // stack entries of the KD walks and tie resolution (k_fast_hard, k_fast_verify)
   int sdepth;  // stack entries of the BVH search (k_trace_fast): the BVH's depth + 1
   int walk_wave;  // 1: the one-ray-per-wave resolutions walk the KD tree with the whole wave (kd_walk_wave)
@@ -374,6 +379,21 @@ __device__ __forceinline__ int kd_member(const DevScene& S, const FastScene& F, 
 // The stack holds (node, tmin) in LDS columns of stride 64; an entry's tmax is
 // the previous entry's tmin (the root tmax for entry 0), the floats the
 // reference's todo[] holds.
+// One primitive of a KD leaf (refs: ref_c.y = prim, or -(prim + 1) for a
+// sphere) or of a BVH leaf (TriRec: the same code in c.y): Triangle::hit
+// (tri_test: the screen against t_best only drops what the exact test rejects
+// or what cannot improve t_best) or Sphere::hit (sph_hit, sphere.cpp:17-78).
+// prim gets the primitive.
+__device__ __forceinline__ bool prim_test(const DevScene& S, float4 a, float4 b, float f, int code, V3 o, V3 d,
+                                          float rtmin, float rtmax, float t_best, float& t, int& prim) {
+  if (code >= 0) {
+    prim = code;
+    return tri_test(a, b, f, o, d, rtmin, rtmax, t_best, t);
+  }
+  prim = -code - 1;
+  return sph_hit(S, prim, o, d, rtmin, rtmax, t);
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtmin, float rtmax, int* stk_node,
                                         float* stk_tmin, float& t_best, int& best, FastCounters& ctr) {
@@ -431,9 +451,11 @@ __device__ __forceinline__ void kd_walk(const DevScene& S, V3 o, V3 d, float rtm
       for (int u = 0; u < 4; ++u) {
         if (k0 + u >= cnt) break;
         float t;
-        if (tri_test(ra[u], rb[u], rc[u].x, o, d, rtmin, rtmax, t_best, t) && cmpf(t - t_best) < 0) {
+        int prim;
+        if (prim_test(S, ra[u], rb[u], rc[u].x, __float_as_int(rc[u].y), o, d, rtmin, rtmax, t_best, t, prim) &&
+            cmpf(t - t_best) < 0) {
           t_best = t;
-          best = __float_as_int(rc[u].y);
+          best = prim;
         }
       }
     }
@@ -634,10 +656,11 @@ __device__ __forceinline__ bool kd_walk_wave(const DevScene& S, V3 o, V3 d, floa
         for (int u = 0; u < 4; ++u) {
           if (k0 + u >= cnt) break;
           float t;
+          int prim;
           // t_best WR_INF: the exact Triangle::hit outcome (the screen drops
           // only what it proves rejected); the replay applies the rule
-          if (tri_test(ra[u], rb[u], rc[u].x, o, d, rtmin, rtmax, WR_INF, t) && cmpf(t - WR_INF) < 0) {
-            const int prim = __float_as_int(rc[u].y);
+          if (prim_test(S, ra[u], rb[u], rc[u].x, __float_as_int(rc[u].y), o, d, rtmin, rtmax, WR_INF, t, prim) &&
+              cmpf(t - WR_INF) < 0) {
             uint32_t h = (static_cast<uint32_t>(prim) * 2654435761u) >> (32 - lg);
             bool put = false;
             for (int probe = 0; probe < T && !put; ++probe) {
@@ -719,7 +742,7 @@ constexpr int kTieWaveLeaves = 65536;  // ... or, one ray per wave, up to this m
 #define WR_TIE_DEFER 0
 #endif
 constexpr int kTieDeferred = -1;
-__device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float rtmin, float rtmax, float cap,
+__device__ __forceinline__ int bvh_collect(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin, float rtmax, float cap,
                                            int* stk_link, float* stk_t, float (&ct)[kTie], int (&cp)[kTie]) {
   rtmax = fminf(rtmax, cap);
 #pragma unroll
@@ -776,12 +799,13 @@ __device__ __forceinline__ int bvh_collect(const FastScene& F, V3 o, V3 d, float
       for (int j = 0; j < cnt; ++j) {
         const float4* tp = F.tris + 3 * static_cast<size_t>(first + j);
         float t;
+        int npr;
         // screen: only hits below the current kTie-th can enter the list
-        if (tri_test(tp[0], tp[1], tp[2].x, o, d, rtmin, rtmax, fminf(ct[kTie - 1], rtmax) + WR_EPS + WR_EPS, t) &&
+        if (prim_test(S, tp[0], tp[1], tp[2].x, __float_as_int(tp[2].y), o, d, rtmin, rtmax,
+                      fminf(ct[kTie - 1], rtmax) + WR_EPS + WR_EPS, t, npr) &&
             t <= rtmax) {
           ++found;
           float nt = t;
-          int npr = __float_as_int(tp[2].y);
 #pragma unroll
           for (int k = 0; k < kTie; ++k) {  // insertion, sorted by t
             const bool sw = nt < ct[k];
@@ -1002,7 +1026,10 @@ __device__ WR_HARD_CALL void kd_first_leaves(const DevScene& S, const FastScene&
       for (uint32_t j0 = 0; j0 < cnt && want; j0 += 8) {
         int pr[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) pr[u] = j0 + u < cnt ? __float_as_int(S.ref_c[first + j0 + u].y) : -1;
+        for (int u = 0; u < 8; ++u) {
+          const int code = j0 + u < cnt ? __float_as_int(S.ref_c[first + j0 + u].y) : -1;
+          pr[u] = code >= 0 || j0 + u >= cnt ? code : -code - 1;  // a sphere's ref: -(prim + 1)
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
           for (int c = 0; c < kTie; ++c)
@@ -1057,7 +1084,7 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
   // triangle is not visited, the kTie smallest hits without a bound
   for (int pass = 0; pass < 2; ++pass) {
     const float cap = pass == 0 ? t1 + 3.f * WR_EPS : WR_INF;
-    n = bvh_collect(F, o, d, rtmin, rtmax, cap, stk_link, stk_t, ct, cp);
+    n = bvh_collect(S, F, o, d, rtmin, rtmax, cap, stk_link, stk_t, ct, cp);
     m = WR_INF;
     const int ncand = min(n, kTie);
     // per candidate: its first visited leaf as a visit-order key (~0: none).
@@ -1171,7 +1198,9 @@ struct QueueIndex {
     int acc = 0;
 #pragma unroll
     for (int i = 0; i < kMaxQueues; ++i) {
-      if (i < Q.n && Q.q[i].count) acc += *Q.q[i].count + (Q.q[i].count2 ? *Q.q[i].count2 : 0);
+      // (a shadow queue's count may pass its capacity: the appends past it were
+      // dropped and the render is redone, BdptBuf)
+      if (i < Q.n && Q.q[i].count) acc += min(*Q.q[i].count + (Q.q[i].count2 ? *Q.q[i].count2 : 0), Q.q[i].cap);
       qend[i] = acc;
     }
     n = acc;
@@ -1244,7 +1273,7 @@ __device__ __forceinline__ bool tri_grazes(float4 a, float4 b, float f, V3 o, V3
   return fabsf(den) <= kGrazeRel * mag && fabsf(tnum) <= kGrazePlaneRel * tmag;
 }
 
-template <bool COUNT, int W>
+template <bool COUNT, int W, bool SPH>
 __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, int* fetch,
                                            float* t2buf, int2* spill, uint32_t* lds, FastCounters& ctr,
                                            int bid, int nblk) {  // this block's index among the launch's nblk search blocks
@@ -1379,6 +1408,11 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           tcap = fmaxf(0.f, fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)));
           olen = fabsf(o.x) + fabsf(o.y) + fabsf(o.z);
           margins();
+          // spheres: their boxes cover Sphere::hit's rounding for origins in
+          // [org_lo, org_hi] only (wr_bvh.cpp): a ray from elsewhere (an API
+          // caller's) takes the KD walk
+          if (SPH) gz = !(o.x >= F.org_lo.x && o.y >= F.org_lo.y && o.z >= F.org_lo.z && o.x <= F.org_hi.x &&
+                          o.y <= F.org_hi.y && o.z <= F.org_hi.z);
         }
         if (__ballot(idle && idx >= n)) pool = false;
       }
@@ -1566,13 +1600,21 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           ++rt;
         }
         float t;
-        gz |= tri_grazes(ta[j], tb[j], tc[j].x, o, d);
-        // screen against t1 + 3 EPS: every hit with t <= t1 + 2 EPS survives
-        if (tri_test(ta[j], tb[j], tc[j].x, o, d, rtmin, rtmax, t1 + 3.f * WR_EPS, t)) {
+        int pr = __float_as_int(tc[j].y);
+        bool hit;
+        if (SPH && pr < 0) {  // a sphere: Sphere::hit, the same floats (no plane to graze)
+          pr = -pr - 1;
+          hit = sph_hit(S, pr, o, d, rtmin, rtmax, t);
+        } else {
+          gz |= tri_grazes(ta[j], tb[j], tc[j].x, o, d);
+          // screen against t1 + 3 EPS: every hit with t <= t1 + 2 EPS survives
+          hit = tri_test(ta[j], tb[j], tc[j].x, o, d, rtmin, rtmax, t1 + 3.f * WR_EPS, t);
+        }
+        if (hit) {
           if (t < t1) {
             t2 = t1;
             t1 = t;
-            p1 = __float_as_int(tc[j].y);
+            p1 = pr;
           } else if (t < t2) {
             t2 = t;
           }

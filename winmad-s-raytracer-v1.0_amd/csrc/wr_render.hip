@@ -131,6 +131,7 @@ struct StepCounters {
   int mq[kSlots];     // VCM: merge queries queued at step `slot`
   int hard[kSlots][2];  // WR_TRACE_BVH: rays of step `slot` left to k_fast_hard (tie list, scan list)
   int late[kSlots][2];  // WR_TRACE_BVH: rays of step `slot` deferred (late list: ties, scans)
+  int vpool, cpool;     // BDPT, overlapped: records taken from the light / camera vertex pools
 };
 struct DevCounters {
   int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
@@ -143,6 +144,7 @@ struct DevCounters {
   unsigned long long deferred;  // BDPT rays settled off the critical path (late lists)
   unsigned long long lat[7];  // WR_TRACE_BVH latency tail (FastCounters mem_max .. scans; max or sum)
   unsigned long long ww[4];   // kd_walk_wave: walks, rounds, nodes, serial fall-backs
+  unsigned long long overflow;  // BDPT: appends a full vertex pool / shadow queue dropped (the render is redone)
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -272,7 +274,9 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
 #ifndef WR_FAST4_WAVES
 #define WR_FAST4_WAVES 5  // the 4-wide search: 98 VGPRs at 4, held to 96 for 5 waves per SIMD
 #endif
-template <bool COUNT, bool LATE, int W>
+// SPH: the tree holds spheres (FastScene::sph) -- a variant of its own, so
+// that the triangle scenes' search keeps its registers
+template <bool COUNT, bool LATE, int W, bool SPH>
 __global__ void __launch_bounds__(kTraceBlock)
 __attribute__((amdgpu_waves_per_eu(W == 4 && !LATE ? WR_FAST4_WAVES : WR_FAST_WAVES, 8))) WR_NO_PK_FP32
 k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* spill,
@@ -288,7 +292,7 @@ k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetc
       atomicAdd(&ctr->deferred, static_cast<unsigned long long>(min(L.n[m][0], half) + min(L.n[m][1], half)));
     }
   } else {
-    trace_fast<COUNT, W>(S, F, Q, fetch, t2buf, spill, smem, fc, b - (LATE ? lblocks : 0),
+    trace_fast<COUNT, W, SPH>(S, F, Q, fetch, t2buf, spill, smem, fc, b - (LATE ? lblocks : 0),
                          static_cast<int>(gridDim.x) - (LATE ? lblocks : 0));
   }
   if (COUNT) fast_counts<COUNT>(ctr, fc);
@@ -298,11 +302,13 @@ k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetc
 using TraceFastKernel = void (*)(DevScene, FastScene, TraceQueues, DevCounters*, int*, float*, int2*, LateArgs, int, int,
                                  int, int, int);
 template <bool COUNT, bool LATE>
-TraceFastKernel trace_fast_kernel(int wide) {
+TraceFastKernel trace_fast_kernel(int wide, bool sph = false) {
 #if WR_BVH_WIDE == 8
-  if (wide == 8) return k_trace_fast<COUNT, LATE, 8>;
+  if (wide == 8) return k_trace_fast<COUNT, LATE, 8, false>;  // (triangle scenes: the 8-wide tree is a build option)
 #endif
-  return wide == 4 ? k_trace_fast<COUNT, LATE, 4> : k_trace_fast<COUNT, LATE, 2>;
+  // (the deferred-hard-ray variants, LATE, are not built with spheres: defer_enabled)
+  if (sph && !LATE) return wide == 4 ? k_trace_fast<COUNT, false, 4, true> : k_trace_fast<COUNT, false, 2, true>;
+  return wide == 4 ? k_trace_fast<COUNT, LATE, 4, false> : k_trace_fast<COUNT, LATE, 2, false>;
 }
 #ifndef WR_RESOLVE_WAVES
 #define WR_RESOLVE_WAVES 0  // > 0: the resolve's register budget as waves per SIMD (0: the compiler's choice, 101 VGPRs)
@@ -503,6 +509,7 @@ struct Pipe {
   size_t work_key = 0;  // P for which `work` is laid out
   int work_kind = 0;    // 1 bdpt, 2 pt, 3 vcm (bdpt + vcm buffers)
   int work_sets = 0;    // buffer sets laid out
+  float work_pool = -1.f;  // the BDPT pool scale they were laid out with (bdpt_pool_scale)
   BdptBuf bb[kGroup]{};
   PtBuf pb[kGroup]{};
   VcmBuf vb[kGroup]{};
@@ -537,6 +544,9 @@ struct wr_context {
   DevCounters* ctr = nullptr;  // API traversal
   float* film_tmp = nullptr;
   size_t film_tmp_n = 0;
+  float* film_bak = nullptr;  // a device film as it was before a BDPT render (redone on pool overflow)
+  size_t film_bak_n = 0;
+  DevCounters* host_ctr = nullptr;  // pinned: the pipelines' counters after a render (finish_render)
   char* api_tmp = nullptr;  // wr_trace_closest / wr_occluded / wr_path_radiance scratch, grown on demand
   size_t api_tmp_n = 0;
   int grid = 2048;
@@ -662,19 +672,47 @@ __global__ void __launch_bounds__(256) k_film_accumulate(float* dst, const float
 // overlapped: the BDPT render's own layout (the camera pass's extension queues
 // and the camera-vertex store); VertexCM's BDPT part runs the sequential
 // schedule and goes without them
+// Overlapped BDPT: the shadow / aux queues and the vertex pools per path of
+// a buffer set (wr_bdpt.h, BdptBuf): what the reference scenes use is far
+// below the worst case (torus: ~3 % of the 11 shadow rays a path may queue in
+// one step; ~1 stored light vertex of 9), so they are sized by use and a
+// render that fills one is redone with pieces the worst case fits (exact).
+// Env WR_BDPT_POOL_SCALE scales all three (tests force small ones); 0: the
+// worst case, no pools.
+constexpr float kSqPerPath = 2.f, kVPoolPerPath = 2.f, kCPoolPerPath = 1.f;
+float bdpt_pool_scale() {  // (read at every layout: a change re-lays out the buffers, ensure_work)
+  const char* e = std::getenv("WR_BDPT_POOL_SCALE");
+  return e ? std::max(0.f, static_cast<float>(std::atof(e))) : 1.f;
+}
+// capacity of a pool of `per` records per path, at least `floor` (a safe
+// re-render piece of 64 paths fits), at most the worst case
+int pool_cap(int P, float per, int worst, int floor) {
+  const float s = bdpt_pool_scale();
+  if (s <= 0.f) return worst * P;
+  const double want = std::ceil(static_cast<double>(P) * per * s);
+  return static_cast<int>(std::min<double>(static_cast<double>(worst) * P, std::max<double>(want, floor)));
+}
+
 void layout_bdpt(Arena& a, BdptBuf& B, int P, bool overlapped) {
   B.P = P;
   // shadow / aux rays queued by one step, per path: sequential schedule, a
   // camera vertex's <= kVMax connections + NEE + DI-BSDF (the light splats of
   // one path: <= kVMax); overlapped, at the step making vertices of length s:
   // camera side <= min(s, 9 - s) connections + NEE + DI-BSDF, light side
-  // <= min(s - 1, 9 - s) connections + its splat: <= 11 as well
-  B.cap_sq = P * (kVMax + 2);
-  const size_t sP = P, sV = size_t(kVMax) * P, sQ = B.cap_sq;
+  // <= min(s - 1, 9 - s) connections + its splat: <= 11 as well.  Overlapped:
+  // sized by use (kSqPerPath), the vertex stores pools (kVPoolPerPath,
+  // kCPoolPerPath) -- 1.0 KB per path instead of 3.0 KB
+  const bool pools = overlapped && bdpt_pool_scale() > 0.f;
+  B.cap_sq = pools ? pool_cap(P, kSqPerPath, kVMax + 2, (kVMax + 2) * 64) : P * (kVMax + 2);
+  B.vcap = pools ? pool_cap(P, kVPoolPerPath, kVMax, kVMax * 64) : kVMax * P;
+  B.ccap = pools ? pool_cap(P, kCPoolPerPath, kCvMax, kCvMax * 64) : kCvMax * P;
+  const size_t sP = P, sV = size_t(B.vcap), sQ = B.cap_sq;
   B.ls = a.take<float>(PS_WORDS * sP);
   B.cs = a.take<float>(PS_WORDS * sP);
   B.vs = a.take<float>(VS_WORDS * sV);
-  B.cv = overlapped ? a.take<float>(CV_WORDS * size_t(kCvMax) * P) : nullptr;
+  B.cv = overlapped ? a.take<float>(CV_WORDS * size_t(B.ccap)) : nullptr;
+  B.vidx = pools ? a.take<int>(size_t(kVMax) * P) : nullptr;
+  B.cidx = pools ? a.take<int>(size_t(kCvMax) * P) : nullptr;
   // overlapped: an extension queue holds both passes' rays (light, then camera)
   B.qs = overlapped ? 2 * P : P;
   const size_t sE = B.qs;
@@ -783,7 +821,7 @@ void layout_set(Arena& a, Pipe* dst, int g, int kind, int P) {
 
 int ensure_work(Pipe& p, int kind, int P, int sets) {
   // (a VCM layout holds the sequential BDPT layout only: no camera-pass queues)
-  const bool same = p.work_kind == kind;
+  const bool same = p.work_kind == kind && p.work_pool == bdpt_pool_scale();
   if (same && p.work_key == static_cast<size_t>(P) && p.work_sets >= sets) return WR_OK;
   p.work_kind = 0;
   auto lay = [&](Arena& a, Pipe* dst) {
@@ -795,6 +833,7 @@ int ensure_work(Pipe& p, int kind, int P, int sets) {
   p.work_kind = kind;
   p.work_key = P;
   p.work_sets = sets;
+  p.work_pool = bdpt_pool_scale();
   return WR_OK;
 }
 
@@ -1037,7 +1076,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     }
     if (late_prev) {  // + the previous step's deferred hard rays, beside the search
       const int lblocks = late_gn * (kLateTieBlocks + kLateScanBlocks);
-      auto kf = count ? trace_fast_kernel<true, true>(F.wide) : trace_fast_kernel<false, true>(F.wide);
+      auto kf = count ? trace_fast_kernel<true, true>(F.wide, F.sph) : trace_fast_kernel<false, true>(F.wide, F.sph);
       hipLaunchKernelGGL(kf, dim3(lblocks + fgrid),
                          dim3(kTraceBlock), std::max(slds, lds), stream, c->ds, F, Q, ctr, fetch, ts.t2, ts.spill,
                          *late_prev, lblocks, late_gn, kLateTieBlocks, kLateLaneBlocks, kLateTieBlocks);
@@ -1045,7 +1084,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
         hipLaunchKernelGGL(k_late_verify, dim3(64, late_gn), dim3(kTraceBlock), lds, stream, c->ds, F, *late_prev,
                            ctr);
     } else {
-      auto kf = count ? trace_fast_kernel<true, false>(F.wide) : trace_fast_kernel<false, false>(F.wide);
+      auto kf = count ? trace_fast_kernel<true, false>(F.wide, F.sph) : trace_fast_kernel<false, false>(F.wide, F.sph);
       hipLaunchKernelGGL(kf, dim3(fgrid),
                          dim3(kTraceBlock), slds, stream, c->ds, F, Q, ctr, fetch, ts.t2, ts.spill, LateArgs{}, 0,
                          1, 0, 0, 0);
@@ -1218,7 +1257,13 @@ double host_now() {
 // Start a render on `n` pipelines: they wait for the context stream's set-up
 // (film clear) and clear their counters.
 void begin_render(wr_context* c, int n, const int time_kernels) {
-  c->timing = time_kernels != 0;
+  // diagnostics: WR_TIME_KERNELS=0 drops the per-launch events of a timed call
+  // (what the events themselves cost)
+  static const bool no_events = [] {
+    const char* e = std::getenv("WR_TIME_KERNELS");
+    return e && std::atoi(e) == 0;
+  }();
+  c->timing = time_kernels != 0 && !no_events;
   // a device film may still be written by the caller's work on the legacy
   // null stream (e.g. torch's default stream zeroing it): the render's streams
   // are non-blocking, so order them after that work explicitly.  The null
@@ -1239,22 +1284,30 @@ void begin_render(wr_context* c, int n, const int time_kernels) {
 // Join the pipelines into the context stream, wait, and add up the work
 // counters and (time_kernels) the per-launch durations of every pipeline.
 // stats->trace_wall_ms is the union of all traversal launch intervals.
-int finish_render(wr_context* c, int n, wr_stats* st, double t0_host) {
+int finish_render(wr_context* c, int n, wr_stats* st, double t0_host, unsigned long long* overflow = nullptr) {
   const double t_issued = host_now();
   for (int i = 0; i < n; ++i) {
     (void)hipEventRecord(c->pipes[i].done, c->pipes[i].stream);
     (void)hipStreamWaitEvent(c->stream, c->pipes[i].done, 0);
   }
+  // every pipeline's counters to pinned host memory behind the render, one
+  // synchronisation (16 synchronous copies took ~0.3 ms of a 60 ms render)
+  if (!c->host_ctr) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->host_ctr), kMaxPipes * sizeof(DevCounters), 0));
+  for (int i = 0; i < n; ++i)
+    HIPCHK(hipMemcpyAsync(&c->host_ctr[i], c->pipes[i].ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (std::getenv("WR_ISSUE_LOG"))  // diagnostics: host issue time vs the render's
     std::fprintf(stderr, "[wr issue] %d pipelines: issued in %.3f ms, done at %.3f ms\n", n,
                  (t_issued - t0_host) * 1e3, (host_now() - t0_host) * 1e3);
   HIPCHK(hipGetLastError());
+  if (overflow) {  // (read whether or not stats are wanted)
+    *overflow = 0;
+    for (int i = 0; i < n; ++i) *overflow += c->host_ctr[i].overflow;
+  }
   if (!st) return WR_OK;
   DevCounters sum{};
   for (int i = 0; i < n; ++i) {
-    DevCounters h;
-    HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
+    const DevCounters& h = c->host_ctr[i];
     sum.closest += h.closest;
     sum.shadow += h.shadow;
     sum.inner += h.inner;
@@ -1829,6 +1882,9 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       }
       fs.lo = v3(lo[0], lo[1], lo[2]);
       fs.hi = v3(hi[0], hi[1], hi[2]);
+      fs.sph = fh.spheres > 0 ? 1 : 0;
+      fs.org_lo = v3(fh.org_lo[0], fh.org_lo[1], fh.org_lo[2]);
+      fs.org_hi = v3(fh.org_hi[0], fh.org_hi[1], fh.org_hi[2]);
       // the search's stack holds BVH entries only; the hard rays' kernel walks
       // both trees
       fs.wide = wide;
@@ -1852,15 +1908,15 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       if (const char* e = std::getenv("WR_WALK_WAVE")) fs.walk_wave = fs.walk_wave && std::atoi(e) != 0;
       c->fast_ok = true;
       int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_fast_kernel<false, false>(wide), kTraceBlock,
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_fast_kernel<false, false>(wide, fs.sph), kTraceBlock,
                                                        search_lds_bytes(fs.sdepth, wide)) != hipSuccess ||
           per_cu <= 0)
         per_cu = 8;
       // diagnostic: WR_FAST_WAVES_PER_CU caps the search's resident waves
       if (const char* e = std::getenv("WR_FAST_WAVES_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
       c->fast_blocks = c->cus * per_cu;
-      // the verified BVH is the default traversal of triangle scenes (same
-      // answers as the KD walk); WR_TRACE_BVH=0 selects the walk
+      // the verified BVH is the default traversal (same answers as the KD
+      // walk); WR_TRACE_BVH=0 selects the walk
       c->fast_on = true;
       if (const char* e = std::getenv("WR_TRACE_BVH")) c->fast_on = std::atoi(e) != 0;
       if (const char* e = std::getenv("WR_BVH_DIAG")) fs.diag = std::atoi(e);
@@ -1876,7 +1932,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
 
 int wr_set_trace_mode(wr_context* c, int mode) {
   if (!c || (mode != WR_TRACE_REFERENCE && mode != WR_TRACE_BVH)) return fail(WR_E_ARG, "bad trace mode");
-  if (mode == WR_TRACE_BVH && !c->fast_ok) return fail(WR_E_SCENE, "the BVH mode covers triangle scenes only");
+  if (mode == WR_TRACE_BVH && !c->fast_ok) return fail(WR_E_SCENE, "the scene has no verified BVH (empty, or too large)");
   c->fast_on = mode == WR_TRACE_BVH;
   for (wr_context* d : c->subs) d->fast_on = c->fast_on;
   return WR_OK;
@@ -1913,6 +1969,8 @@ void wr_destroy(wr_context* c) {
   if (c->t_ref) (void)hipEventDestroy(c->t_ref);
   if (c->t_null) (void)hipEventDestroy(c->t_null);
   if (c->film_tmp) (void)hipFree(c->film_tmp);
+  if (c->film_bak) (void)hipFree(c->film_bak);
+  if (c->host_ctr) (void)hipHostFree(c->host_ctr);
   if (c->api_tmp) (void)hipFree(c->api_tmp);
   if (c->api_t2) (void)hipFree(c->api_t2);
   if (c->api_spill) (void)hipFree(c->api_spill);
@@ -2116,7 +2174,9 @@ static int issue_round(wr_context* c, int live, int nsteps, Fn&& fn, int np) {
 // Deferred hard rays on np pipelines: env WR_DEFER=1 only.
 static bool defer_enabled(const wr_context* c, int np) {
   (void)np;
-  return c->defer > 0;  // off by default: measured slower (deferred hard rays)
+  // off by default: measured slower (deferred hard rays); not
+  // built for trees with spheres (no LATE search variant with spheres)
+  return c->defer > 0 && !c->fs.sph;
 }
 
 // late-list records per group member and step parity (ties + scans) for pieces of `cap` paths
@@ -2199,7 +2259,26 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   float* dfilm = nullptr;
   const size_t nf = size_t(P) * 3;
   if (int rc = film_target(c, film, film_on_device, nf, &dfilm)) return rc;
-  begin_render(c, np, prm->time_kernels);
+  // vertex pools and shadow queues sized by use (BdptBuf): a render that fills
+  // one is redone from the film as it was before it.  A caller's device film is
+  // copied first (after the caller's work on the null stream, before any
+  // pipeline starts: begin_render orders them after the context stream); a
+  // host film's device copy starts at zero
+  const bool pooled = c->pipes[0].bb[0].vidx != nullptr;
+  if (pooled && film_on_device) {
+    if (c->film_bak_n < nf) {
+      if (c->film_bak) (void)hipFree(c->film_bak);
+  if (c->host_ctr) (void)hipHostFree(c->host_ctr);
+      c->film_bak = nullptr;
+      c->film_bak_n = 0;
+      HIPCHK(hipMalloc(&c->film_bak, nf * sizeof(float)));
+      c->film_bak_n = nf;
+    }
+    (void)hipEventRecord(c->t_null, nullptr);
+    (void)hipStreamWaitEvent(c->stream, c->t_null, 0);
+    HIPCHK(hipMemcpyAsync(c->film_bak, dfilm, nf * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+  }
+  const wr_stats st0 = st ? *st : wr_stats{};
   BdptArgs A0;
   A0.S = c->ds;
   A0.film = dfilm;
@@ -2259,7 +2338,8 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
     for (int m = 0; m < gn; ++m) {
       const BdptBuf& B = pp.bb[m];
       const BdptBuf::Sq& Q = B.sq[slot & 1];
-      ql.add(rq(Q.o, Q.d, B.cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut), A[m].n * (kVMax + 2));
+      ql.add(rq(Q.o, Q.d, B.cap_sq, &pp.sc[m].sq[slot], Q.t, Q.prim, nullptr, nullptr, Q.cut),
+             std::min(A[m].n * (kVMax + 2), B.cap_sq));
       if (light || more)
         ql.add(rq(B.q_o[b & 1], B.q_d[b & 1], B.qs, &pp.sc[m].ext[b], B.q_t[b & 1], B.q_prim[b & 1], nullptr, nullptr,
                   nullptr, nullptr, nullptr, 0, &pp.sc[m].ext[slot]),
@@ -2269,7 +2349,7 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
                  gn);
     LateArgs L{};
     if (light) hipLaunchKernelGGL(k_light_shade, dim3(g, gn), dim3(kShadeBlock), 0, sm, G.GA, b, L, 0);
-    const int nres = shade_grid(c, G.nmax * (kVMax + 2));
+    const int nres = shade_grid(c, std::min(G.nmax * (kVMax + 2), pp.bb[0].cap_sq));
     hipLaunchKernelGGL(k_camera_step, dim3(nres + (more ? g : 0), gn), dim3(kShadeBlock), 0, sm, G.GA, slot, nres,
                        more ? 1 : 0, L, 0);
     tm.mark(WR_K_SHADE);
@@ -2307,7 +2387,7 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
       return true;
     };
     const int lg = std::max(1, std::min(shade_grid(c, G.nmax), 32));  // late-vertex blocks per member
-    const int sq_max = G.nmax * (kVMax + 2);  // <= cap_sq
+    const int sq_max = std::min(G.nmax * (kVMax + 2), pp.bb[0].cap_sq);
     const int g = shade_grid(c, G.nmax);
     if (step == 0) {
       HIPCHK(hipMemsetAsync(pp.sc, 0, gn * sizeof(StepCounters), sm));
@@ -2345,7 +2425,7 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
       LateArgs L{};
       const bool lp = late_of(slot, L);
       QueueList ql;
-      for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), A[m].n * (kVMax + 2));
+      for (int m = 0; m < gn; ++m) ql.add(sq(m, slot), std::min(A[m].n * (kVMax + 2), pp.bb[m].cap_sq));
       if (more)
         for (int m = 0; m < gn; ++m) ql.add(ext(m, slot, bit), A[m].n);
       trace_launch(c, sm, pp.ctr, tslot(pp, slot), tm, count, ql.Q, ql.max_rays, WR_BDPT_TRACE_MODE, false,
@@ -2364,14 +2444,18 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   // step across the pipelines: each stream runs its own in order, and all of
   // them get their first launches at once instead of one pipeline's ~90
   // launches after another's (host issue time: ~2 us per call)
-  std::vector<GroupIssue> round(np);
-  for (int r = 0; r < plan.max_groups(); ++r) {
+  unsigned long long overflow = 0;
+  auto run = [&](const PiecePlan& pl) -> int {
+  const int npl = pl.pipes();
+  begin_render(c, npl, prm->time_kernels);
+  std::vector<GroupIssue> round(npl);
+  for (int r = 0; r < pl.max_groups(); ++r) {
     int live = 0;
-    for (int pi = 0; pi < np; ++pi) {
+    for (int pi = 0; pi < npl; ++pi) {
       GroupIssue& G = round[pi];
       G.gn = 0;
-      if (r >= static_cast<int>(plan.per_pipe[pi].size())) continue;
-      const std::vector<Piece>& grp = plan.per_pipe[pi][r];
+      if (r >= static_cast<int>(pl.per_pipe[pi].size())) continue;
+      const std::vector<Piece>& grp = pl.per_pipe[pi][r];
       G.pp = &c->pipes[pi];
       G.gn = static_cast<int>(grp.size());
       G.nmax = 0;
@@ -2392,14 +2476,39 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
     if (!live) continue;
     if (int rc = issue_round(c, live, nsteps, [&](int pi, int step) {
           return round[pi].gn > 0 ? issue(round[pi], step) : WR_OK;
-        }, np))
+        }, npl))
       return rc;
   }
   HIPCHK(hipGetLastError());
   if (std::getenv("WR_ISSUE_LOG"))
     std::fprintf(stderr, "[wr issue] kernel args: BdptGroup %zu B, TraceQueues %zu B, DevScene %zu B, FastScene %zu B\n",
                  sizeof(BdptGroup), sizeof(TraceQueues), sizeof(DevScene), sizeof(c->fs));
-  if (int rc = finish_render(c, np, st, t0)) return rc;
+  return finish_render(c, npl, st, t0, &overflow);
+  };
+  if (int rc = run(plan)) return rc;
+  if (overflow) {
+    // A vertex pool or shadow queue filled up and appends were dropped: redo
+    // the render from the film as it was, with pieces whose worst case fits
+    // every pool (<= 11 shadow rays per path and step, 9 light and 4 camera
+    // vertices per path), in the untiled camera order (64-path units; the
+    // path <-> pixel map is the same), so the film is the one of an unbounded
+    // render.  Rare: the pools hold several times what the reference scenes use.
+    const BdptBuf& B = c->pipes[0].bb[0];
+    const int safe = std::min({B.cap_sq / (kVMax + 2), B.vcap / kVMax, B.ccap / kCvMax, cap}) / 64 * 64;
+    if (safe < 64) return fail(WR_E_HIP, "BDPT pools too small for a 64-path piece");
+    if (film_on_device) HIPCHK(hipMemcpyAsync(dfilm, c->film_bak, nf * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+    else HIPCHK(hipMemsetAsync(dfilm, 0, nf * sizeof(float), c->stream));
+    if (st) *st = st0;
+    A0.untiled = 1;
+    overflow = 0;
+    if (int rc = run(plan_pieces(f_lo, f_hi, P, 64, safe, fit, c->piece_min))) return rc;
+    if (overflow) return fail(WR_E_HIP, "BDPT pools overflowed with pieces the worst case fits");
+    if (st) st->redone += 1;
+  }
+  if (st) {
+    for (int i = 0; i < np; ++i) st->work_bytes += static_cast<int64_t>(c->pipes[i].work.cap);
+    st->work_paths += static_cast<int64_t>(np) * kGroup * cap;
+  }
   return film_return(c, film, film_on_device, nf);
 }
 
@@ -2729,6 +2838,9 @@ static void add_stats(wr_stats* d, const wr_stats& s) {
   d->pipelines = std::max(d->pipelines, s.pipelines);
   d->deferred_rays += s.deferred_rays;
   d->bvh_width = std::max(d->bvh_width, s.bvh_width);
+  d->work_bytes += s.work_bytes;
+  d->work_paths += s.work_paths;
+  d->redone += s.redone;
 }
 
 static int ensure_dev_film(wr_context* d, float** buf, size_t* have, size_t nf) {

@@ -430,7 +430,8 @@ __device__ __forceinline__ void trace_queue(const DevScene& S, const TraceQueues
     int acc = 0;
 #pragma unroll
     for (int i = 0; i < kMaxQueues; ++i) {
-      if (i < Q.n && Q.q[i].count) acc += *Q.q[i].count + (Q.q[i].count2 ? *Q.q[i].count2 : 0);
+      // (capped: a shadow queue's appends past its capacity were dropped, BdptBuf)
+      if (i < Q.n && Q.q[i].count) acc += min(*Q.q[i].count + (Q.q[i].count2 ? *Q.q[i].count2 : 0), Q.q[i].cap);
       qend[i] = acc;
     }
   }

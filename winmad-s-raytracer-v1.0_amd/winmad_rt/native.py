@@ -87,7 +87,8 @@ class WrStats(C.Structure):
                 ("prim_tests", C.c_int64), ("bvh_nodes", C.c_int64), ("bvh_tests", C.c_int64),
                 ("kd_replay_steps", C.c_int64), ("fallback_rays", C.c_int64), ("verify_rays", C.c_int64),
                 ("verify_mismatches", C.c_int64), ("pipelines", C.c_int64),
-                ("deferred_rays", C.c_int64), ("bvh_width", C.c_int64)]
+                ("deferred_rays", C.c_int64), ("bvh_width", C.c_int64), ("work_bytes", C.c_int64),
+                ("work_paths", C.c_int64), ("redone", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
@@ -188,6 +189,17 @@ def lib():
         L.wr_last_error.restype = C.c_char_p
         _lib = L
     return _lib
+
+
+def library_sha16():
+    """sha256 prefix (16 hex digits) of the library file this process loads:
+    ties a measurement (profiles/*/traffic_*.json, lib_sha) to a build."""
+    import hashlib
+    try:
+        with open(LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
 
 
 def check(rc):
