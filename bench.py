@@ -192,6 +192,8 @@ CONFIGS = {
            "steps": 64},
     "c4": {"desc": "1M-triangle synthetic torus BDPT", "integrator": "bdpt", "steps": 64},
     "vcm": {"desc": "torus.scene VertexCM", "integrator": "vcm", "steps": 256},
+    # not a BASELINE config: the Sphere::hit path (Cornell box, glass / mirror / glossy spheres)
+    "sph": {"desc": "Cornell box + three spheres BDPT", "integrator": "bdpt", "steps": 64},
 }
 METRIC = "Mrays/sec + spp/sec at 1920x1080, torus.scene BDPT, 1/2/4/8 MI355X"
 
@@ -202,6 +204,8 @@ def make_scene(cfg, W, H, tmp, obj=None):
         return scenes.write(os.path.join(tmp, "torus.scene"), scenes.torus_scene(W, H))
     if cfg == "c3":
         return scenes.write(os.path.join(tmp, "cbox.scene"), scenes.cbox_scene(W, H))
+    if cfg == "sph":
+        return scenes.write(os.path.join(tmp, "spheres.scene"), scenes.spheres_scene(W, H))
     obj = obj or os.path.join(tmp, "torus_1m.obj")
     if not os.path.exists(obj):
         scenes.synth_torus_obj(obj)
@@ -217,7 +221,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
-                    help="c2 (default, the BASELINE metric), c3 PT, c4 1M triangles, vcm VertexCM")
+                    help="c2 (default, the BASELINE metric), c3 PT, c4 1M triangles, vcm VertexCM, sph spheres")
     ap.add_argument("--spp", type=int, default=512, help="c3: stratification grid of the PT render")
     ap.add_argument("--cpu-paths", type=int, default=1000000)
     ap.add_argument("--no-cpu", action="store_true")
@@ -424,7 +428,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_reference(args.config, cfg["integrator"], W, H, tmp, 4 if args.config == "c4" else 2)
         budget = {"c2": args.cpu_paths, "c3": args.cpu_paths // 4, "c4": args.cpu_paths // 20,
-                  "vcm": args.cpu_paths // 2}[args.config]
+                  "vcm": args.cpu_paths // 2, "sph": args.cpu_paths // 4}[args.config]
         port = cpu_baseline(cfg["integrator"], scene_path, W, H, budget)
         if cpu is None:  # no reference build on this machine: the port is the baseline
             cpu, port = port, None
