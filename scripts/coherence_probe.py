@@ -7,7 +7,8 @@ reports k_trace_fast's kernel duration per order from a rocprofv3 kernel trace
 Ray sets (torus.scene, BDPT camera): primaries in raster order, and secondary
 rays leaving the primaries' hit points in uniformly random directions.  Orders:
 raster (path index), shuffled, Morton code of the origin, direction octant then
-Morton code.
+Morton code, and orders an append-time binning could give (octant, sign of x,
+octant within blocks of consecutive rays).
 """
 import csv
 import glob
@@ -30,6 +31,12 @@ def morton(p, lo, hi, bits=10):
         for a in range(3):
             key |= ((q[:, a] >> b) & 1) << (3 * b + a)
     return key
+
+
+def local_order(key, block):
+    """Stable sort by `key` within each block of `block` consecutive rays."""
+    i = np.arange(len(key))
+    return np.lexsort((i, key, i // block))
 
 
 def run():
@@ -76,6 +83,13 @@ def run():
         ("secondary morton", sec[np.argsort(m, kind="stable")]),
         ("secondary octant+morton", sec[np.argsort(octant << 40 | m, kind="stable")]),
         ("secondary dir-morton", sec[np.argsort(morton(sd, -1, 1, 6), kind="stable")]),
+        # what an append-time binning could give without a sort pass: the
+        # octant alone (8 segments), the sign of x (both ends of one queue),
+        # and octant bins within blocks of 64 / 4,096 consecutive rays
+        ("secondary octant", sec[np.argsort(octant, kind="stable")]),
+        ("secondary x-sign", sec[np.argsort(octant & 1, kind="stable")]),
+        ("secondary octant/64", sec[local_order(octant, 64)]),
+        ("secondary octant/4096", sec[local_order(octant, 4096)]),
     ]
     names = []
     for name, r in sets:

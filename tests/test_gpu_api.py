@@ -191,9 +191,9 @@ def test_reference_main_with_the_mirror_runs_at_the_bench_rate(tmp_path):
     reference's main() with the three integrator branches swapped for the
     winmad:: mirror, nothing else) at the headline configuration, 1920x1080
     torus.scene BDPT, 256 iterations, in a fresh process with the box's own
-    environment: the library's load-time queue set-up and default traversal
-    must give it bench.py's rate (verdict r3: within 10 %; asserted at 20 %
-    against run-to-run noise, both rates printed)."""
+    environment: its wr_request_hw_queues(16) and the library's default
+    traversal must give it bench.py's rate (verdict r3: within 10 %; asserted
+    at 20 % against run-to-run noise, both rates printed)."""
     import json
     import re
     import sys
@@ -217,7 +217,7 @@ def test_reference_main_with_the_mirror_runs_at_the_bench_rate(tmp_path):
     bench_pipes = json.loads([ln for ln in b.stdout.splitlines() if ln.startswith("{")][-1])["config"]["pipelines"]
     print(f"example_main {main_rate:.1f} Mrays/s ({pipes} pipelines) vs bench.py {bench_rate:.1f} "
           f"({bench_pipes} pipelines): {main_rate / bench_rate:.3f}")
-    # the library's load-time set-up gave the program bench.py's queues: the same
+    # wr_request_hw_queues gave the program bench.py's queues: the same
     # pipeline count (16 on an idle GPU; fewer when this test process still
     # holds device memory, as both size their pipelines by the free memory)
     assert pipes == bench_pipes, (pipes, bench_pipes)
