@@ -1273,10 +1273,39 @@ __device__ __forceinline__ bool tri_grazes(float4 a, float4 b, float f, V3 o, V3
   return fabsf(den) <= kGrazeRel * mag && fabsf(tnum) <= kGrazePlaneRel * tmag;
 }
 
-template <bool COUNT, int W, bool SPH>
+// one atomic per wave: this lane's slot in a list (or -1 if !want)
+__device__ __forceinline__ int fast_append(int* counter, bool want) {
+  const unsigned long long m = __ballot(want);
+  if (m == 0ull) return -1;
+  const int lane = __lane_id();
+  const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader);
+  return want ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+// The resolve's first membership test (resolve_fast): is one of the first
+// four KD leaf cells of the winner p1 (its PrimRec) crossed by the ray within
+// the witness margin?  Then the reference's walk visits a leaf holding p1.
+__device__ __forceinline__ bool first_cells_crossed(const FastScene& F, int p1, V3 o, V3 d, V3 binv, float rtmax) {
+  const float4* pr = F.prim_rec + 8 * static_cast<size_t>(p1);
+  const float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3], c4 = pr[4], c5 = pr[5];
+  return box_crossed_with_margin(c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, o, d, binv, rtmax) ||
+         box_crossed_with_margin(c1.z, c1.w, c2.x, c2.y, c2.z, c2.w, o, d, binv, rtmax) ||
+         box_crossed_with_margin(c3.x, c3.y, c3.z, c3.w, c4.x, c4.y, o, d, binv, rtmax) ||
+         box_crossed_with_margin(c4.z, c4.w, c5.x, c5.y, c5.z, c5.w, o, d, binv, rtmax);
+}
+
+// RL (the resolve list): a finished ray whose answer needs no more -- a miss,
+// or an unmarked winner that first_cells_crossed proves -- is settled here;
+// the others (near-ties, grazing rays, winners proven by neither of those
+// cells) are listed by launch index in rlist for k_fast_resolve, which then
+// reads those rays only.  The test is the resolve's own, on the same floats.
+template <bool COUNT, int W, bool SPH, bool RL = false>
 __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, int* fetch,
                                            float* t2buf, int2* spill, uint32_t* lds, FastCounters& ctr,
-                                           int bid, int nblk) {  // this block's index among the launch's nblk search blocks
+                                           int bid, int nblk,  // this block's index among the launch's nblk search blocks
+                                           int* rlist = nullptr, int* rlist_n = nullptr) {
   constexpr int kLdsStack = SearchStack<W>::lds;
   constexpr bool kSearchSpills = SearchStack<W>::spills;
   const int lane = __lane_id();
@@ -1309,6 +1338,19 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   int cur = 0;  // >= 0 inner node to visit; < 0 leaf link to test; kDone when finished
   int pl = 0;   // WR_BVH_SPEC: parked leaf link (< 0), or 0
   constexpr int kDone = 0x7fffffff;
+  // RL: the listed rays gather in a 64-entry LDS buffer behind the stack and go
+  // to rlist 64 at a time (one atomic per 64 listed rays, not per wave round)
+  int* const lbuf = reinterpret_cast<int*>(lds) + search_lds_bytes(F.sdepth, W) / 4;
+  int nlb = 0;
+  bool listed = false;
+  auto flush_list = [&]() {
+    if (nlb == 0) return;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(rlist_n, nlb);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (lane < nlb) rlist[base + lane] = lbuf[lane];
+    nlb = 0;
+  };
   auto reserve = [&](bool want) -> int {
     const unsigned long long m = __ballot(want);
     const int need = __popcll(m);
@@ -1643,25 +1685,28 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
       if (gz) po = po >= 0 ? (po | kGrazeMark) : kGrazeMiss;
       qfield(Q, qi, [](const RayQueue& x) { return x.out_t; })[r] = p1 >= 0 ? t1 : WR_INF;
       qfield(Q, qi, [](const RayQueue& x) { return x.out_prim; })[r] = po;
+      if constexpr (RL) {
+        listed = po != p1;  // marked: a near-tie or a grazing ray
+        if (!listed && p1 >= 0) listed = !first_cells_crossed(F, p1, o, d, binv, rtmax);
+      }
       r = -1;
     }
+    if constexpr (RL) {  // (wave-uniform) the listed rays into the wave's buffer
+      const unsigned long long m = __ballot(listed);
+      if (m) {
+        const int k = __popcll(m);
+        if (nlb + k > 64) flush_list();
+        if (listed) lbuf[nlb + __popcll(m & ((1ull << lane) - 1ull))] = lidx;
+        nlb += k;
+        listed = false;
+      }
+    }
   }
+  if constexpr (RL) flush_list();
 }
 
 // tie-list entries: launch index, | kWalkEntry for a ray the KD walk settles
 constexpr int kWalkEntry = 1 << 30;
-// one atomic per wave: this lane's slot in a list (or -1 if !want)
-__device__ __forceinline__ int fast_append(int* counter, bool want) {
-  const unsigned long long m = __ballot(want);
-  if (m == 0ull) return -1;
-  const int lane = __lane_id();
-  const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
-  int base = 0;
-  if (lane == leader) base = atomicAdd(counter, __popcll(m));
-  base = __shfl(base, leader);
-  return want ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
-}
-
 // k_fast_resolve: one ray per lane (grid-stride over the launch's indices).
 // The rare rays it cannot settle (near-ties, t1 not reached) go to `hard` for
 // k_fast_hard, so that their register-hungry code does not lower this
@@ -1669,13 +1714,27 @@ __device__ __forceinline__ int fast_append(int* counter, bool want) {
 template <bool COUNT>
 __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
                                              const float* t2buf, int* hard, int* hard_n, int hcap,
-                                             FastCounters& ctr) {
+                                             FastCounters& ctr, const int* rlist = nullptr,
+                                             const int* rlist_n = nullptr) {
   const int lane = __lane_id();
   const QueueIndex QI(Q);
-  if (F.diag & 16) return;
+  // the search's list (RL), or every ray of the launch
+  const int nr = rlist ? min(*rlist_n, QI.n) : QI.n;
+  // the capacity diagnostics (wrong answers, never valid indices): the rays a
+  // skipped kernel would settle keep the search's winner, its marks cleared
+  // (a marked primitive would index past the scene in the vertex kernels)
+  if (F.diag & 16) {
+    for (int idx = blockIdx.x * 64 + lane; idx < QI.n; idx += gridDim.x * 64) {
+      int q = 0, r = 0;
+      QI.locate(idx, q, r);
+      int* op = qfield(Q, q, [](const RayQueue& x) { return x.out_prim; });
+      op[r] = unmark(op[r]);
+    }
+    return;
+  }
   // every lane of the wave takes part in each list append (whole iterations)
-  for (int base = blockIdx.x * 64; base < QI.n; base += gridDim.x * 64) {
-    const int idx = base + lane;
+  for (int base = blockIdx.x * 64; base < nr; base += gridDim.x * 64) {
+    const int idx = base + lane < nr ? (rlist ? rlist[base + lane] : base + lane) : QI.n;
     bool need = false, scan = false, big_tie = false, walk = false;
     int q = 0, r = 0, p1 = -1;
     float t1 = WR_INF;
@@ -1770,6 +1829,10 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
           }
         }
       }
+    }
+    if ((need && (F.diag & (32 | 128))) || (scan && (F.diag & (32 | 64)))) {  // (diagnostics, as above)
+      qfield(Q, q, [](const RayQueue& x) { return x.out_prim; })[r] = p1;
+      need = scan = false;
     }
     const int slot = fast_append(hard_n, need);
     if (need) hard[slot] = walk ? (idx | kWalkEntry) : idx;

@@ -130,12 +130,14 @@ struct StepCounters {
   int vcm_nverts;     // VCM: light vertices in the merge grid
   int mq[kSlots];     // VCM: merge queries queued at step `slot`
   int hard[kSlots][2];  // WR_TRACE_BVH: rays of step `slot` left to k_fast_hard (tie list, scan list)
+  int rlist[kSlots];    // WR_TRACE_BVH: rays of step `slot` the search left to k_fast_resolve
   int late[kSlots][2];  // WR_TRACE_BVH: rays of step `slot` deferred (late list: ties, scans)
   int vpool, cpool;     // BDPT, overlapped: records taken from the light / camera vertex pools
 };
 struct DevCounters {
   int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
   int hard[2];  // API path: rays left to k_fast_hard (tie list, scan list)
+  int rlist;    // API path: rays the search left to k_fast_resolve
   unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
   unsigned long long closest, shadow, inner, leaves, refs, tests;
   unsigned long long vm_queries, vm_found, vm_merged;  // VCM range queries / vertices in radius / merges
@@ -276,11 +278,13 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
 #endif
 // SPH: the tree holds spheres (FastScene::sph) -- a variant of its own, so
 // that the triangle scenes' search keeps its registers
-template <bool COUNT, bool LATE, int W, bool SPH>
+// RL: the search settles the rays whose winner's membership its first leaf
+// cells prove (the resolve's first test) and lists the rest for k_fast_resolve
+template <bool COUNT, bool LATE, int W, bool SPH, bool RL = false>
 __global__ void __launch_bounds__(kTraceBlock)
 __attribute__((amdgpu_waves_per_eu(W == 4 && !LATE ? WR_FAST4_WAVES : WR_FAST_WAVES, 8))) WR_NO_PK_FP32
 k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* spill,
-             LateArgs L, int lblocks, int gn, int hblocks, int lane_blocks, int wave_max) {
+             LateArgs L, int lblocks, int gn, int hblocks, int lane_blocks, int wave_max, int* rlist, int* rlist_n) {
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
   const int b = static_cast<int>(blockIdx.x);
@@ -292,22 +296,27 @@ k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetc
       atomicAdd(&ctr->deferred, static_cast<unsigned long long>(min(L.n[m][0], half) + min(L.n[m][1], half)));
     }
   } else {
-    trace_fast<COUNT, W, SPH>(S, F, Q, fetch, t2buf, spill, smem, fc, b - (LATE ? lblocks : 0),
-                         static_cast<int>(gridDim.x) - (LATE ? lblocks : 0));
+    trace_fast<COUNT, W, SPH, RL>(S, F, Q, fetch, t2buf, spill, smem, fc, b - (LATE ? lblocks : 0),
+                                  static_cast<int>(gridDim.x) - (LATE ? lblocks : 0), rlist, rlist_n);
   }
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 // the search kernel for a tree width (instantiated for 2 and 4; 8 when the
 // library is built with WR_BVH_WIDE=8)
+// RL: the search's per-wave buffer of listed rays (trace_fast)
+constexpr size_t kRlistLds = 64 * sizeof(int);
 using TraceFastKernel = void (*)(DevScene, FastScene, TraceQueues, DevCounters*, int*, float*, int2*, LateArgs, int, int,
-                                 int, int, int);
+                                 int, int, int, int*, int*);
 template <bool COUNT, bool LATE>
-TraceFastKernel trace_fast_kernel(int wide, bool sph = false) {
+TraceFastKernel trace_fast_kernel(int wide, bool sph = false, bool rl = false) {
 #if WR_BVH_WIDE == 8
   if (wide == 8) return k_trace_fast<COUNT, LATE, 8, false>;  // (triangle scenes: the 8-wide tree is a build option)
 #endif
   // (the deferred-hard-ray variants, LATE, are not built with spheres: defer_enabled)
   if (sph && !LATE) return wide == 4 ? k_trace_fast<COUNT, false, 4, true> : k_trace_fast<COUNT, false, 2, true>;
+  // (the resolve list: triangle trees, no late lists)
+  if (rl && !LATE)
+    return wide == 4 ? k_trace_fast<COUNT, false, 4, false, true> : k_trace_fast<COUNT, false, 2, false, true>;
   return wide == 4 ? k_trace_fast<COUNT, LATE, 4, false> : k_trace_fast<COUNT, LATE, 2, false>;
 }
 #ifndef WR_RESOLVE_WAVES
@@ -321,9 +330,9 @@ TraceFastKernel trace_fast_kernel(int wide, bool sph = false) {
 template <bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32 WR_RESOLVE_OCC
 k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const float* t2buf, int* hard, int* hard_n,
-               int hcap) {
+               int hcap, const int* rlist, const int* rlist_n) {
   FastCounters fc{};
-  resolve_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, hcap, fc);
+  resolve_fast<COUNT>(S, F, Q, t2buf, hard, hard_n, hcap, fc, rlist, rlist_n);
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
 // WR_HARD_WAVES: register budget of k_fast_hard as waves per SIMD (0: the
@@ -595,6 +604,7 @@ struct wr_context {
   bool fast_on = false;   // WR_TRACE_BVH mode selected
   int fast_blocks = 4096; // resident one-wave workgroups of k_trace_fast
   int resolve_blocks = 0; // k_fast_resolve's one-wave workgroups (0: fast_blocks; env WR_RESOLVE_GRID per CU)
+  bool resolve_list = true;  // the search lists the rays the resolve must see (env WR_RESOLVE_LIST=0: all rays)
   bool verify = false;      // WR_BVH_VERIFY=1: every BVH answer checked against the KD walk
   // BDPT hard rays off the critical path (env WR_DEFER=1; off by default)
   int defer = -1;
@@ -970,9 +980,10 @@ struct TraceSlot {
   size_t t2_cap;
   int* hard_n;
   int2* spill;    // the search stack's spill area
+  int* rlist_n;   // rays the search left to k_fast_resolve (their list: the t2 region)
 };
 TraceSlot tslot(Pipe& p, int slot) {
-  return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap, &p.sc[0].hard[slot][0], p.spill};
+  return TraceSlot{&p.sc[0].fetch[slot], p.t2buf, p.t2_cap, &p.sc[0].hard[slot][0], p.spill, &p.sc[0].rlist[slot]};
 }
 // t2 scratch + hard-ray list of a pipeline for launches of up to `rays` rays
 // search-stack spill entries per lane: the larger of the context's trees
@@ -1066,6 +1077,12 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     const int blocks = (max_rays + kTraceBlock - 1) / kTraceBlock;
     const int fgrid = std::max(1, std::min(c->fast_blocks, blocks));
     const size_t lds = fast_lds_bytes(c->fs.depth), slds = search_lds_bytes(F.sdepth, F.wide);
+    // the search settles the rays its first membership test proves and lists
+    // the rest for the resolve (in the t2 region: t2 is kept by diagnostics only)
+    const bool rl = c->resolve_list && !F.diag && !late_prev && !F.sph && F.wide != 8;
+    int* rlist = rl ? reinterpret_cast<int*>(ts.t2) : nullptr;
+    int* rlist_n = rl ? ts.rlist_n : nullptr;
+    const size_t rlds = slds + (rl ? kRlistLds : 0);
     hipEvent_t f0 = nullptr, f1 = nullptr, fa = nullptr, fb = nullptr;
     if (c->trace_log) {
       (void)hipEventCreate(&f0);
@@ -1079,22 +1096,23 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
       auto kf = count ? trace_fast_kernel<true, true>(F.wide, F.sph) : trace_fast_kernel<false, true>(F.wide, F.sph);
       hipLaunchKernelGGL(kf, dim3(lblocks + fgrid),
                          dim3(kTraceBlock), std::max(slds, lds), stream, c->ds, F, Q, ctr, fetch, ts.t2, ts.spill,
-                         *late_prev, lblocks, late_gn, kLateTieBlocks, kLateLaneBlocks, kLateTieBlocks);
+                         *late_prev, lblocks, late_gn, kLateTieBlocks, kLateLaneBlocks, kLateTieBlocks, nullptr, nullptr);
       if (c->verify)
         hipLaunchKernelGGL(k_late_verify, dim3(64, late_gn), dim3(kTraceBlock), lds, stream, c->ds, F, *late_prev,
                            ctr);
     } else {
-      auto kf = count ? trace_fast_kernel<true, false>(F.wide, F.sph) : trace_fast_kernel<false, false>(F.wide, F.sph);
+      auto kf = count ? trace_fast_kernel<true, false>(F.wide, F.sph, rl)
+                      : trace_fast_kernel<false, false>(F.wide, F.sph, rl);
       hipLaunchKernelGGL(kf, dim3(fgrid),
-                         dim3(kTraceBlock), slds, stream, c->ds, F, Q, ctr, fetch, ts.t2, ts.spill, LateArgs{}, 0,
-                         1, 0, 0, 0);
+                         dim3(kTraceBlock), rlds, stream, c->ds, F, Q, ctr, fetch, ts.t2, ts.spill, LateArgs{}, 0,
+                         1, 0, 0, 0, rlist, rlist_n);
     }
     if (c->trace_log) (void)hipEventRecord(fa, stream);
     int* hard = reinterpret_cast<int*>(ts.t2 + ts.t2_cap);
     hipLaunchKernelGGL(count ? k_fast_resolve<true> : k_fast_resolve<false>,
                        dim3(std::max(1, std::min(c->resolve_blocks > 0 ? c->resolve_blocks : c->fast_blocks, blocks))),
                        dim3(kTraceBlock), 0, stream, c->ds, F,
-                       Q, ctr, ts.t2, hard, ts.hard_n, static_cast<int>(ts.t2_cap));
+                       Q, ctr, ts.t2, hard, ts.hard_n, static_cast<int>(ts.t2_cap), rlist, rlist_n);
     if (c->trace_log) (void)hipEventRecord(fb, stream);
     // the hard rays are a few in 10^4: a small grid drains any count (one
     // ray per wave for the API calls: up to 2048 at once, 8 waves per CU)
@@ -1907,9 +1925,10 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                          : 0;
       if (const char* e = std::getenv("WR_WALK_WAVE")) fs.walk_wave = fs.walk_wave && std::atoi(e) != 0;
       c->fast_ok = true;
+      if (const char* e = std::getenv("WR_RESOLVE_LIST")) c->resolve_list = std::atoi(e) != 0;
       int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_fast_kernel<false, false>(wide, fs.sph), kTraceBlock,
-                                                       search_lds_bytes(fs.sdepth, wide)) != hipSuccess ||
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_fast_kernel<false, false>(wide, fs.sph, c->resolve_list), kTraceBlock,
+                                                       search_lds_bytes(fs.sdepth, wide) + (c->resolve_list ? kRlistLds : 0)) != hipSuccess ||
           per_cu <= 0)
         per_cu = 8;
       // diagnostic: WR_FAST_WAVES_PER_CU caps the search's resident waves
@@ -2043,7 +2062,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
   ql.add(rq(o3, d3, n, cnt, tt, pr, tmn, tmx, occ ? dcut : nullptr), n);
   if (c->fast_on && !c->api_spill && max_spill_entries(c) > 0)
     HIPCHK(hipMalloc(&c->api_spill, max_spill_entries(c) * size_t(c->fast_blocks) * 64 * sizeof(int2)));
-  const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard[0], c->api_spill};
+  const TraceSlot ts{&c->ctr->fetch, c->api_t2, c->api_t2_cap, &c->ctr->hard[0], c->api_spill, &c->ctr->rlist};
   trace_launch(c, c->stream, c->ctr, ts, tm, false, ql.Q, ql.max_rays,
                c->api_dense ? TRACE_DENSE : (occ != nullptr ? TRACE_CUT : TRACE_PLAIN), true);
   hipLaunchKernelGGL(k_api_finish, dim3(g), dim3(256), 0, c->stream, c->ds, o3, d3, tt, pr, dtg, n, dh,
@@ -2268,7 +2287,6 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   if (pooled && film_on_device) {
     if (c->film_bak_n < nf) {
       if (c->film_bak) (void)hipFree(c->film_bak);
-  if (c->host_ctr) (void)hipHostFree(c->host_ctr);
       c->film_bak = nullptr;
       c->film_bak_n = 0;
       HIPCHK(hipMalloc(&c->film_bak, nf * sizeof(float)));
