@@ -183,6 +183,40 @@ def test_bvh_bdpt_render_1m_triangles():
     assert _film_close(fa, fb)
 
 
+@pytest.mark.parametrize("kind", ["bdpt", "vcm", "pt"])
+def test_resolve_list_same_rays_and_film(kind, monkeypatch):
+    """The search settles the rays its first membership test proves and lists
+    the rest for k_fast_resolve (WR_RESOLVE_LIST, the default): the same rays
+    and film as the resolve over every ray."""
+    out = []
+    for rl in ("1", "0"):
+        monkeypatch.setenv("WR_RESOLVE_LIST", rl)
+        c = native.Context(native.Scene(_scenes.torus(192, 144) if kind != "pt" else _scenes.cbox(192, 144)), 0)
+        if kind == "bdpt":
+            out.append(c.render_bdpt(192, 144, iterations=4, seed=13))
+        elif kind == "vcm":
+            out.append(c.render_vcm(192, 144, iterations=2, seed=13))
+        else:
+            out.append(c.render_path(192, 144, spp=4, max_depth=7, seed=13))
+        c.close()
+    (fa, sa), (fb, sb) = out
+    assert sa.closest_rays == sb.closest_rays and sa.shadow_rays == sb.shadow_rays
+    assert _film_close(fa, fb)
+
+
+@pytest.mark.parametrize("diag", [16, 32, 48, 64, 128])
+def test_capacity_diagnostics_keep_primitive_indices_valid(diag, monkeypatch):
+    """WR_BVH_DIAG's capacity probes skip the resolve or the hard launch (wrong
+    answers, measurement only): the rays those kernels would settle keep the
+    search's winner with its marks cleared, so a render completes (a marked
+    primitive index used to reach the vertex kernels)."""
+    monkeypatch.setenv("WR_BVH_DIAG", str(diag))
+    c = native.Context(native.Scene(_scenes.torus(128, 96)), 0)
+    film, st = c.render_bdpt(128, 96, iterations=2, seed=3)
+    c.close()
+    assert np.isfinite(film).all() and st.closest_rays > 0
+
+
 @pytest.mark.parametrize("name,maker,kind", [("torus", lambda: _scenes.torus(256, 256), "bdpt"),
                                              ("torus_vcm", lambda: _scenes.torus(256, 256), "vcm"),
                                              ("cbox", lambda: _scenes.cbox(256, 192), "pt"),

@@ -1078,8 +1078,10 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     const int fgrid = std::max(1, std::min(c->fast_blocks, blocks));
     const size_t lds = fast_lds_bytes(c->fs.depth), slds = search_lds_bytes(F.sdepth, F.wide);
     // the search settles the rays its first membership test proves and lists
-    // the rest for the resolve (in the t2 region: t2 is kept by diagnostics only)
-    const bool rl = c->resolve_list && !F.diag && !late_prev && !F.sph && F.wide != 8;
+    // the rest for the resolve (in the t2 region: t2 is kept by diagnostics
+    // only).  Measured (profiles/r5/resolve_list): C4 +5 %, C2 +1 %, VCM +1 %;
+    // PT's dense launches -0.8 %, so they keep the resolve over every ray
+    const bool rl = c->resolve_list && !F.diag && !late_prev && !F.sph && F.wide != 8 && mode != TRACE_DENSE;
     int* rlist = rl ? reinterpret_cast<int*>(ts.t2) : nullptr;
     int* rlist_n = rl ? ts.rlist_n : nullptr;
     const size_t rlds = slds + (rl ? kRlistLds : 0);
