@@ -153,6 +153,7 @@ def cpu_reference(cfg_name, kind, W, H, tmp, shrink):
     # The GPU box gives one job 16 CPUs while os.cpu_count() shows the whole
     # machine's: the CPUs this process may run on, capped at that share
     ncores = max(1, min(16, _cpu_share()))
+    machine_cpus = os.cpu_count()
     procs = [subprocess.Popen([REFDRV, *map(str, args[:-1]), out + f".{k}"], stdout=subprocess.PIPE,
                               stderr=subprocess.DEVNULL, text=True, env=env) for k in range(ncores)]
     outs = [p.communicate(timeout=900) for p in procs]
