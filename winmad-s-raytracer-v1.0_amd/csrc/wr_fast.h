@@ -99,6 +99,12 @@ __host__ __device__ constexpr size_t fast_lds_bytes(int depth) { return size_t(d
 // binary tree (kMaxBvhDepth + 1 entries fit), so its push / pop carry no
 // spill branch: a generic pointer select between LDS and the spill area made
 // the compiler emit flat loads (vmcnt + lgkmcnt waits) on every pop.
+#ifndef WR_POP_TOGETHER
+#define WR_POP_TOGETHER 1
+#endif
+#ifndef WR_LEAF_SCHED
+#define WR_LEAF_SCHED 1
+#endif
 template <int W>
 struct SearchStack {
   // the 8-wide tree keeps 16 (a ray's stack outgrows 12 entries for 2e-4 of
@@ -1217,12 +1223,51 @@ struct QueueIndex {
     r = idx - q0;
   }
 };
+#ifndef WR_QFIELD_SGPR
+#define WR_QFIELD_SGPR 1
+#endif
+// a wave-uniform value forced into scalar registers (readfirstlane)
+template <class T>
+__device__ __forceinline__ T sgpr_value(T v) {
+  if constexpr (sizeof(T) == 8) {
+    unsigned long long u;
+    __builtin_memcpy(&u, &v, 8);
+    const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readfirstlane(static_cast<int>(u & 0xffffffffull)));
+    const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readfirstlane(static_cast<int>(u >> 32)));
+    u = (static_cast<unsigned long long>(hi) << 32) | lo;
+    T r;
+    __builtin_memcpy(&r, &u, 8);
+    return r;
+  } else {
+    static_assert(sizeof(T) == 4, "4- or 8-byte queue fields");
+    int u;
+    __builtin_memcpy(&u, &v, 4);
+    u = __builtin_amdgcn_readfirstlane(u);
+    T r;
+    __builtin_memcpy(&r, &u, 4);
+    return r;
+  }
+}
+// A queue's field for the lane's queue q.  Each queue's value is uniform and
+// taken into scalar registers before the per-lane select (WR_QFIELD_SGPR):
+// left to itself the compiler turns the select into a per-lane load from the
+// kernel-argument block, a vector-memory round trip before each ray's own
+// loads (refill) and stores (results).
 template <class Fn>
 __device__ __forceinline__ auto qfield(const TraceQueues& Q, int q, Fn field) {
+#if WR_QFIELD_SGPR
+  auto v = sgpr_value(field(Q.q[0]));
+#pragma unroll
+  for (int i = 1; i < kMaxQueues; ++i) {
+    const auto w = sgpr_value(field(Q.q[i]));
+    if (q == i) v = w;
+  }
+#else
   auto v = field(Q.q[0]);
 #pragma unroll
   for (int i = 1; i < kMaxQueues; ++i)
     if (q == i) v = field(Q.q[i]);
+#endif
   return v;
 }
 
@@ -1403,6 +1448,11 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
       if (!kSearchSpills || sp < kLdsStack) {
         link = stk_link[sp * 64];
         te = t_up32(stk_t[sp * 64]);
+#if WR_POP_TOGETHER
+        // the link is read with the entry's t, not after its test: one LDS
+        // round trip per entry instead of two on the search's chain
+        asm volatile("" : : "v"(link), "v"(te));
+#endif
       } else {
         const int2 e = spill[static_cast<size_t>(sp - kLdsStack) * gl + gidx];
         link = e.x;
@@ -1634,6 +1684,12 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         tb[j] = tp[1];
         tc[j] = tp[2];
       }
+#if WR_LEAF_SCHED
+      // every record load issued before the first test (the scheduler would
+      // otherwise start the first test, and wait for its record, before the
+      // second record's loads: two round trips per leaf instead of one)
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int j = 0; j < wrf::kMaxLeaf; ++j) {
         if (j >= cnt) break;
