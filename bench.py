@@ -275,8 +275,8 @@ def main():
     scene_path = make_scene(args.config, W, H, tmp)
     sc = native.Scene(scene_path)
     ctx = native.Context(sc, local)
-    if trace == "bvh":
-        ctx.set_trace_mode(native.TRACE_BVH)
+    # (the library's default is the BVH search: the reference's walk is selected explicitly)
+    ctx.set_trace_mode(native.TRACE_BVH if trace == "bvh" else native.TRACE_REFERENCE)
     film = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
 
     # one step = one iteration (BDPT) / one sample index of the spp grid (PT);

@@ -59,3 +59,13 @@ def test_bench_fails_loudly_without_gpu(cfg):
     assert out.returncode != 0
     assert "no HIP device" in out.stderr
     assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.gpu
+def test_bench_reference_trace_is_the_kd_walk():
+    """`--trace reference` times the reference's KD walk (the library's default
+    is the BVH search, so bench.py must select the walk explicitly)."""
+    d = run_bench("--config", "c2", "--trace", "reference", "--no-compare")
+    assert d["config"]["trace"] == "reference"
+    assert d["roofline"]["kernel"].startswith("k_trace (KD"), d["roofline"]["kernel"]
+    assert "bvh" not in d["roofline"]
