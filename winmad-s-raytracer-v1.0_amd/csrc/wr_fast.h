@@ -31,6 +31,7 @@
 // the end of a lane's search it ran with a handful of lanes active (measured:
 // 13 % VALU lane utilisation, most of it there).
 #pragma once
+#include <type_traits>
 #include "wr_bvh.h"
 
 namespace wrd {
@@ -1226,6 +1227,9 @@ struct QueueIndex {
 #ifndef WR_QFIELD_SGPR
 #define WR_QFIELD_SGPR 1
 #endif
+#ifndef WR_QFIELD_GLOBAL
+#define WR_QFIELD_GLOBAL 1
+#endif
 // a wave-uniform value forced into scalar registers (readfirstlane)
 template <class T>
 __device__ __forceinline__ T sgpr_value(T v) {
@@ -1235,9 +1239,17 @@ __device__ __forceinline__ T sgpr_value(T v) {
     const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readfirstlane(static_cast<int>(u & 0xffffffffull)));
     const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readfirstlane(static_cast<int>(u >> 32)));
     u = (static_cast<unsigned long long>(hi) << 32) | lo;
-    T r;
-    __builtin_memcpy(&r, &u, 8);
-    return r;
+    if constexpr (WR_QFIELD_GLOBAL && std::is_pointer_v<T>) {
+      // queue arrays are global memory: the pointer is rebuilt in the global
+      // address space, so that the loads and stores through it stay global
+      // (a generic pointer makes them flat, which also wait on the LDS counter)
+      using G = __attribute__((address_space(1))) std::remove_pointer_t<T>*;
+      return (T)(reinterpret_cast<G>(u));
+    } else {
+      T r;
+      __builtin_memcpy(&r, &u, 8);
+      return r;
+    }
   } else {
     static_assert(sizeof(T) == 4, "4- or 8-byte queue fields");
     int u;
