@@ -1310,6 +1310,14 @@ int cr_scene_dump(const cr_scene* s, const char* out) {
 /* ------------------------------------------------------------------------- */
 typedef struct { int node; float tmin, tmax; } todo_t;
 
+/* Debugging aid (tests / scripts only): every traversal query of the calls
+ * that follow -- origin, direction, best t (-1 = miss), winner index as int
+ * bits -- into buf[cap][8]; single-threaded callers only. */
+static float* g_ray_log;
+static int64_t g_ray_log_cap, g_ray_log_n;
+void cr_set_ray_log(float* buf, int64_t cap) { g_ray_log = buf; g_ray_log_cap = cap; g_ray_log_n = 0; }
+int64_t cr_ray_log_count(void) { return g_ray_log_n; }
+
 static int traverse(const cr_scene* s, const ray_t* ray, cr_stats* st) {
     float tmin, tmax;
     if (!box_hit(&s->root_box, ray, &tmin, &tmax)) return -1;
@@ -1352,6 +1360,13 @@ static int traverse(const cr_scene* s, const ray_t* ray, cr_stats* st) {
         }
     }
     if (st) { st->inner_visits += ni; st->leaf_visits += nl; st->prim_refs += nr; st->tri_tests += ntt; st->sph_tests += nst; }
+    if (g_ray_log && g_ray_log_n < g_ray_log_cap) { /* debugging: cr_set_ray_log */
+        float* o = g_ray_log + 8 * g_ray_log_n++;
+        o[0] = ray->o.x; o[1] = ray->o.y; o[2] = ray->o.z;
+        o[3] = ray->d.x; o[4] = ray->d.y; o[5] = ray->d.z;
+        o[6] = res >= 0 ? best : -1.f;
+        memcpy(&o[7], &res, 4);
+    }
     return res;
 }
 
@@ -1475,6 +1490,9 @@ static int sample_scatter(bdpt_ctx* c, rng_t* rng, const bsdf_t* b, v3 hit, bsta
     return 1;
 }
 
+#ifdef CR_DEBUG_PATH
+static int g_dbg_on;
+#endif
 static c3 connect_camera(bdpt_ctx* c, const bstate* ls, v3 hit, const bsdf_t* b) { /* :313-368 */
     const cr_scene* s = c->s;
     const camera_t* cam = &s->cam;
@@ -1495,6 +1513,12 @@ static c3 connect_camera(bdpt_ctx* c, const bstate* ls, v3 hit, const bsdf_t* b)
     float pdfA = i2s;
     float s2i = 1.f / i2s;
     res = cdivs(cmul(ls->thr, f), (float)c->P * s2i);
+#ifdef CR_DEBUG_PATH
+    if (g_dbg_on)
+        printf("[dbg cpu] len %d hit %a %a %a thr %a %a %a f %a %a %a cos_to %a d2 %a i2s %a res %a %a %a rp %a dvcm %a dvc %a\n",
+               ls->len, hit.x, hit.y, hit.z, ls->thr.r, ls->thr.g, ls->thr.b, f.r, f.g, f.b, cosTo, d2, i2s,
+               res.r, res.g, res.b, rp, ls->dVCM, ls->dVC);
+#endif
     if (cblack(res)) return res;
     if (occluded(s, hit, dtc, cam->pos, c->st)) return C0;
     float wl = (pdfA / (float)c->P) * (ls->dVCM + rp * ls->dVC);
@@ -1632,6 +1656,9 @@ static void run_iteration(bdpt_ctx* c, mt_state* mt, int mode, uint32_t seed, ui
         bstate ls;
         memset(&ls, 0, sizeof ls);
         gen_light(c, &rng, &ls);
+#ifdef CR_DEBUG_PATH
+        g_dbg_on = pi == CR_DEBUG_PATH && iter == CR_DEBUG_ITER;
+#endif
         for (;; ls.len++) {
             ray_t ray = mkray(vadd(ls.origin, vscale(ls.dir, R_EPS)), ls.dir);
             hit_t h;

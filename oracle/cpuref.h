@@ -64,6 +64,10 @@ void cr_trace(const cr_scene* s, const float* rays9, int64_t n, int32_t* out_i,
  * Iterations [iter_begin, iter_begin + iterations).  Paths restricted to
  * [path_begin, path_end) (full frame: 0, W*H) -- used only to time a bounded
  * CPU sample.  control_length 3 = reference; <= 0 disables the length filter. */
+/* debugging aid: log every traversal query (o, d, best t or -1, winner bits) */
+void cr_set_ray_log(float* buf /* [cap][8] */, int64_t cap);
+int64_t cr_ray_log_count(void);
+
 int cr_render_bdpt(const cr_scene* s, int W, int H, int iter_begin, int iterations,
                    uint32_t seed, int rng_mode, int control_length, int64_t path_begin,
                    int64_t path_end, float* film, cr_stats* st);

@@ -29,7 +29,7 @@ class Stats(C.Structure):
 def lib():
     global _lib
     if _lib is None:
-        so = os.path.join(ORACLE, "liboracle.so")
+        so = os.environ.get("WR_ORACLE_SO") or os.path.join(ORACLE, "liboracle.so")  # debugging variants
         if not os.path.exists(so):
             subprocess.run(["make", "-C", ORACLE, "oracle"], check=True, capture_output=True)
         L = C.CDLL(so)

@@ -142,7 +142,10 @@ def assert_film_parity(film, ref, *, case, bad_rel=1e-4, trimmed=2e-6, bias=2e-7
     assert abs(s["trimmed_bias"]) < bias, s
     # north_star: per-channel RMSE < 1e-3; SURVEY 8(d): per-channel RMSE / RMS(ref) < 1e-2
     assert np.all(s["ch_rmse"] < 1e-3), s
-    if os.environ.get("WR_PARITY_MEASURE") == "1":
+    if os.environ.get("WR_PARITY_MEASURE") == "1" and os.environ.get("WR_PARITY_LOG"):
+        # a measuring run (its statistics go to the log): never mistaken for a pass
+        import warnings
+        warnings.warn(f"WR_PARITY_MEASURE: measured-limit gates skipped for {case}")
         return s
     assert np.all(s["ch_rel_rmse"] < ch_rel_rmse), s
     b = split_bounds(case)

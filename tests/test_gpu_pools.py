@@ -67,6 +67,21 @@ def test_pool_overflow_redo_keeps_a_device_film(monkeypatch):
     assert np.allclose(dev.cpu().numpy() - base.cpu().numpy(), ref, rtol=1e-4, atol=1e-5)
 
 
+def test_failed_redo_leaves_the_device_film_as_it_was(monkeypatch):
+    """An error after the first launch (here a redo that overflows again,
+    forced by WR_TEST_REDO_FAIL) returns with the caller's device film as it
+    was before the render, not holding part of one (advice r5)."""
+    torch = pytest.importorskip("torch")
+    path = _scenes.torus(96, 64)
+    base = torch.rand((64, 96, 3), dtype=torch.float32, device="cuda:0")
+    dev = base.clone()
+    monkeypatch.setenv("WR_TEST_REDO_FAIL", "1")
+    with pytest.raises(native.WrError, match="overflowed"):
+        _render(path, 96, 64, 2, 7, 0.002, monkeypatch, film_ptr=dev.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dev, base)
+
+
 def test_default_pools_hold_the_headline_render_at_1k_per_path(monkeypatch):
     """The default sizing: the C2 frame (1080p torus, 2 iterations, 16
     pipelines) is not redone, and the work buffers hold <= 1.2 KB per path in

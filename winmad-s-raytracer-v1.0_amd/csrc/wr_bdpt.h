@@ -448,6 +448,10 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
                   s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
                   s_val = res * w;
                   s_pix = pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W);
+                } else {
+                  // an EPS-black res is returned before the shadow test and the
+                  // MIS weight (:354-355), and the caller adds it (:116-118)
+                  film_add(A.film, pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W), res);
                 }
               }
             }

@@ -5,11 +5,13 @@
 //
 // Every expression keeps the reference's float evaluation order; the
 // translation units that include this file are built with -ffp-contract=off and
-// HIP's default correctly-rounded f32 divide / sqrt, so the only deviation from
-// the CPU oracle is in the libm transcendentals (cosf / sinf / powf: OCML vs glibc).
+// HIP's default correctly-rounded f32 divide / sqrt, and the libm calls of the
+// reference (cosf / sinf / powf) go through wr_libm.h, which returns glibc's
+// float bit for bit, so every value equals the CPU oracle's.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "wr_libm.h"
 
 namespace wrd {
 
@@ -116,19 +118,19 @@ __device__ __forceinline__ V3 sample_rect_strat(V3 s, V3 v0, V3 v1, V3 v2, int c
 __device__ __forceinline__ V3 sample_cos_hemi(V3 s, float* pdf) {  // sampler.cpp:95-108
   float u1 = 2.f * WR_PI * s.x;
   float u2 = sqrtf(1.f - s.y);
-  V3 r = v3(cosf(u1) * u2, sinf(u1) * u2, sqrtf(s.y));
+  V3 r = v3(wr_cosf(u1) * u2, wr_sinf(u1) * u2, sqrtf(s.y));
   *pdf = r.z * WR_INV_PI;
   return normalize(r);
 }
 __device__ __forceinline__ V3 sample_pow_cos_hemi(V3 s, float power) {  // sampler.cpp:115-129
   float u1 = 2.f * WR_PI * s.x;
-  float u2 = powf(s.y, 1.f / (power + 1.f));
+  float u2 = wr_powf(s.y, 1.f / (power + 1.f));
   float u3 = sqrtf(1.f - u2 * u2);
-  return normalize(v3(cosf(u1) * u3, sinf(u1) * u3, u2));
+  return normalize(v3(wr_cosf(u1) * u3, wr_sinf(u1) * u3, u2));
 }
 __device__ __forceinline__ float pow_cos_pdf(V3 n, V3 d, float power) {  // sampler.cpp:131-136
   float c = clampv(dot(n, d), 0.f, 1.f);
-  return (power + 1.f) * powf(c, power) * (0.5f * WR_INV_PI);
+  return (power + 1.f) * wr_powf(c, power) * (0.5f * WR_INV_PI);
 }
 
 // ------------------------------------------------------------ scene records
@@ -273,7 +275,7 @@ __device__ __forceinline__ V3 calc_diffuse(const Bsdf& b, const DMat& m, V3 wo, 
 }
 __device__ __forceinline__ V3 glossy_rho(const DMat& m, float c) {
   V3 rho = m.phong * (m.phong_exp + 2.f) * 0.5f * WR_INV_PI;
-  return rho * powf(c, m.phong_exp);
+  return rho * wr_powf(c, m.phong_exp);
 }
 __device__ __forceinline__ V3 calc_glossy(const Bsdf& b, const DMat& m, V3 wo, float* dp, float* rp) {
   if (cmpf(b.pg) == 0) return v3(0.f, 0.f, 0.f);  // bsdf.cpp:74-100

@@ -20,6 +20,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -46,13 +47,26 @@ static int fail(int code, const std::string& msg) { return wr::set_error(code, m
 // environment by itself: a host that wants the measured configuration (16
 // pipelines) asks for it with wr_request_hw_queues() before its first HIP call
 // (example_main / tot_main do; bench.py and winmad_rt/native.py set the
-// variable before HIP starts).  wr_create sizes the pipelines by the variable
-// as it reads then, i.e. by what HIP saw, unless the caller changed it after
-// HIP started.
-static int hw_queues_in_effect() {
+// variable before HIP starts).  The count is latched by the library's first
+// wr_create (the library's first HIP call, or later than the host's): pipelines
+// are sized by that value from then on, and a wr_request_hw_queues after it
+// changes nothing (HIP has read the variable by then).  A host that starts HIP
+// itself (e.g. torch.cuda.is_available()) before asking gets the queues HIP
+// saw only if it asks before that, which is what native.py does.
+static std::atomic<int> g_hw_queues_latched{0};
+static int hw_queues_env() {
   const char* q = std::getenv("GPU_MAX_HW_QUEUES");
   const int n = q ? std::atoi(q) : 0;
   return n > 0 ? n : 4;  // HIP's default
+}
+static int hw_queues_in_effect() {
+  const int l = g_hw_queues_latched.load();
+  return l > 0 ? l : hw_queues_env();
+}
+static int latch_hw_queues() {
+  int expect = 0;
+  g_hw_queues_latched.compare_exchange_strong(expect, hw_queues_env());
+  return g_hw_queues_latched.load();
 }
 
 // Every C-ABI entry that selects a device (hipSetDevice) leaves the caller's
@@ -1463,6 +1477,7 @@ int wr_api_version(void) { return WR_API_VERSION; }
 
 int wr_request_hw_queues(int n) {
   if (n < 1 || n > 32) return fail(WR_E_ARG, "hardware queues: 1..32");
+  if (g_hw_queues_latched.load() > 0) return hw_queues_in_effect();  // HIP already read it
   if (hw_queues_in_effect() < n && setenv("GPU_MAX_HW_QUEUES", std::to_string(n).c_str(), 1) != 0)
     return fail(WR_E_ARG, "setenv GPU_MAX_HW_QUEUES failed");
   return hw_queues_in_effect();
@@ -1545,6 +1560,7 @@ int wr_device_count(void) {
 int wr_create(const wr_scene* sc, int device, wr_context** out) {
   if (!sc || !out) return fail(WR_E_ARG, "null argument");
   *out = nullptr;
+  latch_hw_queues();  // before the library's first HIP call: the value HIP reads
   if (int rc = check_device()) return rc;
   DeviceGuard dg;
   const wr::Scene& s = sc->s;
@@ -1586,7 +1602,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
   // one pipeline per hardware queue of this process (HIP's GPU_MAX_HW_QUEUES,
   // default 4; pipeline 0 shares the context stream), at most 16: streams that
   // share a hardware queue serialize behind each other
-  c->npipes = std::max(1, std::min(kMaxPipes, hw_queues_in_effect()));
+  c->npipes = std::max(1, std::min(kMaxPipes, latch_hw_queues()));
   if (const char* e = std::getenv("WR_PIPES")) c->npipes = std::max(1, std::min(kMaxPipes, std::atoi(e)));
   if (const char* e = std::getenv("WR_PIECE_CAP")) c->piece_cap = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("WR_PIECE_MIN")) c->piece_min = std::max(1, std::atoi(e));
@@ -1834,6 +1850,14 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       const int w = std::atoi(e);
       if (w == 2 || w == 4 || (w == 8 && WR_BVH_WIDE == 8)) wide = w;
     }
+    // the 8-wide search is instantiated for triangle leaves only: a scene with
+    // spheres searches the 4-wide tree, whose kernels run the sphere test
+    if (wide == 8)
+      for (const wr::Prim& p : s.prims)
+        if (p.type != wr::kTri) {
+          wide = 4;
+          break;
+        }
     wrf::FastHost fh;
     wrf::build_fast(s, fh, wide, wide == 2);
     if (fh.ok) {
@@ -2505,7 +2529,16 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
                  sizeof(BdptGroup), sizeof(TraceQueues), sizeof(DevScene), sizeof(c->fs));
   return finish_render(c, npl, st, t0, &overflow);
   };
-  if (int rc = run(plan)) return rc;
+  // an error after the first launch leaves a caller's device film as it was
+  // before the render (its saved copy), not holding a partial render
+  auto restore_film = [&](int rc) -> int {
+    if (pooled && film_on_device) {
+      (void)hipDeviceSynchronize();  // the pipelines' launches in flight
+      (void)hipMemcpy(dfilm, c->film_bak, nf * sizeof(float), hipMemcpyDeviceToDevice);
+    }
+    return rc;
+  };
+  if (int rc = run(plan)) return restore_film(rc);
   if (overflow) {
     // A vertex pool or shadow queue filled up and appends were dropped: redo
     // the render from the film as it was, with pieces whose worst case fits
@@ -2515,14 +2548,16 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
     // render.  Rare: the pools hold several times what the reference scenes use.
     const BdptBuf& B = c->pipes[0].bb[0];
     const int safe = std::min({B.cap_sq / (kVMax + 2), B.vcap / kVMax, B.ccap / kCvMax, cap}) / 64 * 64;
-    if (safe < 64) return fail(WR_E_HIP, "BDPT pools too small for a 64-path piece");
+    if (safe < 64) return restore_film(fail(WR_E_HIP, "BDPT pools too small for a 64-path piece"));
     if (film_on_device) HIPCHK(hipMemcpyAsync(dfilm, c->film_bak, nf * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
     else HIPCHK(hipMemsetAsync(dfilm, 0, nf * sizeof(float), c->stream));
     if (st) *st = st0;
     A0.untiled = 1;
     overflow = 0;
-    if (int rc = run(plan_pieces(f_lo, f_hi, P, 64, safe, fit, c->piece_min))) return rc;
-    if (overflow) return fail(WR_E_HIP, "BDPT pools overflowed with pieces the worst case fits");
+    if (int rc = run(plan_pieces(f_lo, f_hi, P, 64, safe, fit, c->piece_min))) return restore_film(rc);
+    // (env WR_TEST_REDO_FAIL=1: the test of this error path treats the redo as overflowed)
+    if (overflow || std::getenv("WR_TEST_REDO_FAIL"))
+      return restore_film(fail(WR_E_HIP, "BDPT pools overflowed with pieces the worst case fits"));
     if (st) st->redone += 1;
   }
   if (st) {

@@ -250,6 +250,8 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_vcm_light_shade(Vc
                       s_d = normalize(dtc);  // occluded() -> Ray(p1, dir)
                       s_val = res;
                       s_pix = pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W);
+                    } else {  // EPS-black: returned unoccluded (vertexcm.cpp:375-376), added (:126-127)
+                      film_add(A.film, pix_index(static_cast<int>(ip.x), static_cast<int>(ip.y), A.H, A.W), res);
                     }
                   }
                 }
