@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Distribution of GPU-vs-oracle film differences (counter RNG, same streams)
-over parity cases beside the -m gpu suite's (larger C3 / C4 / 1080p films) --
-and the derivation of the film gates in tests/_parity.py from them.
+over parity cases beside the -m gpu suite's (larger C3 / C4 / 1080p films),
+each also run through the suite's gates (tests/_parity.py: every pixel).
 
 Measure: per case, relative RMSE (RMSE / RMS(oracle)), per-channel RMSE, the
 fraction of film values whose relative difference exceeds 1e-6 .. 1e-3
@@ -11,12 +11,6 @@ one JSON line per case to stdout (and --out).
 
     python scripts/parity_stats.py [--out gpurun_out/parity_stats.jsonl] [--quick]
 
-Derive: the per-case maxima of such logs -- this script's and the suite's own
-(WR_PARITY_LOG=<file> WR_PARITY_MEASURE=1 pytest -m gpu: every
-tests/_parity.py gate logs its statistics) -- become
-tests/golden/parity_limits.json, which the gates read:
-
-    python scripts/parity_stats.py --derive profiles/r5/parity_suite.jsonl profiles/r5/parity_stats.jsonl
 """
 import argparse
 import json
@@ -140,47 +134,12 @@ def run_case(name, kind, maker, W, H, kw, trace):
     return r
 
 
-def derive(logs, out_path):
-    """Per-case maxima of the logged gate statistics -> tests/golden/parity_limits.json."""
-    cases = {}
-    for p in logs:
-        for line in open(p):
-            r = json.loads(line)
-            if r.get("kind", "film") == "vcm" or r["case"].startswith("vcm"):
-                continue
-            m = cases.setdefault(r["case"], {"bad_pixels": 0, "max_cluster": 0, "max_row": 0, "max_col": 0,
-                                             "bias": 0.0, "ch_rel_rmse": 0.0, "pixels": r.get("pixels") or r.get("npix"),
-                                             "samples": 0})
-            for k in ("bad_pixels", "max_cluster", "max_row", "max_col"):
-                m[k] = max(m[k], int(r[k]))
-            m["bias"] = max(m["bias"], abs(float(r["bias"])))
-            m["ch_rel_rmse"] = max(m["ch_rel_rmse"], max(float(x) for x in r["ch_rel_rmse"]))
-            m["samples"] += 1
-    doc = {"source": [os.path.relpath(p, REPO) for p in logs],
-           "note": "per-case maxima of the GPU-vs-oracle film statistics; tests/_parity.py derives its gates "
-                   "from them (split pixels <= max(16, 4x), cluster <= max(3, 2x), row/column <= max(4, 2x), "
-                   "|bias| <= max(2e-5, 4x))",
-           "cases": dict(sorted(cases.items()))}
-    with open(out_path, "w") as f:
-        json.dump(doc, f, indent=1)
-        f.write("\n")
-    for k, m in sorted(cases.items()):
-        print(f"{k:40s} n={m['samples']} bad={m['bad_pixels']} cl={m['max_cluster']} row={m['max_row']} "
-              f"col={m['max_col']} bias={m['bias']:.2e} chrel={m['ch_rel_rmse']:.2e}")
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--trace", default="reference", choices=["reference", "bvh"])
-    ap.add_argument("--derive", nargs="+", default=None, metavar="LOG",
-                    help="write tests/golden/parity_limits.json from these JSONL logs and exit")
     args = ap.parse_args()
-    if args.derive:
-        derive(args.derive, _parity.LIMITS_PATH)
-        return
-    os.environ["WR_PARITY_MEASURE"] = "1"
     f = open(args.out, "a") if args.out else None
     for cs in cases(args.quick):
         r = run_case(*cs, trace=args.trace)

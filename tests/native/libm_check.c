@@ -5,13 +5,15 @@
  *
  *   libm_check sampler            cos/sin(2*PI*k/2^24), all 2^24 k
  *                                 (sampler.cpp:97-100,121-125)
- *   libm_check range LO HI        cos/sin of every float in [LO, HI]
- *   libm_check powexp E [STEP]    powf(c, E) for every float c in (0, 1]
+ *   libm_check range LO HI [STEP] cos/sin of every (STEP-th) float x in [LO, HI]
+ *                                 (LO >= 0) and of -x
+ *   libm_check powexp E [STEP]    powf(c, E) for every (STEP-th) float c in (0, 1]
  *                                 (bsdf.cpp:99, sampler.cpp:123,135) and
  *                                 powf(k/2^24, 1/(E+1)) for all k (sampler.cpp:119)
  *   libm_check powrand N SEED     powf of N random (x, y) pairs over all floats
  *
- * Built by tests/test_libm.py with gcc -O2 -ffp-contract=off.
+ * Built by tests/test_libm.py (strided, CPU suite) and scripts/libm_check_full.sh
+ * (every input, profiles/r6/libm_check.json) with gcc -O2 -ffp-contract=off.
  */
 #include <math.h>
 #include <stdio.h>
@@ -47,14 +49,18 @@ int main(int argc, char** argv) {
     report("cos_sampler", 1u << 24, dc, fx, 0);
     report("sin_sampler", 1u << 24, ds, fx, 0);
   } else if (!strcmp(argv[1], "range") && argc >= 4) {
-    float lo = strtof(argv[2], 0), hi = strtof(argv[3], 0);
+    /* every STEP-th float x in [LO, HI] (LO >= 0), and -x */
+    uint32_t lo = wr_lm_asuint(strtof(argv[2], 0)), hi = wr_lm_asuint(strtof(argv[3], 0));
+    uint32_t step = argc >= 5 ? (uint32_t)strtoul(argv[4], 0, 10) : 1;
     unsigned long long n = 0, dc = 0, ds = 0;
     float fx = 0;
-    for (float x = lo;; x = nextafterf(x, INFINITY)) {
-      ++n;
-      if (!same(wr_cosf(x), cosf(x))) { if (!dc && !ds) fx = x; ++dc; }
-      if (!same(wr_sinf(x), sinf(x))) { if (!dc && !ds) fx = x; ++ds; }
-      if (x >= hi) break;
+    for (uint64_t u = lo; u <= hi; u += step) {
+      for (int sg = 0; sg < 2; ++sg) {
+        float x = wr_lm_asfloat((uint32_t)u | (sg ? 0x80000000u : 0u));
+        ++n;
+        if (!same(wr_cosf(x), cosf(x))) { if (!dc && !ds) fx = x; ++dc; }
+        if (!same(wr_sinf(x), sinf(x))) { if (!dc && !ds) fx = x; ++ds; }
+      }
     }
     report("cos_range", n, dc, fx, 0);
     report("sin_range", n, ds, fx, 0);

@@ -228,8 +228,6 @@ def test_bdpt_1080p_matches_oracle_counter_rng():
     ref, rst = _oracle.Scene(path).bdpt(W, H, 1, 5489, mode=1)
     assert_film_parity(film, ref, case="bdpt_torus1920x1080_i1_s5489")
     assert_ray_counts(st, rst)
-    if os.environ.get("WR_PARITY_MEASURE") == "1":  # the measurement run logs the real film only
-        return
     # the gates catch the GPU film damaged the ways tests/test_parity_gates.py
     # damages oracle films: one 8-row tile band not written (verdict r4: at
     # 1080p that moves the per-channel RMSE by only ~3e-4), one row's splats a
@@ -246,14 +244,56 @@ def test_bdpt_1080p_matches_oracle_counter_rng():
     bad[row] = np.roll(film[row], 1, axis=0)
     with pytest.raises(AssertionError):
         assert_film_parity(bad, ref, case="bdpt_torus1920x1080_i1_s5489")
+    # and one pixel off by 1e-3 of its value (a single path's share gone)
+    y, x = np.argwhere(ref.any(axis=-1))[len(np.argwhere(ref.any(axis=-1))) // 2]
+    bad = film.copy()
+    bad[y, x] *= 1.001
+    with pytest.raises(AssertionError):
+        assert_film_parity(bad, ref, case="bdpt_torus1920x1080_i1_s5489")
+
+
+# Seeds none of the other cases use, each run once (verdict r5, next 1): the
+# films must equal the oracle's on every pixel for any random numbers, not
+# only for the seeds the gates were first measured on.
+SWEEP_SEEDS = (1, 7, 41, 97, 1234)
+
+
+@pytest.mark.parametrize("seed", SWEEP_SEEDS)
+@pytest.mark.parametrize("name,maker,W,H,it,ctl", [
+    ("cbox", lambda: _scenes.cbox(64, 48, "bdpt"), 64, 48, 3, 0),  # every path length, NEE + connections
+    ("torus", lambda: _scenes.torus(256, 256), 256, 256, 1, 3),
+])
+def test_bdpt_seed_sweep_matches_oracle(name, maker, W, H, it, ctl, seed):
+    path = maker()
+    film, st = ctx(path).render_bdpt(W, H, iterations=it, seed=seed, control_length=ctl)
+    ref, rst = _oracle.Scene(path).bdpt(W, H, it, seed, mode=1, control_length=ctl)
+    assert_film_parity(film, ref, case=f"bdpt_{name}{W}x{H}_i{it}_s{seed}_ctl{ctl}")
+    assert_ray_counts(st, rst)
+
+
+def test_bdpt_1080p_seed_sweep_matches_oracle():
+    """The C2 frame (torus.scene 1920x1080, one iteration) at each sweep
+    seed: every pixel equals the oracle's.  The oracle films are rendered on
+    5 host threads (ctypes releases the GIL; the scene is read-only)."""
+    from concurrent.futures import ThreadPoolExecutor
+    W, H = 1920, 1080
+    path = _scenes.torus(W, H)
+    osc = _oracle.Scene(path)
+    osc.bdpt(2, 2, 1, 1, mode=1)  # (the oracle's one-time constants, before the threads)
+    with ThreadPoolExecutor(len(SWEEP_SEEDS)) as ex:
+        refs = list(ex.map(lambda sd: osc.bdpt(W, H, 1, sd, mode=1), SWEEP_SEEDS))
+    for seed, (ref, rst) in zip(SWEEP_SEEDS, refs):
+        film, st = ctx(path).render_bdpt(W, H, iterations=1, seed=seed)
+        assert_film_parity(film, ref, case=f"bdpt_torus1920x1080_i1_s{seed}")
+        assert_ray_counts(st, rst)
 
 
 def test_path_radiance_per_ray_matches_oracle():
     """wr_path_radiance == PathIntegrator::raytracing per caller ray (same
     counter-RNG stream): camera rays through random raster points and random
-    rays inside the box.  Single-sample radiance is spiky, so the gate is per
-    ray: all but a few (paths split by libm rounding) agree to 1e-3 relative,
-    and the batch mean to 1e-2."""
+    rays inside the box.  Every ray's radiance agrees to 1e-5 relative (the
+    same path, summed in the same order: glibc-exact libm on the device), and
+    the traversal counts are equal."""
     path = _scenes.cbox(64, 48)
     rng = np.random.default_rng(9)
     n = 20000
@@ -267,10 +307,9 @@ def test_path_radiance_per_ray_matches_oracle():
     rad, st = ctx(path).path_radiance(rays, max_depth=7, seed=77, sample=3)
     ref, rst = _oracle.Scene(path).pt_radiance(np.concatenate([o, d], 1), 7, 77, sample=3)
     assert np.all(np.isfinite(rad)) and rad.min() >= 0 and ref.sum() > 0
-    close = np.all(np.abs(rad - ref) <= 1e-3 * (1.0 + np.abs(ref)), axis=1)
-    assert close.mean() > 0.99, close.mean()
-    assert abs(rad.mean() - ref.mean()) <= 1e-2 * ref.mean()
-    assert abs(st.closest_rays - rst.closest_rays) <= 0.005 * rst.closest_rays
+    close = np.all(np.abs(rad - ref) <= 1e-5 * np.abs(ref) + 1e-30, axis=1)
+    assert close.all(), (np.count_nonzero(~close), np.argwhere(~close)[:5].ravel())
+    assert st.closest_rays == rst.closest_rays and st.shadow_rays == rst.shadow_rays
     with pytest.raises(native.WrError):
         ctx(path).path_radiance(rays[:4], max_depth=-1)
 
@@ -474,7 +513,7 @@ def test_bdpt_overlapped_passes_equal_the_sequential_schedule(name, maker, W, H,
     # with every path length counted, a split path moves more pixels (the
     # gates of test_cbox_bdpt_film_matches_oracle); the rest keep the 2e-6 gate
     assert_film_parity(fa, orc, case=f"bdpt_{name}{W}x{H}_i3_s77_ctl{ctl}")
-    assert_ray_counts(sa, ost, slack=64)
+    assert_ray_counts(sa, ost)
 
 
 @pytest.mark.parametrize("W,H,cap,pipes", [(100, 60, 3000, 1), (100, 60, 1000, 2), (99, 61, 2049, 1)])
@@ -606,7 +645,7 @@ def test_cbox_bdpt_film_matches_oracle():
         # every path length counts with control_length 0, so a split path (tests/_parity.py)
         # moves more pixels: 113 of 3,072 measured; the other pixels keep the 2e-6 gate
         assert_film_parity(film, ref, case=f"bdpt_cbox64x48_i3_s5489_ctl{ctl}")
-        assert_ray_counts(st, rst, slack=64)
+        assert_ray_counts(st, rst)
 
 
 def test_bdpt_1m_scene_film_matches_oracle():

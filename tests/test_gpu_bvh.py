@@ -346,7 +346,7 @@ def test_deferred_hard_rays_render_the_same_film(name, maker, W, H, its, monkeyp
     assert _film_close(fa, fb)
     ref, rst = _oracle.Scene(path).bdpt(W, H, its, 5489, mode=1)
     assert_film_parity(fa, ref, case=f"bdpt_{name}{W}x{H}_i{its}_s5489_defer")
-    assert_ray_counts(sa, rst, slack=64)
+    assert_ray_counts(sa, rst)
     # and every deferred answer is the KD walk's, bit for bit
     monkeypatch.setenv("WR_DEFER", "1")
     monkeypatch.setenv("WR_BVH_VERIFY", "1")

@@ -34,13 +34,13 @@ def _render(path, W, H, it, seed, scale, monkeypatch, ctl=3, pipes=None, film_pt
 
 @pytest.mark.parametrize("name,maker,W,H,it,seed,ctl,scale,case", [
     ("torus", lambda: _scenes.torus(256, 256), 256, 256, 2, 5, 3, 0.002, "bdpt_torus256x256_i2_s5"),
-    ("cbox", lambda: _scenes.cbox(64, 48, "bdpt"), 64, 48, 3, 5489, 0, 0.02, "bdpt_cbox64x48_i3_s5489_ctl0"),
+    # seed 41: the case round 5 moved to 5489 when its GPU film split from the oracle's (verdict r5)
+    ("cbox", lambda: _scenes.cbox(64, 48, "bdpt"), 64, 48, 3, 41, 0, 0.02, "bdpt_cbox64x48_i3_s41_ctl0"),
 ])
 def test_pool_overflow_is_redone_exactly(name, maker, W, H, it, seed, ctl, scale, case, monkeypatch):
     """Tiny pools overflow: the render is redone (st.redone) and equals the
     unbounded render -- same rays, same film up to the order of float atomics
-    -- and the oracle's film, under the gates of the same render with the
-    default buffers (its measured split limits)."""
+    -- and the oracle's film, on every pixel."""
     path = maker()
     small, ss = _render(path, W, H, it, seed, scale, monkeypatch, ctl=ctl, pipes=4)
     full, sf = _render(path, W, H, it, seed, 0, monkeypatch, ctl=ctl, pipes=4)
@@ -49,7 +49,7 @@ def test_pool_overflow_is_redone_exactly(name, maker, W, H, it, seed, ctl, scale
     assert np.allclose(small, full, rtol=1e-4, atol=1e-6)
     ref, rst = _oracle.Scene(path).bdpt(W, H, it, seed, mode=1, control_length=ctl)
     assert_film_parity(small, ref, case=case)
-    assert_ray_counts(ss, rst, slack=64)
+    assert_ray_counts(ss, rst)
 
 
 def test_pool_overflow_redo_keeps_a_device_film(monkeypatch):

@@ -1,15 +1,13 @@
 """GPU parity for VertexCM (wr_render_vcm) against the oracle's restatement of
 vertexcm.cpp:47-285 (itself pinned bit for bit to the reference, test_oracle.py).
 
-The GPU and the oracle draw the same counter-RNG numbers.  Differences come
-from OCML vs glibc cosf/sinf/powf rounding (as for BDPT) and from the order in
-which merged contributions are summed (hash grid vs the reference's KD tree:
-the SET of merged light vertices is the same, tests/test_oracle.py
-test_vcm_kdtree_search_is_the_brute_force_set).  Gates: whole-film relative
-RMSE < 5e-3 and summed bias < 1e-3 (tests/_parity.py: an ulp of vertex
-position flips merges at the radius, so per-pixel gates do not apply),
-per-channel RMSE < 1e-3 (north_star), ray counts equal up to split paths,
-merge counts (vertices found in radius, merges) within 1 %.
+The GPU and the oracle draw the same counter-RNG numbers and compute the same
+floats (glibc-exact libm on the device, tests/test_libm.py), and the hash grid
+finds the same SET of light vertices in the merge radius as the reference's KD
+tree (tests/test_oracle.py test_vcm_kdtree_search_is_the_brute_force_set); only
+the order in which merges and splats are summed differs.  Gates: every pixel
+as for BDPT (tests/_parity.py), ray counts and merge counts (queries, vertices
+found in radius, merges) equal.
 """
 import numpy as np
 import pytest
@@ -25,11 +23,8 @@ pytestmark = pytest.mark.gpu
 
 def _check(film, st, ref, rst):
     assert_vcm_parity(film, ref)
-    assert abs(st.closest_rays - rst.closest_rays) <= 16 + 2e-6 * rst.closest_rays
-    assert abs(st.shadow_rays - rst.shadow_rays) <= 16 + 2e-6 * rst.shadow_rays
-    assert abs(st.vm_queries - rst.vm_queries) <= 0.005 * rst.vm_queries + 2
-    assert abs(st.vm_found - rst.vm_found) <= 0.01 * rst.vm_found + 4
-    assert abs(st.vm_merged - rst.vm_merged) <= 0.01 * rst.vm_merged + 4
+    for k in ("closest_rays", "shadow_rays", "vm_queries", "vm_found", "vm_merged"):
+        assert getattr(st, k) == getattr(rst, k), (k, getattr(st, k), getattr(rst, k))
 
 
 @pytest.mark.parametrize("name,maker,W,H,it,seed,rf", [
@@ -89,7 +84,7 @@ def test_vcm_tiny_films_and_errors():
     path = _scenes.torus(7, 5)
     film, st = ctx(path).render_vcm(7, 5, iterations=3, seed=17, radius_factor=0.05)
     ref, rst = _oracle.Scene(path).vcm(7, 5, 3, 17, mode=1, radius_factor=0.05)
-    assert abs(st.closest_rays - rst.closest_rays) <= 2
+    assert st.closest_rays == rst.closest_rays
     assert_vcm_parity(film, ref)
     c = ctx(_scenes.torus(16, 16))
     film, st = c.render_vcm(16, 16, iterations=0)
