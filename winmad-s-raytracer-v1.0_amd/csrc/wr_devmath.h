@@ -118,7 +118,9 @@ __device__ __forceinline__ V3 sample_rect_strat(V3 s, V3 v0, V3 v1, V3 v2, int c
 __device__ __forceinline__ V3 sample_cos_hemi(V3 s, float* pdf) {  // sampler.cpp:95-108
   float u1 = 2.f * WR_PI * s.x;
   float u2 = sqrtf(1.f - s.y);
-  V3 r = v3(wr_cosf(u1) * u2, wr_sinf(u1) * u2, sqrtf(s.y));
+  float sn, cs;
+  wr_sincosf(u1, &sn, &cs);  // == glibc sinf(u1), cosf(u1)
+  V3 r = v3(cs * u2, sn * u2, sqrtf(s.y));
   *pdf = r.z * WR_INV_PI;
   return normalize(r);
 }
@@ -126,7 +128,9 @@ __device__ __forceinline__ V3 sample_pow_cos_hemi(V3 s, float power) {  // sampl
   float u1 = 2.f * WR_PI * s.x;
   float u2 = wr_powf(s.y, 1.f / (power + 1.f));
   float u3 = sqrtf(1.f - u2 * u2);
-  return normalize(v3(wr_cosf(u1) * u3, wr_sinf(u1) * u3, u2));
+  float sn, cs;
+  wr_sincosf(u1, &sn, &cs);
+  return normalize(v3(cs * u3, sn * u3, u2));
 }
 __device__ __forceinline__ float pow_cos_pdf(V3 n, V3 d, float power) {  // sampler.cpp:131-136
   float c = clampv(dot(n, d), 0.f, 1.f);

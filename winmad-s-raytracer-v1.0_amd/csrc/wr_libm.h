@@ -23,11 +23,13 @@
  * built with -ffp-contract=off).  The table constants were checked against
  * the data of the libm in this image.
  *
- * Proof of equality: oracle/libm_check.c runs these functions beside glibc's
- * over every input the renderer can give them (cos / sin of 2*PI*k/2^24 for
- * all 2^24 k, powf of every sampler value and every float cosine to the
- * scene's Phong exponents) and over every float in [-2^8, 2^8]; tests/
- * test_libm.py asserts 0 differing results (profiles/r6/libm_check.json).
+ * Proof of equality: tests/native/libm_check.c runs these functions beside
+ * glibc's over every input the renderer can give them (cos / sin of
+ * 2*PI*k/2^24 for all 2^24 k, powf of every sampler value and of every float
+ * cosine to the scenes' Phong exponents), every float in [-256, 256] and a
+ * stride of all larger ones: 1.06e10 comparisons, 0 differences
+ * (scripts/libm_check_full.sh -> profiles/r6/libm_check.json; a strided run
+ * is the CPU test tests/test_libm.py).
  *
  * Usable from C (the CPU check, compiled with gcc) and from HIP device code.
  */
@@ -185,6 +187,46 @@ WR_LIBM_FN float wr_cosf(float y) {
     return wr_lm_sinf_poly(x * s, x * x, (q & 2) != 0, n ^ 1);
   }
   return (y - y) / (y - y);
+}
+
+/* sinf(y) and cosf(y) together, each bit for bit as wr_sinf / wr_cosf (the
+ * samplers take both of one angle, sampler.cpp:100,125): one reduction, and
+ * since both polynomials are odd / even in x and the negated cosine set is
+ * the exact negation of the other, sin = +-S(x) or +-C(x^2) and cos the other,
+ * with the signs glibc's quadrant tables give. */
+WR_LIBM_FN void wr_sincosf(float y, float* sp, float* cp) {
+  double x = y;
+  int n = 0, q = 0;
+  const uint32_t top = wr_lm_abstop12(y);
+  if (top < 0x3f4) {
+    if (top < 0x398) {
+      *sp = y;
+      *cp = 1.0f;
+      return;
+    }
+  } else if (top < 0x42f) {
+    x = wr_lm_reduce_fast(x, &n);
+    q = n & 3;
+  } else if (top < 0x7f8) {
+    uint32_t xi = wr_lm_asuint(y);
+    x = wr_lm_reduce_large(xi, &n);
+    q = (n + (int)(xi >> 31)) & 3;
+  } else {
+    *sp = *cp = (y - y) / (y - y);
+    return;
+  }
+  const double x2 = x * x;
+  const float S = wr_lm_sinf_poly(x, x2, 0, 0); /* sine polynomial at +x */
+  const float C = wr_lm_sinf_poly(x, x2, 0, 1); /* cosine polynomial    */
+  const float Ss = (q == 1 || q == 2) ? -S : S; /* at x * sign[q]       */
+  const float Cs = (q & 2) ? -C : C;            /* the negated set      */
+  if (n & 1) {
+    *sp = Cs;
+    *cp = Ss;
+  } else {
+    *sp = Ss;
+    *cp = Cs;
+  }
 }
 
 /* --------------------------------------------------------------------- powf */
