@@ -241,6 +241,9 @@ def main():
                     help="global index of rank 0's first iteration (sample): one rank's shard of a bigger job, "
                          "e.g. --config c4 --steps 512 --iter-begin 512 = rank 1 of SURVEY 8(d) C5")
     ap.add_argument("--dump-film", default=None, help="rank 0 writes the reduced film here (.npy, float32 H x W x 3)")
+    ap.add_argument("--rccl-self-check", action="store_true",
+                    help="N = 1 with --backend nccl: run the library's RCCL communicator and film reduce anyway "
+                         "(the N > 1 code path on one GPU; a test of it)")
     args = ap.parse_args()
     if args.no_cut:
         os.environ["WR_TRACE_NO_CUT"] = "1"  # read by wr_create
@@ -278,6 +281,18 @@ def main():
     # (the library's default is the BVH search: the reference's walk is selected explicitly)
     ctx.set_trace_mode(native.TRACE_BVH if trace == "bvh" else native.TRACE_REFERENCE)
     film = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
+    # N > 1 over RCCL: the library's own communicator (wr_comm_init; its unique
+    # id travels over torch.distributed) reduces the films, and its size is read
+    # back from RCCL (wr_comm_info) into the line -- the job checks it spans N ranks
+    comm = None
+    if args.backend == "nccl" and (world > 1 or args.rccl_self_check):
+        uid = [native.comm_unique_id() if rank == 0 else None]
+        if dist:
+            dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(uid[0], world, rank)
+        comm = ctx.comm_info()
+        if comm != (world, rank):
+            raise SystemExit(f"RCCL communicator reports {comm}, expected ({world}, {rank})")
 
     # one step = one iteration (BDPT) / one sample index of the spp grid (PT);
     # every rank renders K of its own (weak scaling)
@@ -306,8 +321,14 @@ def main():
     t0 = time.perf_counter()
     it0 = args.iter_begin + wdist.bdpt_iteration_begin(rank, K)
     _, st = render(it0, K, film_ptr=film.data_ptr(), time_kernels=1)
-    wdist.reduce_film(film, dist)  # one film reduction per batch (RCCL)
     torch.cuda.synchronize()
+    tr0 = time.perf_counter()
+    if comm:  # one film reduction per batch: RCCL through the library (wr_film_reduce)
+        ctx.film_reduce(film.data_ptr(), film.numel(), 0)
+    else:  # gloo (ranks sharing a GPU in tests): through host memory
+        wdist.reduce_film(film, dist)
+    torch.cuda.synchronize()
+    reduce_s = time.perf_counter() - tr0
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -320,6 +341,9 @@ def main():
     trace_ms = st.kernel_ms[native.K_TRACE]
     trace_launches = st.kernel_launches[native.K_TRACE]
     elapsed, total_rays = wdist.job_totals(elapsed, rays, dist, film.device)
+    # the reduce as each rank saw it: the last rank to arrive waits for nobody,
+    # so the minimum is the collective itself, the maximum adds arrival skew
+    red_min, red_max = wdist.min_max(reduce_s, dist, film.device)
 
     roofline = None
     if not args.no_count and rank == 0:
@@ -343,6 +367,9 @@ def main():
                    "fallback_frac": round(cst.fallback_rays / rays, 5),
                    "kd_tests_per_fallback_ray": round(cst.prim_tests / max(1, cst.fallback_rays), 1)}
         per_launch = total_bytes / max(1, trace_launches)
+        # the same bytes over the driver-comparable clock: the timed steps' wall
+        # time (every kernel of the step, not only the traversal's intervals)
+        achieved_step = total_bytes / elapsed / 1e9
         # launches of the concurrent pipelines overlap: the rate is the bytes over
         # the union of the traversal launch intervals (HIP events on each stream);
         # the per-launch event average is reported beside it
@@ -395,7 +422,13 @@ def main():
                     "refs_per_ray": round(cst.prim_refs / rays, 2),
                     "tests_per_ray": round(cst.prim_tests / rays, 2),
                     "nodes_per_ray": round((cst.inner_visits + cst.leaf_visits) / rays, 2),
-                    "trace_share_of_wall": round(st.trace_wall_ms / 1e3 / max(1e-9, elapsed), 3)}
+                    "trace_share_of_wall": round(st.trace_wall_ms / 1e3 / max(1e-9, elapsed), 3),
+                    "algorithmic_bytes_per_step": round(total_bytes / K),
+                    "achieved_step": round(achieved_step, 1),
+                    "frac_step": round(achieved_step / L2_PEAK_GBS, 4),
+                    "frac_step_note": "algorithmic_bytes_per_step / ms_per_step / peak: the driver-timed form; "
+                                      "frac uses the union of the traversal launches' intervals (trace_wall_ms), "
+                                      "reproduced from a rocprofv3 kernel trace by scripts/trace_union.py"}
         if traffic:
             # measured HBM bytes per traversal step against the minimum ray I/O
             # (48 B per ray: origin, direction, hit t and primitive)
@@ -427,7 +460,10 @@ def main():
 
     cpu = port = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_reference(args.config, cfg["integrator"], W, H, tmp, 4 if args.config == "c4" else 2)
+        # the reference on the full frame for C2 (the config's
+        # resolution, fewer iterations: 1 iteration is ~35-40 s of one core);
+        # the 1M-triangle C4 at a quarter of it per axis
+        cpu = cpu_reference(args.config, cfg["integrator"], W, H, tmp, {"c4": 4, "c2": 1}.get(args.config, 2))
         budget = {"c2": args.cpu_paths, "c3": args.cpu_paths // 4, "c4": args.cpu_paths // 20,
                   "vcm": args.cpu_paths // 2, "sph": args.cpu_paths // 4}[args.config]
         port = cpu_baseline(cfg["integrator"], scene_path, W, H, budget)
@@ -455,7 +491,16 @@ def main():
             "spp_per_sec": round(W * H * K * world / elapsed, 1),
             "rays_per_step": round(total_rays / (K * world)),
             "roofline": roofline, "cpu_baseline": cpu,
+            "lib_sha": native.library_sha16(),
         }
+        if world > 1 or comm:
+            out["rccl_ranks"] = comm[0] if comm else None  # from ncclCommCount (wr_comm_info)
+            out["reduce_ms"] = round(red_min * 1e3, 3)
+            out["reduce_ms_max"] = round(red_max * 1e3, 3)
+            out["reduce"] = ("wr_film_reduce (RCCL reduce-sum of the H x W x 3 fp32 film to rank 0, "
+                             f"{H * W * 12 / 1e6:.1f} MB), inside the timed region; reduce_ms = fastest rank "
+                             "(the collective), reduce_ms_max = slowest (plus arrival skew)") if comm else \
+                ("gloo reduce through host memory (ranks sharing a GPU)")
         if trace == "bvh":
             out["trace_note"] = ("verified BVH traversal: every ray gets the reference KD walk's (t, primitive) "
                                  "answer, bit for bit (argument in DESIGN.md 4b; rays running inside the plane of a "

@@ -227,6 +227,9 @@ int wr_comm_init(wr_context* ctx, const uint8_t id[128], int nranks, int rank);
  * rank `root`'s film, in place; collective (every rank calls it).  Ordered
  * after the caller's work on the legacy null stream; returns when done. */
 int wr_film_reduce(wr_context* ctx, float* film_dev, int64_t nfloat, int root);
+/* The communicator's size and this rank, read back from RCCL (ncclCommCount,
+ * ncclCommUserRank): a bench or driver checks the job really spans N ranks. */
+int wr_comm_info(const wr_context* ctx, int* nranks, int* rank);
 /* Concurrent render pipelines (HIP streams, each with its own work buffers,
  * ~5 GB per pair of iterations at 1080p): iterations / samples are dealt
  * round-robin to them so that one stream's late-bounce traversal tail overlaps

@@ -46,6 +46,10 @@ def test_bench_line(cfg):
     assert r["bound"] == "l2" and r["peak"] > 0 and r["achieved"] > 0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) <= 1e-3 * max(r["frac"], 1e-9) + 1e-4
     assert 0 < r["frac"] <= 1, r["frac"]  # a fraction of a peak the kernel can actually meet
+    # the driver-timed form: the step's algorithmic bytes over ms_per_step
+    assert abs(r["achieved_step"] - r["algorithmic_bytes_per_step"] / d["ms_per_step"] / 1e6) \
+        <= 1e-2 * r["achieved_step"]
+    assert 0 < r["frac_step"] <= r["frac"] * 1.001
     if r.get("hbm"):
         assert 0 < r["hbm"]["frac"] <= 1 and r["hbm"]["peak"] == 8000.0
 
@@ -69,3 +73,14 @@ def test_bench_reference_trace_is_the_kd_walk():
     assert d["config"]["trace"] == "reference"
     assert d["roofline"]["kernel"].startswith("k_trace (KD"), d["roofline"]["kernel"]
     assert "bvh" not in d["roofline"]
+
+
+@pytest.mark.gpu
+def test_bench_rccl_self_check_reads_the_communicator():
+    """The N > 1 reduce path on one GPU: the library's RCCL communicator
+    (wr_comm_init) over one rank, its size read back from RCCL (wr_comm_info)
+    into the line, and the film reduce (wr_film_reduce) timed."""
+    d = run_bench("--config", "c2", "--rccl-self-check", "--no-compare", "--no-count")
+    assert d["rccl_ranks"] == 1
+    assert d["reduce_ms"] > 0 and d["reduce_ms_max"] >= d["reduce_ms"]
+    assert d["reduce"].startswith("wr_film_reduce")

@@ -658,6 +658,8 @@ struct RcclApi {
   ncclResult_t (*group_end)() = nullptr;
   ncclResult_t (*destroy)(ncclComm_t) = nullptr;
   const char* (*err_str)(ncclResult_t) = nullptr;
+  ncclResult_t (*count)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*user_rank)(const ncclComm_t, int*) = nullptr;
 };
 const RcclApi& rccl() {
   static const RcclApi api = [] {
@@ -676,7 +678,8 @@ const RcclApi& rccl() {
     };
     a.ok = sym(a.get_unique_id, "ncclGetUniqueId") && sym(a.init_rank, "ncclCommInitRank") &&
            sym(a.init_all, "ncclCommInitAll") && sym(a.reduce, "ncclReduce") && sym(a.group_start, "ncclGroupStart") &&
-           sym(a.group_end, "ncclGroupEnd") && sym(a.destroy, "ncclCommDestroy") && sym(a.err_str, "ncclGetErrorString");
+           sym(a.group_end, "ncclGroupEnd") && sym(a.destroy, "ncclCommDestroy") && sym(a.err_str, "ncclGetErrorString") &&
+           sym(a.count, "ncclCommCount") && sym(a.user_rank, "ncclCommUserRank");
     if (!a.ok) a.why = "RCCL lacks an entry point";
     return a;
   }();
@@ -3176,6 +3179,16 @@ int wr_comm_init(wr_context* c, const uint8_t id[128], int nranks, int rank) {
   NCCLCHK(rccl().init_rank(&c->comm, nranks, u, rank));
   c->comm_ranks = nranks;
   c->comm_rank = rank;
+  return WR_OK;
+}
+
+int wr_comm_info(const wr_context* c, int* nranks, int* rank) {
+  if (!c || !nranks || !rank) return fail(WR_E_ARG, "null argument");
+  if (!c->comm) return fail(WR_E_ARG, "no communicator: call wr_comm_init first");
+  // read back from the communicator itself (ncclCommCount / ncclCommUserRank),
+  // not from what wr_comm_init was given
+  NCCLCHK(rccl().count(c->comm, nranks));
+  NCCLCHK(rccl().user_rank(c->comm, rank));
   return WR_OK;
 }
 

@@ -64,3 +64,17 @@ def job_totals(elapsed_s, rays, dist, device="cpu"):
     r = torch.tensor([float(rays)], dtype=torch.float64, device=device)
     dist.all_reduce(r, op=dist.ReduceOp.SUM)
     return float(t.item()), float(r.item())
+
+
+def min_max(value, dist, device="cpu"):
+    """(min, max) of a per-rank float over the ranks (identity for one rank)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(value), float(value)
+    import torch
+    if _host_backend(dist):
+        device = "cpu"
+    lo = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    hi = lo.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return float(lo.item()), float(hi.item())

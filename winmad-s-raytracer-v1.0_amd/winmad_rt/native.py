@@ -22,7 +22,7 @@ INTEGRATOR_BDPT, INTEGRATOR_VCM, INTEGRATOR_PATH = 0, 1, 2
 # every entry point declared in include/winmad_rt.h
 EXPORTS = ["wr_scene_load", "wr_scene_from_desc", "wr_scene_info_get", "wr_scene_fingerprint", "wr_scene_dump", "wr_scene_free",
            "wr_device_count", "wr_create", "wr_create_multi", "wr_context_devices", "wr_destroy", "wr_comm_unique_id",
-           "wr_comm_init", "wr_film_reduce", "wr_set_pipelines", "wr_set_trace_mode", "wr_trace_closest", "wr_occluded",
+           "wr_comm_init", "wr_comm_info", "wr_film_reduce", "wr_set_pipelines", "wr_set_trace_mode", "wr_trace_closest", "wr_occluded",
            "wr_render_bdpt", "wr_render_path", "wr_render_vcm", "wr_path_radiance", "wr_film_write_ppm",
            "wr_film_write_image", "wr_checkpoint_save", "wr_checkpoint_load", "wr_last_error", "wr_api_version",
            "wr_reserve", "wr_request_hw_queues"]
@@ -164,6 +164,7 @@ def lib():
         L.wr_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.wr_comm_init.argtypes = [P, C.POINTER(C.c_uint8), I, I]
         L.wr_film_reduce.argtypes = [P, P, I64, I]
+        L.wr_comm_info.argtypes = [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.wr_checkpoint_save.argtypes = [C.c_char_p, C.POINTER(WrCheckpointInfo), C.POINTER(C.c_float)]
         L.wr_checkpoint_load.argtypes = [C.c_char_p, C.POINTER(WrCheckpointInfo), C.POINTER(C.c_float), I64]
         L.wr_scene_info_get.argtypes = [P, C.POINTER(WrSceneInfo)]
@@ -341,6 +342,12 @@ class Context:
         """wr_comm_init: this rank's RCCL communicator (one process per GPU)."""
         idb = (C.c_uint8 * 128)(*bytes(unique_id))
         check(lib().wr_comm_init(self.h, idb, nranks, rank))
+
+    def comm_info(self):
+        """wr_comm_info: (ranks, this rank) as the RCCL communicator reports them."""
+        n, r = C.c_int(0), C.c_int(0)
+        check(lib().wr_comm_info(self.h, C.byref(n), C.byref(r)))
+        return n.value, r.value
 
     def film_reduce(self, film_ptr, nfloat, root=0):
         """wr_film_reduce: sum the ranks' device films into rank `root`'s, in place."""
