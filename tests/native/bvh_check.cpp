@@ -145,12 +145,25 @@ int main(int argc, char** argv) {
       s4.pop_back();
       if (++visits > f.nodes4.size()) return fail("4-wide tree has a cycle");
       maxd4 = std::max(maxd4, it.depth);
-      const wrf::BNode4& n = f.nodes4[static_cast<size_t>(it.node)];
+      const auto& n = f.nodes4[static_cast<size_t>(it.node)];
       for (int k = 0; k < 4; ++k) {
+#if WR_BVH4_QUANT
+        // BNode4Q: the decoded box fmaf(q, scale, org) of the slot (unused
+        // slots: kEmptyLink); containment of the binary boxes is checked below
+        if (n.c[k] == wrf::kEmptyLink) continue;
+        float lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+          if (!(n.scale[a] > 0.f)) return fail("4-wide quantised scale");
+          lo[a] = std::fma(static_cast<float>(n.qlo[a][k]), n.scale[a], n.org[a]);
+          hi[a] = std::fma(static_cast<float>(n.qhi[a][k]), n.scale[a], n.org[a]);
+          if (lo[a] > hi[a]) return fail("4-wide decoded box inverted");
+        }
+#else
         const float lo[3] = {n.lo[0][k], n.lo[1][k], n.lo[2][k]}, hi[3] = {n.hi[0][k], n.hi[1][k], n.hi[2][k]};
         if (empty_slot(lo[0], hi[0])) continue;
         for (int a = 0; a < 3; ++a)
           if (lo[a] < it.lo[a] || hi[a] > it.hi[a]) return fail("4-wide child box outside its parent's");
+#endif
         if (n.c[k] >= 0) {
           if (static_cast<size_t>(n.c[k]) >= f.nodes4.size()) return fail("4-wide link out of range");
           s4.push_back(It4{n.c[k], it.depth + 1, {lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}});
@@ -163,9 +176,54 @@ int main(int argc, char** argv) {
     std::sort(want.begin(), want.end());
     std::sort(got.begin(), got.end());
     if (want.size() != got.size()) return fail("4-wide tree leaf count");
+#if WR_BVH4_QUANT
+    // the same leaves, each decoded leaf box CONTAINING the binary one; each
+    // decoded inner box containing every binary leaf box beneath it
+    for (size_t i = 0; i < want.size(); ++i) {
+      if (want[i].first != got[i].first) return fail("4-wide tree leaves differ from the binary tree's");
+      for (int a = 0; a < 3; ++a)
+        if (got[i].second[a] > want[i].second[a] || got[i].second[3 + a] < want[i].second[3 + a])
+          return fail("4-wide decoded leaf box does not contain the binary box");
+    }
+    {
+      std::map<int, std::vector<float>> leaf_box(want.begin(), want.end());
+      // union of the binary leaf boxes under a 4-wide node, checked against the
+      // decoded box of every inner slot on the way
+      std::function<bool(int, float*)> sub = [&](int node, float* u) -> bool {
+        for (int a = 0; a < 3; ++a) {
+          u[a] = INFINITY;
+          u[3 + a] = -INFINITY;
+        }
+        const auto& n = f.nodes4[static_cast<size_t>(node)];
+        for (int k = 0; k < 4; ++k) {
+          if (n.c[k] == wrf::kEmptyLink) continue;
+          float b[6];
+          if (n.c[k] >= 0) {
+            if (!sub(n.c[k], b)) return false;
+            for (int a = 0; a < 3; ++a) {
+              const float lo = std::fma(static_cast<float>(n.qlo[a][k]), n.scale[a], n.org[a]);
+              const float hi = std::fma(static_cast<float>(n.qhi[a][k]), n.scale[a], n.org[a]);
+              if (lo > b[a] || hi < b[3 + a]) return false;
+            }
+          } else {
+            const std::vector<float>& lb = leaf_box[n.c[k]];
+            for (int a = 0; a < 6; ++a) b[a] = lb[static_cast<size_t>(a)];
+          }
+          for (int a = 0; a < 3; ++a) {
+            u[a] = std::min(u[a], b[a]);
+            u[3 + a] = std::max(u[3 + a], b[3 + a]);
+          }
+        }
+        return true;
+      };
+      float u[6];
+      if (!sub(0, u)) return fail("4-wide decoded inner box does not contain its subtree's leaf boxes");
+    }
+#else
     for (size_t i = 0; i < want.size(); ++i)
       if (want[i].first != got[i].first || std::memcmp(want[i].second.data(), got[i].second.data(), 24) != 0)
         return fail("4-wide tree leaves differ from the binary tree's");
+#endif
   }
   // 2c. the 8-wide tree (built with -DWR_BVH_WIDE=8 only): the same leaves,
   //     each once, every decoded child box fmaf(q, scale, org) CONTAINING the

@@ -18,13 +18,14 @@ CSRC = os.path.join(REPO, "winmad-s-raytracer-v1.0_amd", "csrc")
 _bin = {}
 
 
-def checker(wide=None):
+def checker(wide=None, quant=False):
     """The checker built from the product's sources; wide=4 / 8 builds the 4- / 8-wide
-    search tree (WR_BVH_WIDE=4) as well and checks it against the binary one."""
-    key = wide or "default"
+    search tree (WR_BVH_WIDE=4) as well and checks it against the binary one;
+    quant: the 4-wide tree of byte-quantised nodes (WR_BVH4_QUANT=1)."""
+    key = f"{wide or 'default'}{'q' if quant else ''}"
     if key not in _bin:
         out = os.path.join(tempfile.mkdtemp(prefix="wr_bvhchk_"), "bvh_check")
-        flags = [f"-DWR_BVH_WIDE={wide}"] if wide else []
+        flags = ([f"-DWR_BVH_WIDE={wide}"] if wide else []) + (["-DWR_BVH4_QUANT=1"] if quant else [])
         subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", *flags, "-I", CSRC, "-I",
                         os.path.join(REPO, "include"), os.path.join(REPO, "tests", "native", "bvh_check.cpp"),
                         os.path.join(CSRC, "wr_scene.cpp"), os.path.join(CSRC, "wr_bvh.cpp"), "-o", out, "-lpthread"],
@@ -72,6 +73,16 @@ def test_bvh_parallel_build_equals_serial():
 
 def test_bvh_wide_tree_structure():
     r = subprocess.run([checker(4), _scenes.torus(64, 64)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("maker", [lambda: _scenes.torus(64, 64), small_torus, lambda: _scenes.spheres(64, 64)],
+                         ids=["torus", "synthetic_torus_40k", "spheres"])
+def test_bvh_4wide_quantised_tree_structure(maker):
+    """The 64-byte 4-wide node (WR_BVH4_QUANT=1, round 6: measured and left off
+    by default): the binary tree's leaves, each once, every decoded leaf box
+    containing the binary one and every decoded inner box its subtree's."""
+    r = subprocess.run([checker(4, quant=True), maker()], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
 
 

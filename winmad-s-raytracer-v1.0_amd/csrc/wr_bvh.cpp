@@ -453,6 +453,50 @@ void kd_paths(const wr::Scene& s, FastHost& out) {
   }
 }
 
+// One axis of a quantised node (BNode4Q, BNode8): the grid (org, scale) and
+// each child's bytes, with the decoded faces fmaf(q, scale, org) holding the
+// child's [lo, hi] -- checked with the same correctly rounded fmaf the device
+// decodes with.
+void quantise_axis(const float* clo, const float* chi, int n, float& org, float& scale, uint8_t* qlo, uint8_t* qhi) {
+  float lo = INFINITY, hi = -INFINITY;
+  for (int i = 0; i < n; ++i) {
+    lo = std::min(lo, clo[i]);
+    hi = std::max(hi, chi[i]);
+  }
+  if (n == 0) {
+    org = 0.f;
+    scale = 1.f;
+    return;
+  }
+  // the smallest power of two with (hi - lo) / scale <= 254 (one step spare
+  // for the outward corrections below)
+  int e = -126;
+  const double ext = static_cast<double>(hi) - static_cast<double>(lo);
+  while (std::ldexp(254.0, e) < ext) ++e;
+  for (;; ++e) {
+    const float sc = std::ldexp(1.f, e);
+    bool ok = true;
+    for (int i = 0; i < n && ok; ++i) {
+      double ql = std::floor((static_cast<double>(clo[i]) - lo) / sc);
+      double qh = std::ceil((static_cast<double>(chi[i]) - lo) / sc);
+      ql = std::max(0.0, ql);
+      while (ql > 0 && std::fma(static_cast<float>(ql), sc, lo) > clo[i]) ql -= 1;
+      while (qh <= 255 && std::fma(static_cast<float>(qh), sc, lo) < chi[i]) qh += 1;
+      if (std::fma(static_cast<float>(ql), sc, lo) > clo[i] || qh > 255) {
+        ok = false;
+        break;
+      }
+      qlo[i] = static_cast<uint8_t>(ql);
+      qhi[i] = static_cast<uint8_t>(qh);
+    }
+    if (ok) {
+      org = lo;
+      scale = sc;
+      return;
+    }
+  }
+}
+
 // The 4-wide tree: each node takes its binary node's children and opens the
 // inner child of largest area until it holds four (or only leaves remain).
 struct Collapse {
@@ -493,10 +537,30 @@ struct Collapse {
       ks[best] = kid(open, 0);
       ks[n++] = kid(open, 1);
     }
+#if WR_BVH4_QUANT
+    int m = 0;  // drop empty children (the binary root of a tiny scene)
+    for (int i = 0; i < n; ++i)
+      if (!(!(ks[i].lo[0] <= ks[i].hi[0]) || (ks[i].lo[0] == 3e38f && ks[i].hi[0] == 3e38f))) ks[m++] = ks[i];
+    n = m;
+#endif
     const int at = static_cast<int>(out.nodes4.size());
     out.nodes4.emplace_back();
     int links[4];
     for (int i = 0; i < 4; ++i) links[i] = i < n && ks[i].link >= 0 ? node(ks[i].link, depth + 1) : (i < n ? ks[i].link : ~0);
+#if WR_BVH4_QUANT
+    BNode4Q& q = out.nodes4[static_cast<size_t>(at)];
+    std::memset(&q, 0, sizeof q);
+    for (int i = 0; i < 4; ++i) q.c[i] = i < n ? links[i] : kEmptyLink;
+    float lo[4], hi[4];
+    for (int a = 0; a < 3; ++a) {
+      for (int i = 0; i < n; ++i) {
+        lo[i] = ks[i].lo[a];
+        hi[i] = ks[i].hi[a];
+      }
+      quantise_axis(lo, hi, n, q.org[a], q.scale[a], q.qlo[a], q.qhi[a]);
+    }
+    return at;
+#else
     BNode4& d = out.nodes4[static_cast<size_t>(at)];
     for (int i = 0; i < 4; ++i) {
       // an empty slot is a point far outside every scene: its slab interval is
@@ -511,6 +575,7 @@ struct Collapse {
       d.pad[i] = 0;
     }
     return at;
+#endif
   }
 };
 

@@ -57,6 +57,32 @@ struct BNode4 {
 };
 static_assert(sizeof(BNode4) == 128, "4-wide BVH node is 128 bytes");
 
+// 64 bytes (half a cache line): the 4-wide node with its child boxes quantised
+// to bytes on a per-node grid as BNode8 does (decoded fmaf(q, scale[a],
+// org[a]), each decoded box containing the binary tree's box bit for bit) --
+// twice the nodes per line of BNode4, for scenes whose tree outgrows the L2.
+// Layout (float4 words):
+//   [0] org.xyz, scale.x    [1] scale.y, scale.z, qlo.x[0..3], qlo.y[0..3]
+//   [2] qlo.z[0..3], qhi.x[0..3], qhi.y[0..3], qhi.z[0..3]
+//   [3] c[0..3]  (links as in BNode; kEmptyLink: no child in the slot)
+struct BNode4Q {
+  float org[3];
+  float scale[3];
+  uint8_t qlo[3][4];
+  uint8_t qhi[3][4];
+  int32_t c[4];
+};
+static_assert(sizeof(BNode4Q) == 64, "quantised 4-wide BVH node is 64 bytes");
+constexpr int32_t kEmptyLink = static_cast<int32_t>(0x80000000u);  // BNode4Q: an unused child slot
+#ifndef WR_BVH4_QUANT
+#define WR_BVH4_QUANT 0  // 1: the 4-wide search reads BNode4Q (measured C4 -1.3 %)
+#endif
+#if WR_BVH4_QUANT
+using BNode4S = BNode4Q;  // the 4-wide search's node
+#else
+using BNode4S = BNode4;
+#endif
+
 // 128 bytes (one cache line): an 8-wide node of the search, collapsed from the
 // binary BVH (same leaves), with child boxes quantised to bytes on a per-node
 // grid.  Child k's face on axis a is decoded as fmaf(q, scale[a], org[a]) (one
@@ -141,7 +167,7 @@ struct Scene;
 namespace wrf {
 struct FastHost {
   std::vector<BNode> nodes;
-  std::vector<BNode4> nodes4;  // the search's tree (root 0)
+  std::vector<BNode4S> nodes4;  // the search's tree (root 0)
   int depth4 = 0;              // deepest 4-wide node chain
   std::vector<BNode8> nodes8;  // WR_BVH_WIDE 8: the search's tree (root 0)
   int depth8 = 0;              // deepest 8-wide node chain

@@ -38,7 +38,7 @@ namespace wrd {
 
 struct FastScene {
   const float4* nodes;  // 4 per wrf::BNode (tie resolution's collection)
-  const float4* nodes4;  // 8 per wrf::BNode4 (the search when wide == 4)
+  const float4* nodes4;  // 4 per wrf::BNode4Q / 8 per wrf::BNode4 (wrf::BNode4S: the search when wide == 4)
   const float4* nodes8;  // 8 per wrf::BNode8 (the search when wide == 8)
   int wide;              // the search tree's width: 2 (nodes), 4 (nodes4) or 8 (nodes8)
   const float4* tris;   // 3 per wrf::TriRec
@@ -1549,6 +1549,33 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         if constexpr (W == 4) {
         // a 4-wide node: the four boxes, then the hit children nearest first
         // (the nearest is visited next, the others pushed farthest first)
+#if WR_BVH4_QUANT
+        // wrf::BNode4Q: the child boxes decoded from bytes, fmaf(q, scale,
+        // org) -- each contains the binary tree's box, bit for bit checked
+        // by the build -- then tested as below; an unused slot never hits
+        const float4* np = F.nodes4 + 4 * static_cast<size_t>(cur);
+        const float4 h0 = np[0], h1 = np[1], h2 = np[2];
+        const int4 lk = *reinterpret_cast<const int4*>(np + 3);
+        const uint32_t qlx = __float_as_uint(h1.z), qly = __float_as_uint(h1.w), qlz = __float_as_uint(h2.x);
+        const uint32_t qhx = __float_as_uint(h2.y), qhy = __float_as_uint(h2.z), qhz = __float_as_uint(h2.w);
+        auto dq = [](uint32_t w, int k, float sc, float org) {
+          return fmaf(static_cast<float>((w >> (8 * k)) & 255u), sc, org);
+        };
+        auto slabq = [&](int k, int link) {
+          const float lx = dq(qlx, k, h0.w, h0.x), ly = dq(qly, k, h1.x, h0.y), lz = dq(qlz, k, h1.y, h0.z);
+          const float hx = dq(qhx, k, h0.w, h0.x), hy = dq(qhy, k, h1.x, h0.y), hz = dq(qhz, k, h1.y, h0.z);
+          const float x0 = fmaf(lx, binv.x, cl.x), x1 = fmaf(hx, binv.x, ch.x);
+          const float y0 = fmaf(ly, binv.y, cl.y), y1 = fmaf(hy, binv.y, ch.y);
+          const float z0 = fmaf(lz, binv.z, cl.z), z1 = fmaf(hz, binv.z, ch.z);
+          const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), lo_t));
+          const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), hi_t));
+          return (tn <= tf && link != wrf::kEmptyLink) ? tn : __int_as_float(0x7f800000);
+        };
+        float k0 = slabq(0, lk.x);
+        float k1 = slabq(1, lk.y);
+        float k2 = slabq(2, lk.z);
+        float k3 = slabq(3, lk.w);
+#else
         const float4* np = F.nodes4 + 8 * static_cast<size_t>(cur);
         const float4 bx0 = np[0], by0 = np[1], bz0 = np[2], bx1 = np[3], by1 = np[4], bz1 = np[5];
         const int4 lk = *reinterpret_cast<const int4*>(np + 6);
@@ -1564,6 +1591,7 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
         float k1 = slab4(bx0.y, by0.y, bz0.y, bx1.y, by1.y, bz1.y);
         float k2 = slab4(bx0.z, by0.z, bz0.z, bx1.z, by1.z, bz1.z);
         float k3 = slab4(bx0.w, by0.w, bz0.w, bx1.w, by1.w, bz1.w);
+#endif
         int l0 = lk.x, l1 = lk.y, l2 = lk.z, l3 = lk.w;
         const int nh = (k0 < __int_as_float(0x7f800000)) + (k1 < __int_as_float(0x7f800000)) +
                        (k2 < __int_as_float(0x7f800000)) + (k3 < __int_as_float(0x7f800000));

@@ -1870,7 +1870,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       const size_t fbytes = measure([&](Arena& a) {
         a.take<wrf::BNode>(fbn); a.take<wrf::TriRec>(ftr); a.take<int>(fpo); a.take<int>(fpl); a.take<int>(fpl);
         a.take<uint2>(fpa); a.take<int>(fnp); a.take<float4>(2 * fnp); a.take<wrf::PrimRec>(fh.prim_rec.size());
-        a.take<wrf::BNode4>(fh.nodes4.size());
+        a.take<wrf::BNode4S>(fh.nodes4.size());
         a.take<wrf::BNode8>(fh.nodes8.size());
       });
       if (int rc = c->fast_mem.reserve(fbytes)) {
@@ -1887,7 +1887,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
       int* dnp = F.take<int>(fnp);
       float4* dnc = F.take<float4>(2 * fnp);
       auto* dpr = F.take<wrf::PrimRec>(fh.prim_rec.size());
-      auto* dn4 = F.take<wrf::BNode4>(fh.nodes4.size());
+      auto* dn4 = F.take<wrf::BNode4S>(fh.nodes4.size());
       auto* dn8 = F.take<wrf::BNode8>(fh.nodes8.size());
       hipError_t fe = hipSuccess;
       for (hipError_t x : {hipMemcpy(dno, fh.nodes.data(), fbn * sizeof(wrf::BNode), hipMemcpyHostToDevice),
@@ -1901,7 +1901,7 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                            hipMemcpy(dnc, fh.node_cell.data(), 8 * fnp * sizeof(float), hipMemcpyHostToDevice),
                            hipMemcpy(dpr, fh.prim_rec.data(), fh.prim_rec.size() * sizeof(wrf::PrimRec),
                                      hipMemcpyHostToDevice),
-                           hipMemcpy(dn4, fh.nodes4.data(), fh.nodes4.size() * sizeof(wrf::BNode4),
+                           hipMemcpy(dn4, fh.nodes4.data(), fh.nodes4.size() * sizeof(wrf::BNode4S),
                                      hipMemcpyHostToDevice),
                            hipMemcpy(dn8, fh.nodes8.data(), fh.nodes8.size() * sizeof(wrf::BNode8),
                                      hipMemcpyHostToDevice)})
