@@ -47,7 +47,7 @@ L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2, 8 XCDs x 4 MiB, ~34.5 TB/s agg
 # (profiles/<round>/traffic_<config>.json; C2's older rounds: traffic.json);
 # the newest round's file wins and its name is in the line (traffic_source).
 PROFILES = os.path.join(REPO, "profiles")
-ROUNDS = ("r5", "r4", "r3", "r2", "r1")
+ROUNDS = ("r6", "r5", "r4", "r3", "r2", "r1")
 
 
 def pmc_traffic(config):

@@ -47,6 +47,36 @@ __device__ __forceinline__ void st3r(float* s, int p, int k, V3 v) {
   r[2] = v.z;
 }
 
+// BDPT's own subpath record (VertexCM keeps PS_*): 32 bytes per path, half a
+// PS record.  The subpath's origin and direction are not kept: the reference
+// overwrites both in sampleScattering before any read (bidirPathTracing.cpp:
+// 381-400 -- bsdf.sample writes the direction, origin = hitPos), and the next
+// ray travels in the extension queue.  The small counters share one word:
+//   BQ_PACK = len | nspec << 8 | stored vertices << 16 (light: light vertices,
+//   camera: camera vertices of the overlapped schedule)
+enum : int { BQ_THR = 0, BQ_DVCM = 3, BQ_DVC = 4, BQ_CTR = 5, BQ_PACK = 6, BQ_PIX = 7, BQ_WORDS = 8 };
+__device__ __forceinline__ float& bqf(float* s, int p, int k) { return s[size_t(p) * BQ_WORDS + k]; }
+__device__ __forceinline__ int& bqi(float* s, int p, int k) {
+  return reinterpret_cast<int*>(s)[size_t(p) * BQ_WORDS + k];
+}
+__device__ __forceinline__ uint32_t& bqu(float* s, int p, int k) {
+  return reinterpret_cast<uint32_t*>(s)[size_t(p) * BQ_WORDS + k];
+}
+__device__ __forceinline__ V3 bqld3(const float* s, int p, int k) {
+  const float* r = s + size_t(p) * BQ_WORDS + k;
+  return v3(r[0], r[1], r[2]);
+}
+__device__ __forceinline__ void bqst3(float* s, int p, int k, V3 v) {
+  float* r = s + size_t(p) * BQ_WORDS + k;
+  r[0] = v.x;
+  r[1] = v.y;
+  r[2] = v.z;
+}
+__device__ __forceinline__ int bq_pack(int len, int nspec, int cnt) { return len | (nspec << 8) | (cnt << 16); }
+__device__ __forceinline__ int bq_len(int w) { return w & 255; }
+__device__ __forceinline__ int bq_nspec(int w) { return (w >> 8) & 255; }
+__device__ __forceinline__ int bq_count(int w) { return w >> 16; }
+
 // Stored light vertices (lightStates, bidirPathTracing.cpp:101-102), one
 // 80-byte record per vertex slot k * P + p: the camera pass reads a path's
 // vertices by path index (connectVertices, :219-257).
@@ -239,15 +269,11 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_light_gen(BdptGro
     epdf *= lpp;
     dpdf *= lpp;
     thr = div_plain(thr, epdf);
-    st3r(B.ls, p, PS_O, pos);
-    st3r(B.ls, p, PS_D, dir);
-    st3r(B.ls, p, PS_THR, thr);
-    psf(B.ls, p, PS_DVCM) = dpdf / epdf;
-    psf(B.ls, p, PS_DVC) = 1.f / epdf;  // AreaLight::isDelta() == 0
-    psi(B.ls, p, PS_LEN) = 1;
-    psi(B.ls, p, PS_NSPEC) = 0;
-    psu(B.ls, p, PS_CTR) = rng.ctr;
-    psi(B.ls, p, PS_VCOUNT) = 0;
+    bqst3(B.ls, p, BQ_THR, thr);
+    bqf(B.ls, p, BQ_DVCM) = dpdf / epdf;
+    bqf(B.ls, p, BQ_DVC) = 1.f / epdf;  // AreaLight::isDelta() == 0
+    bqu(B.ls, p, BQ_CTR) = rng.ctr;
+    bqi(B.ls, p, BQ_PACK) = bq_pack(1, 0, 0);  // pathLength 1, no specular vertex, no stored vertex
     // Ray(origin + dir * EPS, dir) (:79-80)
     st3(B.q_o[0], B.qs, p, pos + dir * WR_EPS);
     st3(B.q_d[0], B.qs, p, normalize(dir));
@@ -381,14 +407,15 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
     Bsdf b;
     bsdf_init(b, -d, h.n, h.mat, S.mats);
     if (b.mat != 0) {
-      float dvcm = psf(B.ls, p, PS_DVCM), dvc = psf(B.ls, p, PS_DVC);
-      int len = psi(B.ls, p, PS_LEN), nspec = psi(B.ls, p, PS_NSPEC);
-      V3 thr = ld3r(B.ls, p, PS_THR);
+      float dvcm = bqf(B.ls, p, BQ_DVCM), dvc = bqf(B.ls, p, BQ_DVC);
+      const int pk = bqi(B.ls, p, BQ_PACK);
+      int len = bq_len(pk), nspec = bq_nspec(pk), nstored = bq_count(pk);
+      V3 thr = bqld3(B.ls, p, BQ_THR);
       dvcm *= (t * t);  // pathLength > 1 || isFiniteLight: always for area lights (:94-97)
       dvcm /= fabsf(b.wi.z);
       dvc /= fabsf(b.wi.z);
       if (!b.delta) {  // lightStates.push_back (:101-102)
-        const int k = psi(B.ls, p, PS_VCOUNT);
+        const int k = nstored;
         int slot = k * P + p;
         if (B.vidx) {  // a pool record (the storing lanes of the wave take theirs together)
           slot = pool_take(A, &A.sc->vpool, B.vcap);
@@ -408,11 +435,11 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
           vsi(B.vs, slot, VS_NSPEC) = nspec;
           vsi(B.vs, slot, VS_MAT) = b.mat;
         }
-        psi(B.ls, p, PS_VCOUNT) = k + 1;
+        nstored = k + 1;
         if (A.overlap && slot >= 0) {  // the camera vertices stored at earlier steps (lengths < len)
           lslot = slot;
           llen = len;
-          lconn = psi(B.cs, p, PS_CVCOUNT);
+          lconn = bq_count(bqi(B.cs, p, BQ_PACK));
         }
         if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
           const DCam& cam = S.cam;
@@ -459,23 +486,21 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
         }
       }
       if (!(len + 2 > A.maxlen)) {  // (:123-127)
-        Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), psu(B.ls, p, PS_CTR)};
-        V3 lo = ld3r(B.ls, p, PS_O), ld = ld3r(B.ls, p, PS_D);
+        Rng rng{stream_key(A.seed, A.iter, 0, static_cast<uint32_t>(A.base + p)), bqu(B.ls, p, BQ_CTR)};
+        V3 lo{}, ld{};  // sampleScattering's origin and direction (outputs only)
         if (sample_scatter(S, rng, b, h.p, lo, ld, thr, dvcm, dvc, nspec)) {
           ext = true;
           ++len;
           e_o = lo + ld * WR_EPS;
           e_d = normalize(ld);
-          st3r(B.ls, p, PS_O, lo);
-          st3r(B.ls, p, PS_D, ld);
-          st3r(B.ls, p, PS_THR, thr);
-          psf(B.ls, p, PS_DVCM) = dvcm;
-          psf(B.ls, p, PS_DVC) = dvc;
-          psi(B.ls, p, PS_LEN) = len;
-          psi(B.ls, p, PS_NSPEC) = nspec;
+          bqst3(B.ls, p, BQ_THR, thr);
+          bqf(B.ls, p, BQ_DVCM) = dvcm;
+          bqf(B.ls, p, BQ_DVC) = dvc;
         }
-        psu(B.ls, p, PS_CTR) = rng.ctr;
+        bqu(B.ls, p, BQ_CTR) = rng.ctr;
       }
+      // len / nspec of the next vertex (when it scatters), the stored vertices
+      if (ext || nstored != bq_count(pk)) bqi(B.ls, p, BQ_PACK) = bq_pack(len, nspec, nstored);
     }
   }
   const int ei = wave_append(&A.sc->ext[oslot], ext);
@@ -575,6 +600,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_SHADE_OCC k_light_shade(BdptGr
 // generateCameraSample (:418-452) + first extension ray, for queue entry s of
 // the piece; returns the path's local index.  (VertexCM::generateCameraSample,
 // vertexcm.cpp:446-479, is the same plus dVM = 0.)
+template <bool VCM = false>
 __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s, int ebase = 0) {
   const BdptBuf& B = A.B;
   const DCam& cam = A.S.cam;
@@ -602,16 +628,25 @@ __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s, int ebas
   const float cos_at = dot(cam.fwd, d);
   const float ipd = cam.plane_dist / cos_at;
   const float i2sa = (ipd * ipd) / cos_at;
-  st3r(B.cs, l, PS_O, cam.pos);
-  st3r(B.cs, l, PS_D, d);
-  st3r(B.cs, l, PS_THR, v3(1.f, 1.f, 1.f));
-  psf(B.cs, l, PS_DVCM) = static_cast<float>(A.P) / i2sa;  // lightPathNum / cameraPdf
-  psf(B.cs, l, PS_DVC) = 0.f;
-  psi(B.cs, l, PS_LEN) = 1;
-  psi(B.cs, l, PS_NSPEC) = 0;
-  psu(B.cs, l, PS_CTR) = rng.ctr;
-  psi(B.cs, l, PS_PIX) = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
-  psi(B.cs, l, PS_CVCOUNT) = 0;  // (BDPT only: VertexCM's camera gen sets PS_DVM here after this)
+  const int pix = pix_index(static_cast<int>(sx), static_cast<int>(sy), A.H, A.W);  // (:263)
+  if (VCM) {
+    st3r(B.cs, l, PS_O, cam.pos);
+    st3r(B.cs, l, PS_D, d);
+    st3r(B.cs, l, PS_THR, v3(1.f, 1.f, 1.f));
+    psf(B.cs, l, PS_DVCM) = static_cast<float>(A.P) / i2sa;  // lightPathNum / cameraPdf
+    psf(B.cs, l, PS_DVC) = 0.f;
+    psi(B.cs, l, PS_LEN) = 1;
+    psi(B.cs, l, PS_NSPEC) = 0;
+    psu(B.cs, l, PS_CTR) = rng.ctr;
+    psi(B.cs, l, PS_PIX) = pix;  // (VertexCM's camera gen sets PS_DVM after this)
+  } else {
+    bqst3(B.cs, l, BQ_THR, v3(1.f, 1.f, 1.f));
+    bqf(B.cs, l, BQ_DVCM) = static_cast<float>(A.P) / i2sa;  // lightPathNum / cameraPdf
+    bqf(B.cs, l, BQ_DVC) = 0.f;
+    bqu(B.cs, l, BQ_CTR) = rng.ctr;
+    bqi(B.cs, l, BQ_PACK) = bq_pack(1, 0, 0);  // no camera vertex stored yet
+    bqi(B.cs, l, BQ_PIX) = pix;
+  }
   const int e = ebase + s;  // overlapped: behind the light pass's first rays (cam_ext_base)
   st3(B.q_o[0], B.qs, e, cam.pos + d * WR_EPS);
   st3(B.q_d[0], B.qs, e, normalize(d));
@@ -642,7 +677,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
   const BdptBuf::Sq& Q = B.sq[oslot & 1];  // rays traced at step oslot
   const BdptBuf::Di& D = B.di[oslot & 1];
   bool live = false, ext = false, conn_phase = false, nee = false, dib = false;
-  int pix = -1, nv = 0, len = 0, nspec = 0, cnspec = 0;
+  int pix = -1, nv = 0, len = 0, nspec = 0, cnspec = 0, pk = 0, ncv = 0;  // ncv: stored camera vertices
   V3 hp{}, thr{}, cthr{}, e_o{}, e_d{}, nee_tgt{}, nee_d{}, dib_o{}, dib_d{};
   float dvcm = 0.f, dvc = 0.f, cdvcm = 0.f, cdvc = 0.f;
   Bsdf b;
@@ -652,12 +687,14 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
     bsdf_init(b, -d, h.n, h.mat, S.mats);
     if (b.mat != 0) {
       hp = h.p;
-      pix = psi(B.cs, p, PS_PIX);
-      dvcm = psf(B.cs, p, PS_DVCM);
-      dvc = psf(B.cs, p, PS_DVC);
-      len = psi(B.cs, p, PS_LEN);
-      nspec = psi(B.cs, p, PS_NSPEC);
-      thr = ld3r(B.cs, p, PS_THR);
+      pix = bqi(B.cs, p, BQ_PIX);
+      dvcm = bqf(B.cs, p, BQ_DVCM);
+      dvc = bqf(B.cs, p, BQ_DVC);
+      pk = bqi(B.cs, p, BQ_PACK);
+      len = bq_len(pk);
+      nspec = bq_nspec(pk);
+      ncv = bq_count(pk);
+      thr = bqld3(B.cs, p, BQ_THR);
       dvcm *= (t * t);  // (:180-182)
       dvcm /= fabsf(b.wi.z);
       dvc /= fabsf(b.wi.z);
@@ -684,7 +721,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
         }
       } else if (len < A.maxlen) {
         live = true;
-        Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(A.base + p)), psu(B.cs, p, PS_CTR)};
+        Rng rng{stream_key(A.seed, A.iter, 1, static_cast<uint32_t>(A.base + p)), bqu(B.cs, p, BQ_CTR)};
         if (!b.delta && len_ok(A.ctl, len + 1)) {  // getDirectIllumination (:205-217, :484-608)
           const float wlen = 1.f / (static_cast<float>(len) + 1.f - static_cast<float>(nspec));
           const int lid = min(static_cast<int>(rng.f() * static_cast<float>(S.nlights)), S.nlights - 1);
@@ -755,11 +792,11 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
         }
         if (!b.delta) {
           conn_phase = true;
-          nv = psi(B.ls, p, PS_VCOUNT);
+          nv = bq_count(bqi(B.ls, p, BQ_PACK));
           // overlapped schedule: a vertex a later light vertex may still meet
           // (len < l, l + 1 + len <= maxlen) is kept for that light vertex
           if (A.overlap && 2 * len + 2 <= A.maxlen) {
-            const int j = psi(B.cs, p, PS_CVCOUNT);
+            const int j = ncv;
             int cs = j * P + p;
             if (B.cidx) {  // a pool record
               cs = pool_take(A, &A.sc->cpool, B.ccap);
@@ -780,20 +817,18 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
             cvi(B.cv, cs, CV_MAT) = b.mat;
             cvi(B.cv, cs, CV_PIX) = pix;
             }
-            psi(B.cs, p, PS_CVCOUNT) = j + 1;
+            ncv = j + 1;
           }
         }
-        V3 so = ld3r(B.cs, p, PS_O), sd = ld3r(B.cs, p, PS_D);
+        V3 so{}, sd{};  // sampleScattering's origin and direction (outputs only)
         if (sample_scatter(S, rng, b, hp, so, sd, thr, dvcm, dvc, nspec)) {
           ext = true;
           e_o = so + sd * WR_EPS;
           e_d = normalize(sd);
         }
-        psu(B.cs, p, PS_CTR) = rng.ctr;
-        // state for the NEXT vertex; the connections below use the values of
-        // THIS vertex, so keep them (thr/dvcm/dvc/nspec are re-read below)
-        st3r(B.cs, p, PS_O, so);
-        st3r(B.cs, p, PS_D, sd);
+        bqu(B.cs, p, BQ_CTR) = rng.ctr;
+        // the state for the NEXT vertex is committed below; the connections
+        // use the values of THIS vertex (cthr, cdvcm, cdvc, cnspec)
       }
     }
   }
@@ -836,11 +871,12 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
   }
   if (live) {  // commit scattered state (:259-260) and the loop increment
     if (ext) {
-      st3r(B.cs, p, PS_THR, thr);
-      psf(B.cs, p, PS_DVCM) = dvcm;
-      psf(B.cs, p, PS_DVC) = dvc;
-      psi(B.cs, p, PS_NSPEC) = nspec;
-      psi(B.cs, p, PS_LEN) = len + 1;
+      bqst3(B.cs, p, BQ_THR, thr);
+      bqf(B.cs, p, BQ_DVCM) = dvcm;
+      bqf(B.cs, p, BQ_DVC) = dvc;
+      bqi(B.cs, p, BQ_PACK) = bq_pack(len + 1, nspec, ncv);
+    } else if (ncv != bq_count(pk)) {
+      bqi(B.cs, p, BQ_PACK) = bq_pack(len, nspec, ncv);
     }
   }
   const int ei = wave_append(&A.sc->ext[oslot], ext) + ebase;

@@ -720,7 +720,7 @@ int pool_cap(int P, float per, int worst, int floor) {
   return static_cast<int>(std::min<double>(static_cast<double>(worst) * P, std::max<double>(want, floor)));
 }
 
-void layout_bdpt(Arena& a, BdptBuf& B, int P, bool overlapped) {
+void layout_bdpt(Arena& a, BdptBuf& B, int P, bool overlapped, bool vcm = false) {
   B.P = P;
   // shadow / aux rays queued by one step, per path: sequential schedule, a
   // camera vertex's <= kVMax connections + NEE + DI-BSDF (the light splats of
@@ -734,8 +734,10 @@ void layout_bdpt(Arena& a, BdptBuf& B, int P, bool overlapped) {
   B.vcap = pools ? pool_cap(P, kVPoolPerPath, kVMax, kVMax * 64) : kVMax * P;
   B.ccap = pools ? pool_cap(P, kCPoolPerPath, kCvMax, kCvMax * 64) : kCvMax * P;
   const size_t sP = P, sV = size_t(B.vcap), sQ = B.cap_sq;
-  B.ls = a.take<float>(PS_WORDS * sP);
-  B.cs = a.take<float>(PS_WORDS * sP);
+  // subpath records: BDPT's 32-byte BQ_* (wr_bdpt.h), VertexCM's 64-byte PS_*
+  const size_t rec = vcm ? PS_WORDS : BQ_WORDS;
+  B.ls = a.take<float>(rec * sP);
+  B.cs = a.take<float>(rec * sP);
   B.vs = a.take<float>(VS_WORDS * sV);
   B.cv = overlapped ? a.take<float>(CV_WORDS * size_t(B.ccap)) : nullptr;
   B.vidx = pools ? a.take<int>(size_t(kVMax) * P) : nullptr;
@@ -842,7 +844,7 @@ void layout_set(Arena& a, Pipe* dst, int g, int kind, int P) {
     layout_pt(a, dst ? dst->pb[g] : t, P);
     return;
   }
-  layout_bdpt(a, dst ? dst->bb[g] : b, P, kind == 1);
+  layout_bdpt(a, dst ? dst->bb[g] : b, P, kind == 1, kind == 3);
   if (kind == 3) layout_vcm(a, dst ? dst->vb[g] : v, P);
 }
 

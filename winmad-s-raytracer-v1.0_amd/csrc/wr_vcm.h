@@ -440,7 +440,7 @@ __device__ __forceinline__ V3 vcm_merge(const VcmArgs& X, const Bsdf& b, V3 hp, 
 __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_vcm_camera_gen(VcmGroup G_) {
   const VcmArgs& X = G_.a[blockIdx.y];
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < X.a.P; s += gridDim.x * blockDim.x) {
-    const int p = camera_gen_one(X.a, s);
+    const int p = camera_gen_one<true>(X.a, s);
     psf(X.a.B.cs, p, PS_DVM) = 0.f;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) X.a.sc->ext[kCamSlot] = X.a.P;
