@@ -26,7 +26,7 @@ enum : int {
   PS_VCOUNT = 14,  // light paths: stored light vertices
   PS_PIX = 14,     // camera paths: film pixel
   PS_DVM = 15,     // VCM: dVM (vertexcm.h:36)
-  PS_CVCOUNT = 15, // BDPT camera paths, overlapped schedule: stored camera vertices (CV_*)
+  PS_CVCOUNT = 15, // (unused: BDPT keeps its counters in BQ_PACK)
   PS_WORDS = 16
 };
 __device__ __forceinline__ float& psf(float* s, int p, int k) { return s[size_t(p) * PS_WORDS + k]; }
@@ -76,6 +76,58 @@ __device__ __forceinline__ int bq_pack(int len, int nspec, int cnt) { return len
 __device__ __forceinline__ int bq_len(int w) { return w & 255; }
 __device__ __forceinline__ int bq_nspec(int w) { return (w >> 8) & 255; }
 __device__ __forceinline__ int bq_count(int w) { return w >> 16; }
+constexpr int kLightAlive = 0x80;  // BdptBuf::lvc
+
+// BDPT's stored vertices (VertexCM keeps VS_*), light (B.vs) and camera (B.cv,
+// overlapped schedule) alike: 64 bytes.  The geometric normal and the BSDF's
+// probabilities are not stored: they are functions of the primitive (and, for
+// a sphere, the position), the local wi and the material, and stored_bsdf
+// rebuilds them with the operations the vertex itself ran (prim_normal,
+// bsdf_probs), to the same floats.
+//   BV_PACK = len | nspec << 8 | material << 16 (int16: emitters are < 0)
+enum : int { BV_POS = 0, BV_WI = 3, BV_THR = 6, BV_DVCM = 9, BV_DVC = 10, BV_PRIM = 11, BV_PACK = 12, BV_PIX = 13,
+             BV_WORDS = 16 };
+__device__ __forceinline__ float& bvf(float* s, int i, int k) { return s[size_t(i) * BV_WORDS + k]; }
+__device__ __forceinline__ int& bvi(float* s, int i, int k) {
+  return reinterpret_cast<int*>(s)[size_t(i) * BV_WORDS + k];
+}
+__device__ __forceinline__ V3 bvld3(const float* s, int i, int k) {
+  const float* r = s + size_t(i) * BV_WORDS + k;
+  return v3(r[0], r[1], r[2]);
+}
+__device__ __forceinline__ void bvst3(float* s, int i, int k, V3 v) {
+  float* r = s + size_t(i) * BV_WORDS + k;
+  r[0] = v.x;
+  r[1] = v.y;
+  r[2] = v.z;
+}
+__device__ __forceinline__ int bv_pack(int len, int nspec, int mat) {
+  return len | (nspec << 8) | static_cast<int>(static_cast<uint32_t>(mat) << 16);
+}
+__device__ __forceinline__ int bv_len(int w) { return w & 255; }
+__device__ __forceinline__ int bv_nspec(int w) { return (w >> 8) & 255; }
+__device__ __forceinline__ int bv_mat(int w) { return w >> 16; }  // arithmetic: the sign comes back
+// one stored vertex: position, local wi, throughput, dVCM, dVC, primitive,
+// (len, nspec, material) and the camera pixel
+__device__ __forceinline__ void store_vertex(float* s, int i, V3 pos, const Bsdf& b, V3 thr, float dvcm, float dvc,
+                                             int prim, int len, int nspec, int pix) {
+  bvst3(s, i, BV_POS, pos);
+  bvst3(s, i, BV_WI, b.wi);
+  bvst3(s, i, BV_THR, thr);
+  bvf(s, i, BV_DVCM) = dvcm;
+  bvf(s, i, BV_DVC) = dvc;
+  bvi(s, i, BV_PRIM) = prim;
+  bvi(s, i, BV_PACK) = bv_pack(len, nspec, b.mat);
+  bvi(s, i, BV_PIX) = pix;
+}
+// the BSDF of stored vertex i (BSDF::init at its hit, bsdf.h:66-89)
+__device__ __forceinline__ Bsdf stored_bsdf(const DevScene& S, const float* s, int i, int pack) {
+  Bsdf b;
+  b.fr = frame_from_z(prim_normal(S, bvi(const_cast<float*>(s), i, BV_PRIM), bvld3(s, i, BV_POS)));
+  b.wi = bvld3(s, i, BV_WI);
+  bsdf_probs(b, bv_mat(pack), S.mats);
+  return b;
+}
 
 // Stored light vertices (lightStates, bidirPathTracing.cpp:101-102), one
 // 80-byte record per vertex slot k * P + p: the camera pass reads a path's
@@ -120,36 +172,25 @@ __device__ __forceinline__ void drst3(float* s, int p, int k, V3 v) {
   r[2] = v.z;
 }
 
-// Stored camera vertices of the overlapped schedule, one 96-byte record per
-// slot j * P + p (j < kCvMax): what connectVertices (:610-665) reads of the
-// camera side when a LATER light vertex of the path makes the connection.
-// Only vertices with length <= (maxlen - 2) / 2 can meet a later light vertex
+// Stored camera vertices of the overlapped schedule (BV_* records, slot
+// j * P + p, j < kCvMax): what connectVertices (:610-665) reads of the camera
+// side when a LATER light vertex of the path makes the connection.  Only
+// vertices with length <= (maxlen - 2) / 2 can meet a later light vertex
 // (c < l and l + 1 + c <= maxlen), so kCvMax = 4 slots for maxlen <= 10.
-enum : int {
-  CV_POS = 0, CV_N = 3, CV_WI = 6, CV_THR = 9, CV_DVCM = 12, CV_DVC = 13, CV_CONT = 14, CV_PD = 15, CV_PG = 16,
-  CV_LEN = 17, CV_NSPEC = 18, CV_MAT = 19, CV_PIX = 20, CV_WORDS = 24
-};
 constexpr int kCvMax = (kVMax + 1 - 2) / 2;
-__device__ __forceinline__ float& cvf(float* s, int i, int k) { return s[size_t(i) * CV_WORDS + k]; }
-__device__ __forceinline__ int& cvi(float* s, int i, int k) {
-  return reinterpret_cast<int*>(s)[size_t(i) * CV_WORDS + k];
-}
-__device__ __forceinline__ V3 cvld3(const float* s, int i, int k) {
-  const float* r = s + size_t(i) * CV_WORDS + k;
-  return v3(r[0], r[1], r[2]);
-}
-__device__ __forceinline__ void cvst3(float* s, int i, int k, V3 v) {
-  float* r = s + size_t(i) * CV_WORDS + k;
-  r[0] = v.x;
-  r[1] = v.y;
-  r[2] = v.z;
-}
 
 struct BdptBuf {
   int P = 0, cap_sq = 0;
-  float *ls, *cs;  // light / camera subpath state, PS_WORDS floats per path
-  float* vs;       // stored light vertices, VS_WORDS floats per record (sequential schedule: record k * P + p)
-  float* cv;       // overlapped schedule: stored camera vertices, CV_WORDS floats per record
+  float *ls, *cs;  // light / camera subpath state: BDPT BQ_WORDS, VertexCM PS_WORDS floats per path
+  float* vs;       // stored light vertices: BDPT BV_WORDS, VertexCM VS_WORDS floats per record
+                   // (sequential schedule: record k * P + p)
+  float* cv;       // overlapped schedule: stored camera vertices, BV_WORDS floats per record
+  // BDPT: stored light / camera vertices per path, one byte each -- what each
+  // pass reads of the other's subpath (2 MB per 2M paths: L2-resident, where a
+  // read of the other pass's record would be a line from HBM per vertex).
+  // lvc's kLightAlive bit: the light subpath has an extension ray (a light
+  // vertex of a greater length may still come)
+  uint8_t *lvc, *cvc;
   // Overlapped schedule: the vertex stores are pools, sized by use rather than
   // by the worst case (the reference pushes only the vertices a path makes,
   // bidirPathTracing.cpp:101-102): vertex k of path p is record vidx[k * P +
@@ -274,6 +315,7 @@ __global__ void __launch_bounds__(kShadeBlock) WR_NO_PK_FP32 k_light_gen(BdptGro
     bqf(B.ls, p, BQ_DVC) = 1.f / epdf;  // AreaLight::isDelta() == 0
     bqu(B.ls, p, BQ_CTR) = rng.ctr;
     bqi(B.ls, p, BQ_PACK) = bq_pack(1, 0, 0);  // pathLength 1, no specular vertex, no stored vertex
+    B.lvc[p] = kLightAlive;  // no stored vertex, the first ray queued
     // Ray(origin + dir * EPS, dir) (:79-80)
     st3(B.q_o[0], B.qs, p, pos + dir * WR_EPS);
     st3(B.q_d[0], B.qs, p, normalize(dir));
@@ -318,11 +360,12 @@ __device__ __forceinline__ bool sample_scatter(const DevScene& S, Rng& rng, cons
 // splatted if unoccluded.  One function for both sides of the overlapped
 // schedule, so a pair's floats do not depend on which vertex came second.
 __device__ __forceinline__ bool connect_pair(const BdptArgs& A, const Bsdf& b, V3 hp, V3 cthr, float cdvcm, float cdvc,
-                                             int cnspec, int len, int slot, int llen, V3& sdir, V3& stgt, V3& sval) {
+                                             int cnspec, int len, int slot, int llen, V3& sdir, V3& stgt, V3& sval,
+                                             bool& counted) {
   const BdptBuf& B = A.B;
   const DevScene& S = A.S;
   bool shoot = false;
-  const V3 lpos = vld3(B.vs, slot, VS_POS);
+  const V3 lpos = bvld3(B.vs, slot, BV_POS);
   V3 dir = lpos - hp;
   const float d2 = sqr_len(dir);
   const float dist = sqrtf(d2);
@@ -332,13 +375,8 @@ __device__ __forceinline__ bool connect_pair(const BdptArgs& A, const Bsdf& b, V
   if (!black(cf)) {
     cdp *= b.cont;
     crp *= b.cont;
-    Bsdf lb;
-    lb.mat = vsi(B.vs, slot, VS_MAT);
-    lb.fr = frame_from_z(vld3(B.vs, slot, VS_N));
-    lb.wi = vld3(B.vs, slot, VS_WI);
-    lb.pd = vsf(B.vs, slot, VS_PD);
-    lb.pg = vsf(B.vs, slot, VS_PG);
-    lb.cont = vsf(B.vs, slot, VS_CONT);
+    const int lpk = bvi(B.vs, slot, BV_PACK);
+    const Bsdf lb = stored_bsdf(S, B.vs, slot, lpk);
     float cos_l = 0.f, ldp, lrp;
     const V3 lf = bsdf_f(lb, S.mats, -dir, &cos_l, &ldp, &lrp);
     if (!black(lf)) {
@@ -350,18 +388,19 @@ __device__ __forceinline__ bool connect_pair(const BdptArgs& A, const Bsdf& b, V
         const float ldpa = ldp * fabsf(cos_c) / (dist * dist);
         const V3 res = mul(cf, lf) * G;
         if (!black(res)) {
-          const float wl = cdpa * (vsf(B.vs, slot, VS_DVCM) + lrp * vsf(B.vs, slot, VS_DVC));
+          const float wl = cdpa * (bvf(B.vs, slot, BV_DVCM) + lrp * bvf(B.vs, slot, BV_DVC));
           const float wc = ldpa * (cdvcm + crp * cdvc);
           const float w = WR_TEST_CONN_W / (wl + 1.f + wc);
           const bool counts = len_ok(A.ctl, llen + 1 + len);
+          counted = counts;
           if (counts || A.faithful) {
             shoot = true;
             sdir = normalize(dir);
             stgt = hp + dir * dist;
             if (counts) {
               const float wlen = 1.f / (static_cast<float>(llen) + 1.f + static_cast<float>(len) -
-                                        static_cast<float>(vsi(B.vs, slot, VS_NSPEC)) - static_cast<float>(cnspec));
-              const V3 lthr = vld3(B.vs, slot, VS_THR);
+                                        static_cast<float>(bv_nspec(lpk)) - static_cast<float>(cnspec));
+              const V3 lthr = bvld3(B.vs, slot, BV_THR);
               sval = mul(mul(cthr, lthr), res * w) * wlen;
             }
           }
@@ -373,8 +412,12 @@ __device__ __forceinline__ bool connect_pair(const BdptArgs& A, const Bsdf& b, V
 }
 
 // queue a connection's shadow ray (every lane of the wave calls it)
-__device__ __forceinline__ void queue_connection(const BdptArgs& A, int qslot, bool shoot, int p, int pix, V3 hp,
-                                                 V3 sdir, V3 stgt, V3 sval) {
+// A connection whose path length the control-length filter drops (:252-253)
+// is still traced (faithful ray set, :244) but its outcome is never used: its
+// entry carries the ray and kSqNoValue only (no target, value or pixel).
+constexpr int kSqNoValue = 1 << 29;  // Sq meta: kind << 30 | kSqNoValue? | local path (< 2^29)
+__device__ __forceinline__ void queue_connection(const BdptArgs& A, int qslot, bool shoot, bool counted, int p, int pix,
+                                                 V3 hp, V3 sdir, V3 stgt, V3 sval) {
   const BdptBuf& B = A.B;
   const BdptBuf::Sq& Q = B.sq[qslot & 1];
   const int cap = B.cap_sq;
@@ -382,11 +425,15 @@ __device__ __forceinline__ void queue_connection(const BdptArgs& A, int qslot, b
   if (sq_fits(A, shoot, si)) {
     st3(Q.o, cap, si, hp);
     st3(Q.d, cap, si, sdir);
-    st3(Q.tgt, cap, si, stgt);
-    st3(Q.val, cap, si, sval);
     Q.cut[si] = occl_cut(hp, stgt, dot(stgt - hp, sdir));
-    Q.meta[si] = (SQ_CONN << 30) | p;
-    Q.pix[si] = pix;
+    if (counted) {
+      st3(Q.tgt, cap, si, stgt);
+      st3(Q.val, cap, si, sval);
+      Q.meta[si] = (SQ_CONN << 30) | p;
+      Q.pix[si] = pix;
+    } else {
+      Q.meta[si] = (SQ_CONN << 30) | kSqNoValue | p;
+    }
   }
 }
 
@@ -421,25 +468,12 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
           slot = pool_take(A, &A.sc->vpool, B.vcap);
           B.vidx[size_t(k) * P + p] = slot;
         }
-        if (slot >= 0) {
-          vst3(B.vs, slot, VS_POS, h.p);
-          vst3(B.vs, slot, VS_N, h.n);
-          vst3(B.vs, slot, VS_WI, b.wi);
-          vst3(B.vs, slot, VS_THR, thr);
-          vsf(B.vs, slot, VS_DVCM) = dvcm;
-          vsf(B.vs, slot, VS_DVC) = dvc;
-          vsf(B.vs, slot, VS_CONT) = b.cont;
-          vsf(B.vs, slot, VS_PD) = b.pd;
-          vsf(B.vs, slot, VS_PG) = b.pg;
-          vsi(B.vs, slot, VS_LEN) = len;
-          vsi(B.vs, slot, VS_NSPEC) = nspec;
-          vsi(B.vs, slot, VS_MAT) = b.mat;
-        }
+        if (slot >= 0) store_vertex(B.vs, slot, h.p, b, thr, dvcm, dvc, prim, len, nspec, -1);
         nstored = k + 1;
         if (A.overlap && slot >= 0) {  // the camera vertices stored at earlier steps (lengths < len)
           lslot = slot;
           llen = len;
-          lconn = bq_count(bqi(B.cs, p, BQ_PACK));
+          lconn = B.cvc[p];
         }
         if (len_ok(A.ctl, len + 1)) {  // connectToCamera (:105-120, :313-368)
           const DCam& cam = S.cam;
@@ -501,7 +535,13 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
       }
       // len / nspec of the next vertex (when it scatters), the stored vertices
       if (ext || nstored != bq_count(pk)) bqi(B.ls, p, BQ_PACK) = bq_pack(len, nspec, nstored);
+      const int lv = nstored | (ext ? kLightAlive : 0);
+      if (lv != (bq_count(pk) | kLightAlive)) B.lvc[p] = static_cast<uint8_t>(lv);
+    } else {  // an invalid BSDF ends the subpath (:86-88)
+      B.lvc[p] &= static_cast<uint8_t>(~kLightAlive);
     }
+  } else if (p >= 0) {  // a miss ends the subpath (:81-82)
+    B.lvc[p] &= static_cast<uint8_t>(~kLightAlive);
   }
   const int ei = wave_append(&A.sc->ext[oslot], ext);
   if (ext) {
@@ -527,29 +567,24 @@ __device__ __forceinline__ void light_vertex(const BdptArgs& A, int p, int prim,
   // vertices stored at earlier steps (:219-257 reached from the camera side)
   if (A.overlap && __ballot(lconn > 0)) {
     for (int j = 0; __ballot(j < lconn); ++j) {
-      bool shoot = false;
+      bool shoot = false, counted = false;
       int pix = -1;
       V3 hp{}, sdir{}, stgt{}, sval{};
       const int cs = j < lconn ? cv_slot(B, j, p) : -1;
       if (cs >= 0) {
-        const int clen = cvi(B.cv, cs, CV_LEN);
+        const int cpk = bvi(B.cv, cs, BV_PACK);
+        const int clen = bv_len(cpk);
         if (llen + 1 + clen > A.maxlen) {
           lconn = j;  // camera vertices are stored by increasing length
         } else {
-          Bsdf cb;
-          cb.mat = cvi(B.cv, cs, CV_MAT);
-          cb.fr = frame_from_z(cvld3(B.cv, cs, CV_N));
-          cb.wi = cvld3(B.cv, cs, CV_WI);
-          cb.pd = cvf(B.cv, cs, CV_PD);
-          cb.pg = cvf(B.cv, cs, CV_PG);
-          cb.cont = cvf(B.cv, cs, CV_CONT);
-          hp = cvld3(B.cv, cs, CV_POS);
-          pix = cvi(B.cv, cs, CV_PIX);
-          shoot = connect_pair(A, cb, hp, cvld3(B.cv, cs, CV_THR), cvf(B.cv, cs, CV_DVCM), cvf(B.cv, cs, CV_DVC),
-                               cvi(B.cv, cs, CV_NSPEC), clen, lslot, llen, sdir, stgt, sval);
+          const Bsdf cb = stored_bsdf(S, B.cv, cs, cpk);
+          hp = bvld3(B.cv, cs, BV_POS);
+          pix = bvi(B.cv, cs, BV_PIX);
+          shoot = connect_pair(A, cb, hp, bvld3(B.cv, cs, BV_THR), bvf(B.cv, cs, BV_DVCM), bvf(B.cv, cs, BV_DVC),
+                               bv_nspec(cpk), clen, lslot, llen, sdir, stgt, sval, counted);
         }
       }
-      queue_connection(A, sslot, shoot, p, pix, hp, sdir, stgt, sval);
+      queue_connection(A, sslot, shoot, counted, p, pix, hp, sdir, stgt, sval);
     }
   }
 }
@@ -646,6 +681,7 @@ __device__ __forceinline__ int camera_gen_one(const BdptArgs& A, int s, int ebas
     bqu(B.cs, l, BQ_CTR) = rng.ctr;
     bqi(B.cs, l, BQ_PACK) = bq_pack(1, 0, 0);  // no camera vertex stored yet
     bqi(B.cs, l, BQ_PIX) = pix;
+    B.cvc[l] = 0;
   }
   const int e = ebase + s;  // overlapped: behind the light pass's first rays (cam_ext_base)
   st3(B.q_o[0], B.qs, e, cam.pos + d * WR_EPS);
@@ -792,31 +828,20 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
         }
         if (!b.delta) {
           conn_phase = true;
-          nv = bq_count(bqi(B.ls, p, BQ_PACK));
+          const int lv = B.lvc[p];
+          nv = lv & ~kLightAlive;
           // overlapped schedule: a vertex a later light vertex may still meet
-          // (len < l, l + 1 + len <= maxlen) is kept for that light vertex
-          if (A.overlap && 2 * len + 2 <= A.maxlen) {
+          // (len < l, l + 1 + len <= maxlen) is kept for that light vertex --
+          // if the light subpath still has a ray (after this step's light
+          // kernel: a vertex of length > len may come); else none will
+          if (A.overlap && 2 * len + 2 <= A.maxlen && (lv & kLightAlive)) {
             const int j = ncv;
             int cs = j * P + p;
             if (B.cidx) {  // a pool record
               cs = pool_take(A, &A.sc->cpool, B.ccap);
               B.cidx[size_t(j) * P + p] = cs;
             }
-            if (cs >= 0) {
-            cvst3(B.cv, cs, CV_POS, hp);
-            cvst3(B.cv, cs, CV_N, h.n);
-            cvst3(B.cv, cs, CV_WI, b.wi);
-            cvst3(B.cv, cs, CV_THR, cthr);
-            cvf(B.cv, cs, CV_DVCM) = cdvcm;
-            cvf(B.cv, cs, CV_DVC) = cdvc;
-            cvf(B.cv, cs, CV_CONT) = b.cont;
-            cvf(B.cv, cs, CV_PD) = b.pd;
-            cvf(B.cv, cs, CV_PG) = b.pg;
-            cvi(B.cv, cs, CV_LEN) = len;
-            cvi(B.cv, cs, CV_NSPEC) = cnspec;
-            cvi(B.cv, cs, CV_MAT) = b.mat;
-            cvi(B.cv, cs, CV_PIX) = pix;
-            }
+            if (cs >= 0) store_vertex(B.cv, cs, hp, b, cthr, cdvcm, cdvc, prim, len, cnspec, pix);
             ncv = j + 1;
           }
         }
@@ -855,18 +880,18 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
   // vertex connections to the paired light subpath (:219-257)
   if (__ballot(conn_phase && nv > 0)) {
     for (int k = 0; __ballot(conn_phase && k < nv); ++k) {
-      bool shoot = false;
+      bool shoot = false, counted = false;
       V3 sdir{}, stgt{}, sval{};
       const int slot = conn_phase && k < nv ? lv_slot(B, k, p) : -1;
       if (slot >= 0) {
-        const int llen = vsi(B.vs, slot, VS_LEN);
+        const int llen = bv_len(bvi(B.vs, slot, BV_PACK));
         if (llen + 1 + len > A.maxlen) {
           nv = k;  // break (:237-239)
         } else {
-          shoot = connect_pair(A, b, hp, cthr, cdvcm, cdvc, cnspec, len, slot, llen, sdir, stgt, sval);
+          shoot = connect_pair(A, b, hp, cthr, cdvcm, cdvc, cnspec, len, slot, llen, sdir, stgt, sval, counted);
         }
       }
-      queue_connection(A, oslot, shoot, p, pix, hp, sdir, stgt, sval);
+      queue_connection(A, oslot, shoot, counted, p, pix, hp, sdir, stgt, sval);
     }
   }
   if (live) {  // commit scattered state (:259-260) and the loop increment
@@ -878,6 +903,7 @@ __device__ __forceinline__ void camera_vertex(const BdptArgs& A, int p, int prim
     } else if (ncv != bq_count(pk)) {
       bqi(B.cs, p, BQ_PACK) = bq_pack(len, nspec, ncv);
     }
+    if (ncv != bq_count(pk)) B.cvc[p] = static_cast<uint8_t>(ncv);
   }
   const int ei = wave_append(&A.sc->ext[oslot], ext) + ebase;
   if (ext) {
@@ -960,11 +986,13 @@ __device__ __forceinline__ void sq_resolve_body(const BdptArgs& A, int slot, int
     bool is_shadow = false, is_closest = false;
     if (j < n) {
       const int meta = Q.meta[j];
-      const int kind = (meta >> 30) & 3, p = meta & 0x3fffffff;
+      const int kind = (meta >> 30) & 3, p = meta & (kSqNoValue - 1);
       const int prim = Q.prim[j];
       const float t = Q.t[j];
       int di_bits = -1;  // >= 0: this ray belongs to DI record p
-      if (kind == SQ_DIB) {  // DI BSDF-sampled ray: same light? (:570-596)
+      if (meta & kSqNoValue) {  // a filtered connection: traced and counted, nothing to add
+        is_shadow = true;
+      } else if (kind == SQ_DIB) {  // DI BSDF-sampled ray: same light? (:570-596)
         is_closest = true;
         bool same = false;
         if (prim >= 0) {

@@ -239,11 +239,10 @@ struct Bsdf {
 
 // BSDF::init (bsdf.h:66-89).  Emitter hits (mat < 0) get the pinned values of
 // the oracle: probabilities 0, continueProb 0, isDelta false.
-__device__ __forceinline__ void bsdf_init(Bsdf& b, V3 wi, V3 n, int hit_mat, const DMat* mats) {
-  b.mat = 0;
-  b.fr = frame_from_z(n);
-  b.wi = normalize(to_local(b.fr, wi));
-  if (cmpf(b.wi.z) == 0) return;
+// The component / continuation probabilities of BSDF::init from the local
+// wi and the material (the tail of bsdf_init; also how a stored vertex's
+// BSDF is rebuilt, wr_bdpt.h stored_bsdf).
+__device__ __forceinline__ void bsdf_probs(Bsdf& b, int hit_mat, const DMat* mats) {
   b.pd = b.pg = b.pr = b.pt = 0.f;
   b.cont = 0.f;
   b.fres = 1.f;
@@ -268,6 +267,13 @@ __device__ __forceinline__ void bsdf_init(Bsdf& b, V3 wi, V3 n, int hit_mat, con
     b.delta = (cmpf(b.pd) == 0 && cmpf(b.pg) == 0);
   }
   b.mat = hit_mat;
+}
+__device__ __forceinline__ void bsdf_init(Bsdf& b, V3 wi, V3 n, int hit_mat, const DMat* mats) {
+  b.mat = 0;
+  b.fr = frame_from_z(n);
+  b.wi = normalize(to_local(b.fr, wi));
+  if (cmpf(b.wi.z) == 0) return;
+  bsdf_probs(b, hit_mat, mats);
 }
 
 __device__ __forceinline__ V3 calc_diffuse(const Bsdf& b, const DMat& m, V3 wo, float* dp, float* rp) {

@@ -738,8 +738,11 @@ void layout_bdpt(Arena& a, BdptBuf& B, int P, bool overlapped, bool vcm = false)
   const size_t rec = vcm ? PS_WORDS : BQ_WORDS;
   B.ls = a.take<float>(rec * sP);
   B.cs = a.take<float>(rec * sP);
-  B.vs = a.take<float>(VS_WORDS * sV);
-  B.cv = overlapped ? a.take<float>(CV_WORDS * size_t(B.ccap)) : nullptr;
+  // stored vertices: BDPT's 64-byte BV_* records, VertexCM's 80-byte VS_*
+  B.vs = a.take<float>((vcm ? VS_WORDS : BV_WORDS) * sV);
+  B.cv = overlapped ? a.take<float>(BV_WORDS * size_t(B.ccap)) : nullptr;
+  B.lvc = vcm ? nullptr : a.take<uint8_t>(sP);
+  B.cvc = vcm ? nullptr : a.take<uint8_t>(sP);
   B.vidx = pools ? a.take<int>(size_t(kVMax) * P) : nullptr;
   B.cidx = pools ? a.take<int>(size_t(kCvMax) * P) : nullptr;
   // overlapped: an extension queue holds both passes' rays (light, then camera)

@@ -973,6 +973,16 @@ struct Hit {
   V3 p, n;
   int inside, mat;
 };
+// The geometric normal of primitive prim at p (Triangle::hit / Sphere::hit):
+// rebuild_hit's operations, for a stored vertex (wr_bdpt.h stored_bsdf).
+__device__ __forceinline__ V3 prim_normal(const DevScene& S, int prim, V3 p) {
+  const float4 r0 = S.prim_rec[2 * static_cast<size_t>(prim)], r1 = S.prim_rec[2 * static_cast<size_t>(prim) + 1];
+  if (__float_as_int(r1.w) != 0) {
+    const float4 cs = S.prim_sph[prim];
+    return normalize(p - v3(cs.x, cs.y, cs.z));
+  }
+  return normalize(cross(v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y)));
+}
 __device__ __forceinline__ Hit rebuild_hit(const DevScene& S, int prim, float t, V3 o, V3 d) {
   Hit h;
   h.t = t;
