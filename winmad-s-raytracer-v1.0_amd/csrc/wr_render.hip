@@ -186,13 +186,30 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
   return v;
 }
 
+// Queue entries (SoA x / y / z columns) are written by one kernel and read by
+// the next one or two: with WR_QUEUE_NT they move with the non-temporal policy,
+// leaving the L2 to the scene's nodes and triangles, which every search re-reads.
+#ifndef WR_QUEUE_NT
+#define WR_QUEUE_NT 1
+#endif
 __device__ __forceinline__ V3 ld3(const float* b, int stride, int i) {
+#if WR_QUEUE_NT
+  return v3(__builtin_nontemporal_load(b + i), __builtin_nontemporal_load(b + stride + i),
+            __builtin_nontemporal_load(b + 2 * stride + i));
+#else
   return v3(b[i], b[stride + i], b[2 * stride + i]);
+#endif
 }
 __device__ __forceinline__ void st3(float* b, int stride, int i, V3 v) {
+#if WR_QUEUE_NT
+  __builtin_nontemporal_store(v.x, b + i);
+  __builtin_nontemporal_store(v.y, b + stride + i);
+  __builtin_nontemporal_store(v.z, b + 2 * stride + i);
+#else
   b[i] = v.x;
   b[stride + i] = v.y;
   b[2 * stride + i] = v.z;
+#endif
 }
 __device__ __forceinline__ void film_add(float* film, int pix, V3 v) {
   if (pix < 0) return;
