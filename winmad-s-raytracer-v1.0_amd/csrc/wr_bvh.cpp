@@ -46,10 +46,14 @@ constexpr int kMaxBins = 256;
 //   WR_BVH_SWEEP  ranges of at most this many triangles take the exact SAH sweep
 //   WR_BVH_CT     cost of one node visit relative to one triangle test
 //   WR_BVH_SERIAL 1: no helper threads for subtrees and splits (the same tree)
+// Round 6 re-sweep on the current kernels (profiles/r6/bvh_knobs/): 64 bins
+// and a node visit priced as one triangle test (was 16 and 0.5) take C2 at 20
+// iterations from 3,002 to 3,107 Mrays/s (6 runs each), C3 +2.8 %, VCM
+// +1.3 %, C4 and one iteration unchanged; 20.55 -> 20.12 nodes per ray
 struct BuildKnobs {
-  int bins = 16;
+  int bins = 64;
   int sweep = 0;
-  double ct = 0.5;
+  double ct = 1.0;
   bool serial = false;
   BuildKnobs() {
     if (const char* e = std::getenv("WR_BVH_SERIAL")) serial = std::atoi(e) != 0;
