@@ -73,6 +73,9 @@ struct FastCounters {  // algorithmic work (count_work)
   // k_fast_hard tie resolution and KD walk -- max and sum per ray -- and the
   // rays whose membership test scanned a many-leaf primitive's whole list
   uint32_t mem_max, mem_sum, tie_max, tie_sum, walk_max, walk_sum, scans;
+  // WR_TIE_SPLIT (diagnostic build): the tie resolutions' ticks in bvh_collect and in
+  // the first-leaf searches, and their second collect passes
+  uint32_t tie_col, tie_leaf, tie_pass2;
   // kd_walk_wave (count_work): walks, their rounds and nodes, and fall-backs
   // to the serial walk (work stack or hit list outgrown)
   uint32_t ww_walks, ww_rounds, ww_nodes, ww_over;
@@ -130,6 +133,9 @@ __host__ __device__ constexpr size_t search_spill_entries(int depth, int wide) {
 // (larger) bound only add hits beyond the window, never drop one inside it.
 #ifndef WR_BVH_SPEC
 #define WR_BVH_SPEC 1
+#endif
+#ifndef WR_TIE_SPLIT
+#define WR_TIE_SPLIT 0  // diagnostic: time the tie resolution's phases (count_work)
 #endif
 // the tie resolution's leaf searches: calls (WR_HARD_CALL=__noinline__) or inlined
 #ifndef WR_HARD_CALL
@@ -1077,7 +1083,8 @@ __device__ WR_HARD_CALL void kd_first_leaves(const DevScene& S, const FastScene&
 template <bool WAVE>
 __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin,
                                             float rtmax, float t1, int* stk_link, float* stk_t, float& t_out,
-                                            int& p_out, uint32_t& steps, uint32_t& psteps, int& dbg) {
+                                            int& p_out, uint32_t& steps, uint32_t& psteps, int& dbg,
+                                            uint32_t* split = nullptr, int p1 = -1, int2 pair = {-1, 0}) {
   float tmin0, tmax0;
   if (!box_hit(S.root_l, S.root_r, o, d, tmin0, tmax0) || rtmax < tmin0) return false;
   const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
@@ -1091,7 +1098,28 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
   // triangle is not visited, the kTie smallest hits without a bound
   for (int pass = 0; pass < 2; ++pass) {
     const float cap = pass == 0 ? t1 + 3.f * WR_EPS : WR_INF;
-    n = bvh_collect(S, F, o, d, rtmin, rtmax, cap, stk_link, stk_t, ct, cp);
+#if WR_TIE_SPLIT
+    const uint64_t a0 = wall_clock64();
+#endif
+    if (pass == 0 && pair.x >= 0 && p1 >= 0) {
+      // the search's pair (kPairWindow): the first window holds exactly these
+      // two hits, the collection's answer without the collection
+      n = 2;
+#pragma unroll
+      for (int j = 0; j < kTie; ++j) {
+        ct[j] = j == 0 ? t1 : (j == 1 ? __int_as_float(pair.y) : WR_INF);
+        cp[j] = j == 0 ? p1 : (j == 1 ? pair.x : -1);
+      }
+    } else {
+      n = bvh_collect(S, F, o, d, rtmin, rtmax, cap, stk_link, stk_t, ct, cp);
+    }
+#if WR_TIE_SPLIT
+    const uint64_t a1 = wall_clock64();
+    if (split) {
+      split[0] += static_cast<uint32_t>(a1 - a0);
+      split[2] += pass;
+    }
+#endif
     m = WR_INF;
     const int ncand = min(n, kTie);
     // per candidate: its first visited leaf as a visit-order key (~0: none).
@@ -1134,6 +1162,9 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
         if (c < ncand) first_leaf(F, cp[c], o, d, inv, tmin0, tmax0, rtmax, key[c], pos[c], steps);
       }
     }
+#if WR_TIE_SPLIT
+    if (split) split[1] += static_cast<uint32_t>(wall_clock64() - a1);
+#endif
 #pragma unroll
     for (int c = 0; c < kTie; ++c)
       if (c < ncand && key[c] != ~0ull && m == WR_INF) m = ct[c];  // sorted by t: the first visited one
@@ -1360,7 +1391,7 @@ __device__ __forceinline__ bool first_cells_crossed(const FastScene& F, int p1, 
 // reads those rays only.  The test is the resolve's own, on the same floats.
 template <bool COUNT, int W, bool SPH, bool RL = false>
 __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q, int* fetch,
-                                           float* t2buf, int2* spill, uint32_t* lds, FastCounters& ctr,
+                                           float* t2buf, int2* pairs, int2* spill, uint32_t* lds, FastCounters& ctr,
                                            int bid, int nblk,  // this block's index among the launch's nblk search blocks
                                            int* rlist = nullptr, int* rlist_n = nullptr) {
   constexpr int kLdsStack = SearchStack<W>::lds;
@@ -1388,6 +1419,8 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   V3 o = v3(0.f, 0.f, 0.f), d = o, binv = o;
   V3 cl = o, ch = o;  // slab offsets -(o + g) binv, -(o - g) binv for the current margin g
   float rtmin = 0.f, rtmax = WR_INF, t1 = WR_INF, t2 = WR_INF, tcap = 0.f, dlen = 1.f, olen = 0.f;
+  float t3 = WR_INF;  // the third smallest hit (kPairWindow)
+  int p2 = -1;        // the second smallest hit's primitive
   float lo_t = 0.f, hi_t = 0.f;
   int p1 = -1, sp = 0;
   bool gz = false;          // the ray grazes a tested triangle's plane (tri_grazes)
@@ -1427,8 +1460,10 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
     }
     return idx;
   };
-  // the search window: hits up to t1 + 2 EPS, and rtmax
-  auto bound = [&]() { return fminf(rtmax, t1 + 2.f * WR_EPS); };
+  // the search window: hits up to t1 + 3 EPS (the tie resolution's first
+  // window: a near-tie whose window holds two hits leaves with both, kPairWindow),
+  // and rtmax
+  auto bound = [&]() { return fminf(rtmax, t1 + 3.f * WR_EPS); };
   // the ray's box margin g (space) and the node test's constants for it.  A
   // box face x is tested as fma(x, binv, -(o -+ g) binv): the product
   // (o -+ g) binv is rounded once, an error of < 1 ulp of |o| |binv| in t, i.e.
@@ -1500,7 +1535,9 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           if (!(dlen > 0.f)) dlen = 1.f;
           t1 = WR_INF;
           t2 = WR_INF;
+          t3 = WR_INF;
           p1 = -1;
+          p2 = -1;
           gz = false;
           sp = 0;
           cur = 0;
@@ -1745,16 +1782,22 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
           hit = sph_hit(S, pr, o, d, rtmin, rtmax, t);
         } else {
           gz |= tri_grazes(ta[j], tb[j], tc[j].x, o, d);
-          // screen against t1 + 3 EPS: every hit with t <= t1 + 2 EPS survives
-          hit = tri_test(ta[j], tb[j], tc[j].x, o, d, rtmin, rtmax, t1 + 3.f * WR_EPS, t);
+          // screen against t1 + 4 EPS: every hit with t <= t1 + 3 EPS survives
+          hit = tri_test(ta[j], tb[j], tc[j].x, o, d, rtmin, rtmax, t1 + 4.f * WR_EPS, t);
         }
         if (hit) {
           if (t < t1) {
+            t3 = t2;
             t2 = t1;
+            p2 = p1;
             t1 = t;
             p1 = pr;
           } else if (t < t2) {
+            t3 = t2;
             t2 = t;
+            p2 = pr;
+          } else if (t < t3) {
+            t3 = t;
           }
         }
       }
@@ -1776,8 +1819,16 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
       // diagnostic probes (F.diag) keep t2, as they may skip the kernels that
       // clear the mark.
       int po = p1;
-      if (F.diag) t2buf[lidx] = t2;
-      else if (p1 >= 0 && !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0)) po = p1 | kTieMark;
+      if (F.diag) {
+        t2buf[lidx] = t2;
+      } else if (p1 >= 0 && !(cmpf(t2 - t1) > 0 && cmpf(t1 - WR_INF) < 0)) {
+        po = p1 | kTieMark;
+        // every hit up to t1 + 3 EPS was seen (the window above): when the
+        // third lies beyond the tie resolution's first window, its collection
+        // would return exactly (t1, p1), (t2, p2) -- they travel with the ray
+        const bool two = t3 > fminf(rtmax, t1 + 3.f * WR_EPS);
+        pairs[lidx] = two ? make_int2(p2, __float_as_int(t2)) : make_int2(-1, 0);
+      }
       if (gz) po = po >= 0 ? (po | kGrazeMark) : kGrazeMiss;
       qfield(Q, qi, [](const RayQueue& x) { return x.out_t; })[r] = p1 >= 0 ? t1 : WR_INF;
       qfield(Q, qi, [](const RayQueue& x) { return x.out_prim; })[r] = po;
@@ -1801,8 +1852,10 @@ __device__ __forceinline__ void trace_fast(const DevScene& S, const FastScene& F
   if constexpr (RL) flush_list();
 }
 
-// tie-list entries: launch index, | kWalkEntry for a ray the KD walk settles
+// tie-list entries: launch index, | kWalkEntry for a ray the KD walk settles,
+// | kTieEntry for a near-tie (its pair record is the search's)
 constexpr int kWalkEntry = 1 << 30;
+constexpr int kTieEntry = 1 << 29;
 // k_fast_resolve: one ray per lane (grid-stride over the launch's indices).
 // The rare rays it cannot settle (near-ties, t1 not reached) go to `hard` for
 // k_fast_hard, so that their register-hungry code does not lower this
@@ -1831,7 +1884,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
   // every lane of the wave takes part in each list append (whole iterations)
   for (int base = blockIdx.x * 64; base < nr; base += gridDim.x * 64) {
     const int idx = base + lane < nr ? (rlist ? rlist[base + lane] : base + lane) : QI.n;
-    bool need = false, scan = false, big_tie = false, walk = false;
+    bool need = false, scan = false, big_tie = false, walk = false, pair_tie = false;
     int q = 0, r = 0, p1 = -1;
     float t1 = WR_INF;
     V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 0.f);
@@ -1867,6 +1920,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
           // one per lane
           const bool big = WR_TIE_WAVE_ALL || F.prim_leaf_off[p1 + 1] - F.prim_leaf_off[p1] > kTieLeaves;
           need = !big;
+          pair_tie = !F.diag;
           scan = big;
           big_tie = big;
         } else if (!(F.diag & 8)) {
@@ -1931,7 +1985,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
       need = scan = false;
     }
     const int slot = fast_append(hard_n, need);
-    if (need) hard[slot] = walk ? (idx | kWalkEntry) : idx;
+    if (need) hard[slot] = walk ? (idx | kWalkEntry) : (pair_tie ? (idx | kTieEntry) : idx);
     // the scan list fills the same array from the top (a ray is in one list)
     const int sslot = fast_append(hard_n + 1, scan);
     if (scan) hard[hcap - 1 - sslot] = big_tie ? ~idx : idx;
@@ -1959,14 +2013,17 @@ template <bool COUNT, bool WAVE>
 __device__ __forceinline__ bool settle_ray(const DevScene& S, const FastScene& F, V3 o, V3 d, float rtmin, float rtmax,
                                            float t1, int* stk_node, float* stk_tmin, float* outt, int* outp, int r,
                                            bool lead, FastCounters& ctr, bool walk = false,
-                                           bool* hand_walk = nullptr) {
+                                           bool* hand_walk = nullptr, int p1 = -1, int2 pair = {-1, 0}) {
   float tb;
   int pb;
   if (!(F.diag & 2) && !walk) {
     uint32_t steps = 0, psteps = 0;
     int dbg = 0;
     const uint64_t c0 = COUNT ? wall_clock64() : 0;
-    const bool done = resolve_tie<WAVE>(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, psteps, dbg);
+    uint32_t split[3] = {0, 0, 0};
+    const bool done =
+        resolve_tie<WAVE>(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, psteps, dbg, split, p1,
+                          pair);
     if (!WAVE && dbg == kTieDeferred) {
       if (COUNT) ctr.replay += steps;
       return false;
@@ -1977,6 +2034,9 @@ __device__ __forceinline__ bool settle_ray(const DevScene& S, const FastScene& F
         const uint32_t dt = static_cast<uint32_t>(wall_clock64() - c0);
         ctr.tie_max = max(ctr.tie_max, dt);
         ctr.tie_sum += dt;
+        ctr.tie_col += split[0];
+        ctr.tie_leaf += split[1];
+        ctr.tie_pass2 += split[2];
         ctr.replay += steps;
         ctr.fb_tie += done ? 1u : 0u;
         const int why = dbg >> 16;
@@ -2033,6 +2093,7 @@ struct ListedRay {
   float* outt;
   int* outp;
   bool walk;  // straight to the KD walk (k_fast_resolve's grazing winners)
+  int2 pair;  // near-ties: the search's second hit (p2, t2 bits) when its first window holds two, else (-1, 0)
 };
 
 __device__ __forceinline__ ListedRay listed_ray(const TraceQueues& Q, const QueueIndex& QI, int idx) {
@@ -2054,6 +2115,7 @@ __device__ __forceinline__ ListedRay listed_ray(const TraceQueues& Q, const Queu
   L.rtmin = tmn ? tmn[r] : 0.f;
   L.rtmax = tmx ? tmx[r] : WR_INF;
   L.walk = false;
+  L.pair = make_int2(-1, 0);
   return L;
 }
 
@@ -2070,7 +2132,7 @@ __device__ __forceinline__ void hard_rays(const DevScene& S, const FastScene& F,
     for (int i = bid; i < nh; i += nb) {
       const ListedRay L = get(i);
       settle_ray<COUNT, true>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r, lead,
-                              ctr, L.walk);
+                              ctr, L.walk, nullptr, L.p1, L.pair);
     }
     return;
   }
@@ -2083,7 +2145,7 @@ __device__ __forceinline__ void hard_rays(const DevScene& S, const FastScene& F,
     if (i < nh) {
       L = get(i);
       back = !settle_ray<COUNT, false>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r,
-                                       true, ctr, L.walk, &hw);
+                                       true, ctr, L.walk, &hw, L.p1, L.pair);
     }
     for (unsigned long long m = __ballot(back); m != 0ull; m &= m - 1ull) {
       const int src = __ffsll(static_cast<unsigned long long>(m)) - 1;
@@ -2096,20 +2158,22 @@ __device__ __forceinline__ void hard_rays(const DevScene& S, const FastScene& F,
       };
       settle_ray<COUNT, true>(S, F, v3(bf(L.o.x), bf(L.o.y), bf(L.o.z)), v3(bf(L.d.x), bf(L.d.y), bf(L.d.z)),
                               bf(L.rtmin), bf(L.rtmax), bf(L.t1), stk_node, stk_tmin, bp(L.outt), bp(L.outp), bi(L.r),
-                              lane == 0, ctr, bi(hw ? 1 : 0) != 0);
+                              lane == 0, ctr, bi(hw ? 1 : 0) != 0, nullptr, bi(L.p1), make_int2(bi(L.pair.x), bi(L.pair.y)));
     }
   }
 }
 template <bool COUNT, bool WAVE>
 __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
-                                          const int* hard, const int* hard_n, int bid, int nb, uint32_t* lds,
-                                          FastCounters& ctr) {
+                                          const int* hard, const int* hard_n, const int2* pairs, int bid, int nb,
+                                          uint32_t* lds, FastCounters& ctr) {
   const QueueIndex QI(Q);
   const int nh = (F.diag & (32 | 128)) ? 0 : hard_n[0];
   hard_rays<COUNT, WAVE>(S, F, nh, [&](int i) {
     const int e = hard[i];
-    ListedRay L = listed_ray(Q, QI, e & ~kWalkEntry);
+    const int idx = e & ~(kWalkEntry | kTieEntry);
+    ListedRay L = listed_ray(Q, QI, idx);
     L.walk = (e & kWalkEntry) != 0;
+    if (pairs && (e & kTieEntry)) L.pair = pairs[idx];
     return L;
   }, bid, nb, lds, ctr);
 }
@@ -2177,7 +2241,7 @@ __device__ __forceinline__ void scan_rays(const DevScene& S, const FastScene& F,
       continue;
     }
     settle_ray<COUNT, true>(S, F, L.o, L.d, L.rtmin, L.rtmax, L.t1, stk_node, stk_tmin, L.outt, L.outp, L.r,
-                            lane == 0, ctr);
+                            lane == 0, ctr, false, nullptr, L.p1, L.pair);
   }
 }
 template <bool COUNT>
@@ -2189,7 +2253,9 @@ __device__ __forceinline__ void scan_fast(const DevScene& S, const FastScene& F,
   scan_rays<COUNT>(S, F, ns, [&](int i, bool& tie) {
     const int e = hard[hcap - 1 - i];
     tie = e < 0;
-    return listed_ray(Q, QI, tie ? ~e : e);
+    ListedRay L = listed_ray(Q, QI, tie ? ~e : e);
+    if (tie && !F.diag) L.pair = reinterpret_cast<const int2*>(hard + hcap)[tie ? ~e : e];  // (kPairWindow)
+    return L;
   }, bid, nb, lds, ctr);
 }
 
@@ -2207,6 +2273,7 @@ __device__ __forceinline__ ListedRay late_ray(const LateList& LL, int i) {
   L.outt = LL.t;
   L.outp = LL.prim;
   L.walk = false;
+  L.pair = make_int2(-1, 0);
   return L;
 }
 // k_late_hard: a late list's tie entries (blocks [0, hard_blocks): one per

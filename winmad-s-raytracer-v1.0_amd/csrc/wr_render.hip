@@ -158,7 +158,7 @@ struct DevCounters {
   unsigned long long bvh_nodes, bvh_tests, kd_replay, fallback;  // WR_TRACE_BVH work (count_work)
   unsigned long long verify_rays, verify_bad;                   // WR_BVH_VERIFY
   unsigned long long deferred;  // BDPT rays settled off the critical path (late lists)
-  unsigned long long lat[7];  // WR_TRACE_BVH latency tail (FastCounters mem_max .. scans; max or sum)
+  unsigned long long lat[10];  // WR_TRACE_BVH latency tail (FastCounters mem_max .. scans; max or sum; tie_col .. tie_pass2)
   unsigned long long ww[4];   // kd_walk_wave: walks, rounds, nodes, serial fall-backs
   unsigned long long overflow;  // BDPT: appends a full vertex pool / shadow queue dropped (the render is redone)
 };
@@ -286,8 +286,9 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
   atomicAdd(&ctr->stamps[7], static_cast<unsigned long long>(fc.long_rays));
   atomicAdd(&ctr->stamps[4], static_cast<unsigned long long>(fc.fb_tie));
   for (int k = 0; k < 4; ++k) atomicAdd(&ctr->stamps[k], static_cast<unsigned long long>(fc.why[k]));
-  const uint32_t lat[7] = {fc.mem_max, fc.mem_sum, fc.tie_max, fc.tie_sum, fc.walk_max, fc.walk_sum, fc.scans};
-  for (int k = 0; k < 7; ++k) {
+  const uint32_t lat[10] = {fc.mem_max, fc.mem_sum, fc.tie_max, fc.tie_sum, fc.walk_max,
+                            fc.walk_sum, fc.scans,   fc.tie_col, fc.tie_leaf, fc.tie_pass2};
+  for (int k = 0; k < 10; ++k) {
     if (k % 2 == 0 && k < 6) atomicMax(&ctr->lat[k], static_cast<unsigned long long>(lat[k]));
     else atomicAdd(&ctr->lat[k], static_cast<unsigned long long>(lat[k]));
   }
@@ -314,8 +315,9 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
 template <bool COUNT, bool LATE, int W, bool SPH, bool RL = false>
 __global__ void __launch_bounds__(kTraceBlock)
 __attribute__((amdgpu_waves_per_eu(W == 4 && !LATE ? WR_FAST4_WAVES : WR_FAST_WAVES, 8))) WR_NO_PK_FP32
-k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* spill,
-             LateArgs L, int lblocks, int gn, int hblocks, int lane_blocks, int wave_max, int* rlist, int* rlist_n) {
+k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetch, float* t2buf, int2* pairs,
+             int2* spill, LateArgs L, int lblocks, int gn, int hblocks, int lane_blocks, int wave_max, int* rlist,
+             int* rlist_n) {
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
   const int b = static_cast<int>(blockIdx.x);
@@ -327,7 +329,7 @@ k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetc
       atomicAdd(&ctr->deferred, static_cast<unsigned long long>(min(L.n[m][0], half) + min(L.n[m][1], half)));
     }
   } else {
-    trace_fast<COUNT, W, SPH, RL>(S, F, Q, fetch, t2buf, spill, smem, fc, b - (LATE ? lblocks : 0),
+    trace_fast<COUNT, W, SPH, RL>(S, F, Q, fetch, t2buf, pairs, spill, smem, fc, b - (LATE ? lblocks : 0),
                                   static_cast<int>(gridDim.x) - (LATE ? lblocks : 0), rlist, rlist_n);
   }
   if (COUNT) fast_counts<COUNT>(ctr, fc);
@@ -336,8 +338,8 @@ k_trace_fast(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, int* fetc
 // library is built with WR_BVH_WIDE=8)
 // RL: the search's per-wave buffer of listed rays (trace_fast)
 constexpr size_t kRlistLds = 64 * sizeof(int);
-using TraceFastKernel = void (*)(DevScene, FastScene, TraceQueues, DevCounters*, int*, float*, int2*, LateArgs, int, int,
-                                 int, int, int, int*, int*);
+using TraceFastKernel = void (*)(DevScene, FastScene, TraceQueues, DevCounters*, int*, float*, int2*, int2*, LateArgs,
+                                 int, int, int, int, int, int*, int*);
 template <bool COUNT, bool LATE>
 TraceFastKernel trace_fast_kernel(int wide, bool sph = false, bool rl = false) {
 #if WR_BVH_WIDE == 8
@@ -393,10 +395,12 @@ k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const int*
   FastCounters fc{};
   const int b = static_cast<int>(blockIdx.x);
   if (b < hard_blocks) {
+    // the search's pair records follow the lists (TraceSlot::t2)
+    const int2* pairs = reinterpret_cast<const int2*>(hard + hcap);
     if (WAVE || hard_n[0] <= wave_max)  // wave_max <= hard_blocks
-      hard_fast<COUNT, true>(S, F, Q, hard, hard_n, b, hard_blocks, smem, fc);
+      hard_fast<COUNT, true>(S, F, Q, hard, hard_n, pairs, b, hard_blocks, smem, fc);
     else if (b < lane_blocks)
-      hard_fast<COUNT, false>(S, F, Q, hard, hard_n, b, lane_blocks, smem, fc);
+      hard_fast<COUNT, false>(S, F, Q, hard, hard_n, pairs, b, lane_blocks, smem, fc);
   } else {
     scan_fast<COUNT>(S, F, Q, hard, hard_n, hcap, b - hard_blocks, static_cast<int>(gridDim.x) - hard_blocks, smem, fc);
   }
@@ -1015,7 +1019,8 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, int
 // WR_TRACE_BVH mode the per-ray t2 scratch of the BVH search (>= the launch's rays).
 struct TraceSlot {
   int* fetch;
-  float* t2;      // [t2_cap] t2 per launch index, then [t2_cap] the tie list (from the bottom) and the scan list (from the top)
+  float* t2;      // [t2_cap] t2 per launch index, then [t2_cap] the tie list (from the bottom) and the scan list (from the
+                  // top), then [t2_cap] int2 pair records (kPairWindow)
   size_t t2_cap;
   int* hard_n;
   int2* spill;    // the search stack's spill area
@@ -1049,7 +1054,7 @@ int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
   if (p.t2buf) (void)hipFree(p.t2buf);
   p.t2buf = nullptr;
   p.t2_cap = 0;
-  HIPCHK(hipMalloc(&p.t2buf, 2 * rays * sizeof(float)));
+  HIPCHK(hipMalloc(&p.t2buf, 4 * rays * sizeof(float)));  // t2 / list, hard lists, pair records (int2)
   p.t2_cap = rays;
   return WR_OK;
 }
@@ -1124,6 +1129,8 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     int* rlist = rl ? reinterpret_cast<int*>(ts.t2) : nullptr;
     int* rlist_n = rl ? ts.rlist_n : nullptr;
     const size_t rlds = slds + (rl ? kRlistLds : 0);
+    // the search's pair records of near-ties (kPairWindow): after the lists
+    int2* pairs = reinterpret_cast<int2*>(ts.t2 + 2 * ts.t2_cap);
     hipEvent_t f0 = nullptr, f1 = nullptr, fa = nullptr, fb = nullptr;
     if (c->trace_log) {
       (void)hipEventCreate(&f0);
@@ -1136,7 +1143,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
       const int lblocks = late_gn * (kLateTieBlocks + kLateScanBlocks);
       auto kf = count ? trace_fast_kernel<true, true>(F.wide, F.sph) : trace_fast_kernel<false, true>(F.wide, F.sph);
       hipLaunchKernelGGL(kf, dim3(lblocks + fgrid),
-                         dim3(kTraceBlock), std::max(slds, lds), stream, c->ds, F, Q, ctr, fetch, ts.t2, ts.spill,
+                         dim3(kTraceBlock), std::max(slds, lds), stream, c->ds, F, Q, ctr, fetch, ts.t2, pairs, ts.spill,
                          *late_prev, lblocks, late_gn, kLateTieBlocks, kLateLaneBlocks, kLateTieBlocks, nullptr, nullptr);
       if (c->verify)
         hipLaunchKernelGGL(k_late_verify, dim3(64, late_gn), dim3(kTraceBlock), lds, stream, c->ds, F, *late_prev,
@@ -1145,7 +1152,7 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
       auto kf = count ? trace_fast_kernel<true, false>(F.wide, F.sph, rl)
                       : trace_fast_kernel<false, false>(F.wide, F.sph, rl);
       hipLaunchKernelGGL(kf, dim3(fgrid),
-                         dim3(kTraceBlock), rlds, stream, c->ds, F, Q, ctr, fetch, ts.t2, ts.spill, LateArgs{}, 0,
+                         dim3(kTraceBlock), rlds, stream, c->ds, F, Q, ctr, fetch, ts.t2, pairs, ts.spill, LateArgs{}, 0,
                          1, 0, 0, 0, rlist, rlist_n);
     }
     if (c->trace_log) (void)hipEventRecord(fa, stream);
@@ -1412,18 +1419,21 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host, unsigned l
       mx[1] = std::max(mx[1], h.stamps[6]);
       mx[2] += h.stamps[7];
     }
-    unsigned long long ties = 0, why[4] = {0, 0, 0, 0}, lat[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ties = 0, why[4] = {0, 0, 0, 0}, lat[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < n; ++i) {
       DevCounters h;
       HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
       ties += h.stamps[4];
       for (int k = 0; k < 4; ++k) why[k] += h.stamps[k];
-      for (int k = 0; k < 7; ++k) lat[k] = (k % 2 == 0 && k < 6) ? std::max(lat[k], h.lat[k]) : lat[k] + h.lat[k];
+      for (int k = 0; k < 10; ++k) lat[k] = (k % 2 == 0 && k < 6) ? std::max(lat[k], h.lat[k]) : lat[k] + h.lat[k];
     }
     std::fprintf(stderr,
                  "[wr bvh latency, us] membership max %.1f sum %.1f; ties max %.1f sum %.1f; walks max %.1f sum %.1f; "
                  "long many-leaf scans %llu\n",
                  lat[0] * 0.01, lat[1] * 0.01, lat[2] * 0.01, lat[3] * 0.01, lat[4] * 0.01, lat[5] * 0.01, lat[6]);
+    if (lat[7] + lat[8])
+      std::fprintf(stderr, "[wr bvh tie split, us] collect %.1f, first leaves %.1f, second passes %llu\n",
+                   lat[7] * 0.01, lat[8] * 0.01, lat[9]);
     std::fprintf(stderr, "[wr bvh walks] many-leaf %llu, no visited hit %llu, crowd %llu, band %llu\n", why[0], why[1],
                  why[2], why[3]);
     unsigned long long ww[4] = {0, 0, 0, 0};
@@ -2106,7 +2116,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
     if (c->api_t2) (void)hipFree(c->api_t2);
     c->api_t2 = nullptr;
     c->api_t2_cap = 0;
-    HIPCHK(hipMalloc(&c->api_t2, 2 * nb * sizeof(float)));
+    HIPCHK(hipMalloc(&c->api_t2, 4 * nb * sizeof(float)));  // as ensure_t2
     c->api_t2_cap = nb;
   }
   QueueList ql;
