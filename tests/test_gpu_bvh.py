@@ -204,6 +204,29 @@ def test_resolve_list_same_rays_and_film(kind, monkeypatch):
     assert _film_close(fa, fb)
 
 
+@pytest.mark.parametrize("kind", ["bdpt", "vcm", "bdpt1m"])
+def test_pair_record_same_rays_and_film(kind, monkeypatch):
+    """Near-ties settled from the search's pair record (WR_PAIR_RECORD: 2 = the
+    pair list, one near-tie per lane, the default; 1 = the record in the tie
+    list only) give the rays and the film of the tie resolution's own BVH
+    collection (0).  (Every answer of the default against the KD walk:
+    test_bvh_verify_every_ray_against_the_kd_walk.)"""
+    W, H = (128, 72) if kind == "bdpt1m" else (192, 144)
+    out = []
+    for mode in ("2", "1", "0"):
+        monkeypatch.setenv("WR_PAIR_RECORD", mode)
+        c = native.Context(native.Scene(big_torus(W, H) if kind == "bdpt1m" else _scenes.torus(W, H)), 0)
+        if kind == "vcm":
+            out.append(c.render_vcm(W, H, iterations=2, seed=13))
+        else:
+            out.append(c.render_bdpt(W, H, iterations=4, seed=13))
+        c.close()
+    f0, s0 = out[0]
+    for f, s in out[1:]:
+        assert s.closest_rays == s0.closest_rays and s.shadow_rays == s0.shadow_rays
+        assert _film_close(f0, f)
+
+
 @pytest.mark.parametrize("diag", [16, 32, 48, 64, 128])
 def test_capacity_diagnostics_keep_primitive_indices_valid(diag, monkeypatch):
     """WR_BVH_DIAG's capacity probes skip the resolve or the hard launch (wrong

@@ -58,6 +58,7 @@ struct FastScene {
   int depth;   // stack entries of the KD walks and tie resolution (k_fast_hard, k_fast_verify)
   int sdepth;  // stack entries of the BVH search (k_trace_fast): the BVH's depth + 1
   int walk_wave;  // 1: the one-ray-per-wave resolutions walk the KD tree with the whole wave (kd_walk_wave)
+  int pair;       // near-ties use the search's pair record: 2 = pair list (one per lane), 1 = tie list only, 0 = never
   int diag;   // WR_BVH_DIAG (measurement only): 1 = skip the KD walks, 8 = skip the replays, 16 = skip k_fast_resolve,
               // 32 = skip k_fast_hard, 64 its scan list, 128 its tie list (all wrong answers);
               // 2 = KD walk for every tie, 256 = every ray to k_fast_hard's KD walk (exact: a test of the walks)
@@ -75,7 +76,7 @@ struct FastCounters {  // algorithmic work (count_work)
   uint32_t mem_max, mem_sum, tie_max, tie_sum, walk_max, walk_sum, scans;
   // WR_TIE_SPLIT (diagnostic build): the tie resolutions' ticks in bvh_collect and in
   // the first-leaf searches, and their second collect passes
-  uint32_t tie_col, tie_leaf, tie_pass2;
+  uint32_t tie_col, tie_leaf, tie_pass2, scan_t, pair_used;
   // kd_walk_wave (count_work): walks, their rounds and nodes, and fall-backs
   // to the serial walk (work stack or hit list outgrown)
   uint32_t ww_walks, ww_rounds, ww_nodes, ww_over;
@@ -1104,6 +1105,9 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
     if (pass == 0 && pair.x >= 0 && p1 >= 0) {
       // the search's pair (kPairWindow): the first window holds exactly these
       // two hits, the collection's answer without the collection
+#if WR_TIE_SPLIT
+      if (split) ++split[3];
+#endif
       n = 2;
 #pragma unroll
       for (int j = 0; j < kTie; ++j) {
@@ -1884,7 +1888,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
   // every lane of the wave takes part in each list append (whole iterations)
   for (int base = blockIdx.x * 64; base < nr; base += gridDim.x * 64) {
     const int idx = base + lane < nr ? (rlist ? rlist[base + lane] : base + lane) : QI.n;
-    bool need = false, scan = false, big_tie = false, walk = false, pair_tie = false;
+    bool need = false, scan = false, big_tie = false, walk = false, pair_tie = false, lane_pair = false;
     int q = 0, r = 0, p1 = -1;
     float t1 = WR_INF;
     V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 0.f);
@@ -1920,7 +1924,14 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
           // one per lane
           const bool big = WR_TIE_WAVE_ALL || F.prim_leaf_off[p1 + 1] - F.prim_leaf_off[p1] > kTieLeaves;
           need = !big;
-          pair_tie = !F.diag;
+          pair_tie = !F.diag && F.pair > 0;
+          if (need && pair_tie && F.pair > 1) {
+            const int2 pr2 = reinterpret_cast<const int2*>(hard + hcap)[idx];
+            if (pr2.x >= 0 && F.prim_leaf_off[pr2.x + 1] - F.prim_leaf_off[pr2.x] <= kTieLeaves) {
+              lane_pair = true;
+              need = false;
+            }
+          }
           scan = big;
           big_tie = big;
         } else if (!(F.diag & 8)) {
@@ -1986,6 +1997,10 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
     }
     const int slot = fast_append(hard_n, need);
     if (need) hard[slot] = walk ? (idx | kWalkEntry) : (pair_tie ? (idx | kTieEntry) : idx);
+    // near-ties the search's pair record covers, both candidates in few KD
+    // leaves: the pair list (k_fast_hard, one per lane: lane_pair)
+    const int pslot = fast_append(hard_n + 2, lane_pair);
+    if (lane_pair) hard[3 * static_cast<size_t>(hcap) + pslot] = idx;
     // the scan list fills the same array from the top (a ray is in one list)
     const int sslot = fast_append(hard_n + 1, scan);
     if (scan) hard[hcap - 1 - sslot] = big_tie ? ~idx : idx;
@@ -2020,7 +2035,7 @@ __device__ __forceinline__ bool settle_ray(const DevScene& S, const FastScene& F
     uint32_t steps = 0, psteps = 0;
     int dbg = 0;
     const uint64_t c0 = COUNT ? wall_clock64() : 0;
-    uint32_t split[3] = {0, 0, 0};
+    uint32_t split[4] = {0, 0, 0, 0};
     const bool done =
         resolve_tie<WAVE>(S, F, o, d, rtmin, rtmax, t1, stk_node, stk_tmin, tb, pb, steps, psteps, dbg, split, p1,
                           pair);
@@ -2037,6 +2052,7 @@ __device__ __forceinline__ bool settle_ray(const DevScene& S, const FastScene& F
         ctr.tie_col += split[0];
         ctr.tie_leaf += split[1];
         ctr.tie_pass2 += split[2];
+        ctr.pair_used += split[3];
         ctr.replay += steps;
         ctr.fb_tie += done ? 1u : 0u;
         const int why = dbg >> 16;
@@ -2178,6 +2194,27 @@ __device__ __forceinline__ void hard_fast(const DevScene& S, const FastScene& F,
   }, bid, nb, lds, ctr);
 }
 
+// The pair list: near-ties whose 3-EPS window the search's pair record
+// covers, both candidates in at most kTieLeaves KD leaves.  One per lane: the
+// tie resolution then costs two candidates' leaf replays and no BVH search,
+// and 64 of them share a wave (a near-tie per wave holds a wave per tie, and
+// at one iteration's early steps those waves outnumber the slots the hard
+// kernel's registers leave).  A ray the lane cannot settle (a walk) is
+// resolved by its whole wave afterwards (hard_rays).
+template <bool COUNT>
+__device__ __forceinline__ void pair_fast(const DevScene& S, const FastScene& F, const TraceQueues& Q,
+                                          const int* plist, const int* hard_n, const int2* pairs, int bid, int nb,
+                                          uint32_t* lds, FastCounters& ctr) {
+  const QueueIndex QI(Q);
+  const int np = hard_n[2];
+  hard_rays<COUNT, false>(S, F, np, [&](int i) {
+    const int idx = plist[i];
+    ListedRay L = listed_ray(Q, QI, idx);
+    L.pair = pairs[idx];
+    return L;
+  }, bid, nb, lds, ctr);
+}
+
 // The scan list (k_fast_resolve's kScan rays and near-ties on many-leaf
 // primitives, at the top of the list array): one ray per wave.  The lanes share out p1's leaves -- the witness for each
 // leaf's cell, else the replay of its path -- and stop once one is reached;
@@ -2195,6 +2232,9 @@ __device__ __forceinline__ void scan_rays(const DevScene& S, const FastScene& F,
     bool member = false;
     float tmin, tmax;
     uint32_t steps = 0;
+#if WR_TIE_SPLIT
+    const uint64_t s0 = wall_clock64();
+#endif
     if (!tie && box_hit(S.root_l, S.root_r, L.o, L.d, tmin, tmax) && !(L.rtmax < tmin)) {  // :312-313, :323
       const V3 inv = v3(1.f / L.d.x, 1.f / L.d.y, 1.f / L.d.z);
       const V3 binv = v3(clamp_inv(L.d.x), clamp_inv(L.d.y), clamp_inv(L.d.z));
@@ -2232,6 +2272,9 @@ __device__ __forceinline__ void scan_rays(const DevScene& S, const FastScene& F,
     if (COUNT) {
       ctr.replay += steps;
       ctr.scans += lane == 0 ? 1u : 0u;
+#if WR_TIE_SPLIT
+      if (lane == 0) ctr.scan_t += static_cast<uint32_t>(wall_clock64() - s0);
+#endif
     }
     if (member) {  // p1 stands (a queue entry holds it already; a late record gets it)
       if (lane == 0) {
@@ -2254,7 +2297,7 @@ __device__ __forceinline__ void scan_fast(const DevScene& S, const FastScene& F,
     const int e = hard[hcap - 1 - i];
     tie = e < 0;
     ListedRay L = listed_ray(Q, QI, tie ? ~e : e);
-    if (tie && !F.diag) L.pair = reinterpret_cast<const int2*>(hard + hcap)[tie ? ~e : e];  // (kPairWindow)
+    if (tie && !F.diag && F.pair > 0) L.pair = reinterpret_cast<const int2*>(hard + hcap)[~e];  // (kPairWindow)
     return L;
   }, bid, nb, lds, ctr);
 }

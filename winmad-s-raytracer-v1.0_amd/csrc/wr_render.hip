@@ -143,14 +143,14 @@ struct StepCounters {
   int vcm_pending;    // VCM: light paths whose first vertex is an emitter (k_vcm_fixup)
   int vcm_nverts;     // VCM: light vertices in the merge grid
   int mq[kSlots];     // VCM: merge queries queued at step `slot`
-  int hard[kSlots][2];  // WR_TRACE_BVH: rays of step `slot` left to k_fast_hard (tie list, scan list)
+  int hard[kSlots][3];  // WR_TRACE_BVH: rays of step `slot` left to k_fast_hard (tie list, scan list, pair list)
   int rlist[kSlots];    // WR_TRACE_BVH: rays of step `slot` the search left to k_fast_resolve
   int late[kSlots][2];  // WR_TRACE_BVH: rays of step `slot` deferred (late list: ties, scans)
   int vpool, cpool;     // BDPT, overlapped: records taken from the light / camera vertex pools
 };
 struct DevCounters {
   int fetch;  // traversal cursor of the API path (wr_trace_closest / wr_occluded)
-  int hard[2];  // API path: rays left to k_fast_hard (tie list, scan list)
+  int hard[3];  // API path: rays left to k_fast_hard (tie list, scan list, pair list)
   int rlist;    // API path: rays the search left to k_fast_resolve
   unsigned long long stamps[8];  // diagnostic build only (WR_TRACE_STAMPS=1)
   unsigned long long closest, shadow, inner, leaves, refs, tests;
@@ -158,7 +158,7 @@ struct DevCounters {
   unsigned long long bvh_nodes, bvh_tests, kd_replay, fallback;  // WR_TRACE_BVH work (count_work)
   unsigned long long verify_rays, verify_bad;                   // WR_BVH_VERIFY
   unsigned long long deferred;  // BDPT rays settled off the critical path (late lists)
-  unsigned long long lat[10];  // WR_TRACE_BVH latency tail (FastCounters mem_max .. scans; max or sum; tie_col .. tie_pass2)
+  unsigned long long lat[12];  // WR_TRACE_BVH latency tail (FastCounters mem_max .. scans; max or sum; tie_col .. tie_pass2)
   unsigned long long ww[4];   // kd_walk_wave: walks, rounds, nodes, serial fall-backs
   unsigned long long overflow;  // BDPT: appends a full vertex pool / shadow queue dropped (the render is redone)
 };
@@ -286,9 +286,9 @@ __device__ __forceinline__ void fast_counts(DevCounters* ctr, const FastCounters
   atomicAdd(&ctr->stamps[7], static_cast<unsigned long long>(fc.long_rays));
   atomicAdd(&ctr->stamps[4], static_cast<unsigned long long>(fc.fb_tie));
   for (int k = 0; k < 4; ++k) atomicAdd(&ctr->stamps[k], static_cast<unsigned long long>(fc.why[k]));
-  const uint32_t lat[10] = {fc.mem_max, fc.mem_sum, fc.tie_max, fc.tie_sum, fc.walk_max,
-                            fc.walk_sum, fc.scans,   fc.tie_col, fc.tie_leaf, fc.tie_pass2};
-  for (int k = 0; k < 10; ++k) {
+  const uint32_t lat[12] = {fc.mem_max, fc.mem_sum, fc.tie_max,   fc.tie_sum, fc.walk_max,  fc.walk_sum,
+                            fc.scans,   fc.tie_col, fc.tie_leaf, fc.tie_pass2, fc.scan_t, fc.pair_used};
+  for (int k = 0; k < 12; ++k) {
     if (k % 2 == 0 && k < 6) atomicMax(&ctr->lat[k], static_cast<unsigned long long>(lat[k]));
     else atomicAdd(&ctr->lat[k], static_cast<unsigned long long>(lat[k]));
   }
@@ -390,19 +390,23 @@ k_fast_resolve(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const f
 template <bool COUNT, bool WAVE>
 __global__ void __launch_bounds__(kTraceBlock) WR_NO_PK_FP32 WR_HARD_OCC
 k_fast_hard(DevScene S, FastScene F, TraceQueues Q, DevCounters* ctr, const int* hard, const int* hard_n, int hcap,
-            int hard_blocks, int lane_blocks, int wave_max) {
+            int hard_blocks, int lane_blocks, int wave_max, int pair_blocks) {
   extern __shared__ uint32_t smem[];
   FastCounters fc{};
   const int b = static_cast<int>(blockIdx.x);
-  if (b < hard_blocks) {
-    // the search's pair records follow the lists (TraceSlot::t2)
-    const int2* pairs = reinterpret_cast<const int2*>(hard + hcap);
+  // the search's pair records and the pair list follow the lists (TraceSlot::t2)
+  const int2* pairs = reinterpret_cast<const int2*>(hard + hcap);
+  if (b >= hard_blocks && b < hard_blocks + pair_blocks) {
+    pair_fast<COUNT>(S, F, Q, hard + 3 * static_cast<size_t>(hcap), hard_n, pairs, b - hard_blocks, pair_blocks, smem,
+                     fc);
+  } else if (b < hard_blocks) {
     if (WAVE || hard_n[0] <= wave_max)  // wave_max <= hard_blocks
       hard_fast<COUNT, true>(S, F, Q, hard, hard_n, pairs, b, hard_blocks, smem, fc);
     else if (b < lane_blocks)
       hard_fast<COUNT, false>(S, F, Q, hard, hard_n, pairs, b, lane_blocks, smem, fc);
   } else {
-    scan_fast<COUNT>(S, F, Q, hard, hard_n, hcap, b - hard_blocks, static_cast<int>(gridDim.x) - hard_blocks, smem, fc);
+    const int s0 = hard_blocks + pair_blocks;
+    scan_fast<COUNT>(S, F, Q, hard, hard_n, hcap, b - s0, static_cast<int>(gridDim.x) - s0, smem, fc);
   }
   if (COUNT) fast_counts<COUNT>(ctr, fc);
 }
@@ -634,6 +638,7 @@ struct wr_context {
   bool fs4_ok = false;
   bool lat_wide = true;  // env WR_BVH_WIDE_LAT=0: off
   int wide_now = 0;
+  bool lat_now = false;  // the current BDPT render is latency-bound (see wide_now)
   Arena fast_mem;
   bool fast_ok = false;   // scene supports it
   bool fast_on = false;   // WR_TRACE_BVH mode selected
@@ -1020,7 +1025,7 @@ TraceKernel trace_kernel(bool count, bool spheres, bool narrow, bool stamps, int
 struct TraceSlot {
   int* fetch;
   float* t2;      // [t2_cap] t2 per launch index, then [t2_cap] the tie list (from the bottom) and the scan list (from the
-                  // top), then [t2_cap] int2 pair records (kPairWindow)
+                  // top), then [t2_cap] int2 pair records (kPairWindow), then [t2_cap] the pair list
   size_t t2_cap;
   int* hard_n;
   int2* spill;    // the search stack's spill area
@@ -1040,6 +1045,10 @@ size_t max_spill_entries(const wr_context* c) {
 // tree (every other field -- KD stack depth, diagnostics -- is fs's own)
 FastScene search_scene(const wr_context* c) {
   FastScene F = c->fs;
+  // a latency-bound render keeps every near-tie one per wave (the pair list's
+  // one per lane waits for its slowest lane: C2 at 1 iteration -4 %, while C4 at
+  // 64 iterations gains 2.6 %, profiles/r6/pair_list/ab.txt)
+  if (c->lat_now && F.pair > 1) F.pair = 1;
   if (c->wide_now == 4 && c->fs4_ok) {
     F.wide = 4;
     F.sdepth = c->sdepth4;
@@ -1054,7 +1063,7 @@ int ensure_t2(wr_context* c, Pipe& p, size_t rays) {
   if (p.t2buf) (void)hipFree(p.t2buf);
   p.t2buf = nullptr;
   p.t2_cap = 0;
-  HIPCHK(hipMalloc(&p.t2buf, 4 * rays * sizeof(float)));  // t2 / list, hard lists, pair records (int2)
+  HIPCHK(hipMalloc(&p.t2buf, 5 * rays * sizeof(float)));  // t2 / list, hard lists, pair records (int2), pair list
   p.t2_cap = rays;
   return WR_OK;
 }
@@ -1171,9 +1180,11 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
     const int sgrid = std::max(1, std::min(c->scan_waves, max_rays));  // scan waves
     auto hk = hard_wave ? (count ? k_fast_hard<true, true> : k_fast_hard<false, true>)
                         : (count ? k_fast_hard<true, false> : k_fast_hard<false, false>);
-    hipLaunchKernelGGL(hk, dim3(hgrid + sgrid),
+    // the pair list (near-ties the search's pair record settles, one per lane)
+    const int pgrid = (F.diag || F.pair < 2) ? 0 : lgrid;
+    hipLaunchKernelGGL(hk, dim3(hgrid + pgrid + sgrid),
                        dim3(kTraceBlock), lds, stream, c->ds, F, Q, ctr, hard, ts.hard_n,
-                       static_cast<int>(ts.t2_cap), hgrid, lgrid, std::min(hgrid, c->tie_wave_max));
+                       static_cast<int>(ts.t2_cap), hgrid, lgrid, std::min(hgrid, c->tie_wave_max), pgrid);
     if (c->verify)
       hipLaunchKernelGGL(k_fast_verify, dim3(std::max(1, std::min(c->fast_blocks, blocks))), dim3(kTraceBlock), lds,
                          stream, c->ds, F, Q, ctr);
@@ -1184,14 +1195,15 @@ int trace_launch(wr_context* c, hipStream_t stream, DevCounters* ctr, const Trac
       int tot = 0;
       for (int i = 0; i < Q.n; ++i) tot += host_count(Q.q[i]);
       float ms = 0.f, ma = 0.f, mb = 0.f;
-      int nhs[2] = {0, 0};
-      (void)hipMemcpy(nhs, ts.hard_n, 2 * sizeof(int), hipMemcpyDeviceToHost);
+      int nhs[3] = {0, 0, 0};
+      (void)hipMemcpy(nhs, ts.hard_n, 3 * sizeof(int), hipMemcpyDeviceToHost);
       const int nh = nhs[0], ns = nhs[1];
       (void)hipEventElapsedTime(&ms, f0, f1);
       (void)hipEventElapsedTime(&ma, f0, fa);
       (void)hipEventElapsedTime(&mb, fa, fb);
-      std::fprintf(stderr, "[wr bvh] %d rays  %.1f us (search %.1f, resolve %.1f, hard %.1f: %d + %d scan rays)  grid %d\n",
-                   tot, ms * 1e3f, ma * 1e3f, mb * 1e3f, (ms - ma - mb) * 1e3f, nh, ns, fgrid);
+      std::fprintf(stderr,
+                   "[wr bvh] %d rays  %.1f us (search %.1f, resolve %.1f, hard %.1f: %d + %d pair + %d scan rays)  grid %d\n",
+                   tot, ms * 1e3f, ma * 1e3f, mb * 1e3f, (ms - ma - mb) * 1e3f, nh, nhs[2], ns, fgrid);
       (void)hipEventDestroy(f0);
       (void)hipEventDestroy(f1);
       (void)hipEventDestroy(fa);
@@ -1419,21 +1431,23 @@ int finish_render(wr_context* c, int n, wr_stats* st, double t0_host, unsigned l
       mx[1] = std::max(mx[1], h.stamps[6]);
       mx[2] += h.stamps[7];
     }
-    unsigned long long ties = 0, why[4] = {0, 0, 0, 0}, lat[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ties = 0, why[4] = {0, 0, 0, 0}, lat[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < n; ++i) {
       DevCounters h;
       HIPCHK(hipMemcpy(&h, c->pipes[i].ctr, sizeof h, hipMemcpyDeviceToHost));
       ties += h.stamps[4];
       for (int k = 0; k < 4; ++k) why[k] += h.stamps[k];
-      for (int k = 0; k < 10; ++k) lat[k] = (k % 2 == 0 && k < 6) ? std::max(lat[k], h.lat[k]) : lat[k] + h.lat[k];
+      for (int k = 0; k < 12; ++k) lat[k] = (k % 2 == 0 && k < 6) ? std::max(lat[k], h.lat[k]) : lat[k] + h.lat[k];
     }
     std::fprintf(stderr,
                  "[wr bvh latency, us] membership max %.1f sum %.1f; ties max %.1f sum %.1f; walks max %.1f sum %.1f; "
                  "long many-leaf scans %llu\n",
                  lat[0] * 0.01, lat[1] * 0.01, lat[2] * 0.01, lat[3] * 0.01, lat[4] * 0.01, lat[5] * 0.01, lat[6]);
     if (lat[7] + lat[8])
-      std::fprintf(stderr, "[wr bvh tie split, us] collect %.1f, first leaves %.1f, second passes %llu\n",
-                   lat[7] * 0.01, lat[8] * 0.01, lat[9]);
+      std::fprintf(stderr,
+                   "[wr bvh tie split, us] collect %.1f, first leaves %.1f, second passes %llu, pair records used %llu; "
+                   "scan membership %.1f\n",
+                   lat[7] * 0.01, lat[8] * 0.01, lat[9], lat[11], lat[10] * 0.01);
     std::fprintf(stderr, "[wr bvh walks] many-leaf %llu, no visited hit %llu, crowd %llu, band %llu\n", why[0], why[1],
                  why[2], why[3]);
     unsigned long long ww[4] = {0, 0, 0, 0};
@@ -1985,6 +1999,10 @@ int wr_create(const wr_scene* sc, int device, wr_context** out) {
                          ? 1
                          : 0;
       if (const char* e = std::getenv("WR_WALK_WAVE")) fs.walk_wave = fs.walk_wave && std::atoi(e) != 0;
+      // near-ties and the search's pair record (kPairWindow): 2 = the pair list
+      // (one per lane), 1 = the record in the tie list only, 0 = neither
+      fs.pair = 2;
+      if (const char* e = std::getenv("WR_PAIR_RECORD")) fs.pair = std::max(0, std::min(2, std::atoi(e)));
       c->fast_ok = true;
       if (const char* e = std::getenv("WR_RESOLVE_LIST")) c->resolve_list = std::atoi(e) != 0;
       int per_cu = 0;
@@ -2116,7 +2134,7 @@ static int trace_api(wr_context* c, const wr_ray* rays, const float* targets, in
     if (c->api_t2) (void)hipFree(c->api_t2);
     c->api_t2 = nullptr;
     c->api_t2_cap = 0;
-    HIPCHK(hipMalloc(&c->api_t2, 4 * nb * sizeof(float)));  // as ensure_t2
+    HIPCHK(hipMalloc(&c->api_t2, 5 * nb * sizeof(float)));  // as ensure_t2
     c->api_t2_cap = nb;
   }
   QueueList ql;
@@ -2300,9 +2318,13 @@ static int render_bdpt_one(wr_context* c, const wr_bdpt_params* prm, int64_t f_l
   for (const auto& pp : plan.per_pipe) most_groups = std::max(most_groups, pp.size());
   struct WideNow {
     wr_context* c;
-    ~WideNow() { c->wide_now = 0; }
+    ~WideNow() {
+      c->wide_now = 0;
+      c->lat_now = false;
+    }
   } wide_guard{c};
-  c->wide_now = (np < fit && most_groups <= 1 && c->fs4_ok && c->lat_wide) ? 4 : 0;
+  c->lat_now = np < fit && most_groups <= 1;
+  c->wide_now = (c->lat_now && c->fs4_ok && c->lat_wide) ? 4 : 0;
   // the buffer sets, queues and shadow-queue bounds below are laid out for `cap`
   // paths: a larger piece would write past them
   for (const auto& pp : plan.per_pipe)
