@@ -138,6 +138,9 @@ __host__ __device__ constexpr size_t search_spill_entries(int depth, int wide) {
 #ifndef WR_TIE_SPLIT
 #define WR_TIE_SPLIT 0  // diagnostic: time the tie resolution's phases (count_work)
 #endif
+#ifndef WR_TIE_PASS2_CAP
+#define WR_TIE_PASS2_CAP 1  // resolve_tie's second collection bounded by m + 3 EPS (0: unbounded)
+#endif
 // the tie resolution's leaf searches: calls (WR_HARD_CALL=__noinline__) or inlined
 #ifndef WR_HARD_CALL
 #define WR_HARD_CALL __forceinline__  // calls: 560-752 B of scratch per lane
@@ -1096,9 +1099,13 @@ __device__ __forceinline__ bool resolve_tie(const DevScene& S, const FastScene& 
   float m = WR_INF;
   int n = 0;
   // first the hits up to t1 + 3 EPS (t1 = the scene's smallest); if t1's
-  // triangle is not visited, the kTie smallest hits without a bound
+  // triangle is not visited, the hits up to m + 3 EPS, m = the smallest
+  // visited hit of that window (WR_TIE_PASS2_CAP): every hit below t1 + 3 EPS
+  // was in it, so no visited hit lies below m and m stays the smallest
+  // visited -- the rule below needs every hit up to m + 3 EPS, no more.  Only
+  // when no hit of the window is visited, the kTie smallest without a bound
   for (int pass = 0; pass < 2; ++pass) {
-    const float cap = pass == 0 ? t1 + 3.f * WR_EPS : WR_INF;
+    const float cap = pass == 0 ? t1 + 3.f * WR_EPS : ((WR_TIE_PASS2_CAP && m < WR_INF) ? m + 3.f * WR_EPS : WR_INF);
 #if WR_TIE_SPLIT
     const uint64_t a0 = wall_clock64();
 #endif
