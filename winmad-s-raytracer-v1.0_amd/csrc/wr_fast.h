@@ -203,8 +203,8 @@ __device__ __forceinline__ bool kd_reaches(const uint2* rec, V3 o, V3 d, V3 inv,
 }
 
 // The KD leaf whose cell holds point p (descent by p's coordinates, three
-// levels per 64-byte record): its path record offset.
-__device__ __forceinline__ int kd_locate(const DevScene& S, const FastScene& F, V3 p) {
+// levels per 64-byte record): its node index.
+__device__ __forceinline__ uint32_t kd_locate_node(const DevScene& S, V3 p) {
   uint32_t node = 0;
   for (;;) {
     const uint4* rp = S.nrec3 + 4 * static_cast<size_t>(node);
@@ -218,7 +218,7 @@ __device__ __forceinline__ int kd_locate(const DevScene& S, const FastScene& F, 
 #pragma unroll
     for (int lev = 0; lev < 3; ++lev) {
       const uint2 w = e[h];
-      if ((w.y & 3u) == 3u) return F.node_path[at];
+      if ((w.y & 3u) == 3u) return at;
       const uint32_t axis = w.y & 3u;
       const float split = __uint_as_float(w.x);
       const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
@@ -317,8 +317,11 @@ __device__ __forceinline__ bool cell_may_be_reached(uint4 h0, uint4 h1, V3 o, V3
 #define WR_RESOLVE_SCAN 0
 #endif
 constexpr int kNotMember = 0, kMember = 1, kScan = 2;
+#ifndef WR_MEMBER_REFS
+#define WR_MEMBER_REFS 0  // 1: kd_member tests the located leaf's references instead of a binary search of p1's leaf list (measured alike)
+#endif
 __device__ __forceinline__ int kd_member(const DevScene& S, const FastScene& F, int lb, int ln, V3 o, V3 d,
-                                         float rtmax, float t_hit, uint32_t& steps) {
+                                         float rtmax, float t_hit, uint32_t& steps, int p1) {
   float tmin, tmax;
   if (!box_hit(S.root_l, S.root_r, o, d, tmin, tmax) || rtmax < tmin) return kNotMember;  // :312-313, :323
   const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
@@ -332,14 +335,34 @@ __device__ __forceinline__ int kd_member(const DevScene& S, const FastScene& F, 
     // descent, then by binary search in the (ascending) list
     for (int side = 0; side < 2; ++side) {
       const float tp = side == 0 ? t_hit * 0.99999f - 1e-4f : t_hit * 1.00001f + 1e-4f;
-      const int want = kd_locate(S, F, o + d * tp);
+      const uint32_t at = kd_locate_node(S, o + d * tp);
+#if WR_MEMBER_REFS
+      // does the located leaf list p1?  Its own references, 8 per round trip
+      // (one for the usual leaf), instead of a binary search of p1's
+      // ascending leaf list (~11 dependent loads for a floor's thousands)
+      const uint4 w = S.nrec[at];
+      const uint32_t first = w.x, cnt = w.y >> 2;
+      bool listed = false;
+      for (uint32_t j0 = 0; j0 < cnt && !listed; j0 += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int code = j0 + u < cnt ? __float_as_int(S.ref_c[first + j0 + u].y) : -1;
+          const int pr = code >= 0 ? code : -code - 1;  // a sphere's ref: -(prim + 1)
+          listed |= j0 + u < cnt && pr == p1;
+        }
+      }
+      const int want = F.node_path[at];
+#else
+      const int want = F.node_path[at];
       int a = lb, b = lb + ln;
       while (a < b) {
         const int mid = (a + b) >> 1;
         if (F.prim_leaf[mid] < want) a = mid + 1;
         else b = mid;
       }
-      if (a < lb + ln && F.prim_leaf[a] == want) {
+      const bool listed = a < lb + ln && F.prim_leaf[a] == want;
+#endif
+      if (listed) {
         const uint2* rec = F.path + want;
         const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
         const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 2);
@@ -1952,7 +1975,7 @@ __device__ __forceinline__ void resolve_fast(const DevScene& S, const FastScene&
             uint32_t steps = 0;
             const uint64_t t0 = COUNT ? wall_clock64() : 0;
             const int lb = F.prim_leaf_off[p1], ln = F.prim_leaf_off[p1 + 1] - lb;
-            const int m = kd_member(S, F, lb, ln, o, d, rtmax, t1, steps);
+            const int m = kd_member(S, F, lb, ln, o, d, rtmax, t1, steps, p1);
             need = m == kNotMember;
             scan = m == kScan;
             if (COUNT) {
