@@ -625,7 +625,9 @@ struct wr_context {
   // 1,182 to 1,328 Mrays/s and keeps 20 (2,766 -> 2,788); every tie one per
   // wave loses at 20 (2,432)
   int tie_wave_max = 4096;
-  int scan_waves = 256;  // k_fast_hard's scan-list waves (WR_SCAN_WAVES)
+  // k_fast_hard's scan-list waves (WR_SCAN_WAVES): 1,024 against 256, five runs each: C4 +1.3 %,
+  // C2 20 it. +0.5 %, C3 and one iteration alike (profiles/r6/scan_waves*.txt)
+  int scan_waves = 1024;
   // host threads issuing a render's launches (env WR_ISSUE_THREADS): the
   // pipelines are dealt out to them, each thread issues its pipelines' steps
   int issue_threads = 1;
